@@ -1,0 +1,922 @@
+// pt_oracle.cpp -- CPU restatement of the reference hw5 render path.
+//
+// TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+// bench.py cpu_baseline leg may load or run this code, and only as the checker
+// (or, for the baseline, as the timed CPU "port").  The product renderer
+// (raytracing-course_amd/) never links, loads or calls anything under oracle/.
+//
+// Parity pinning: this restatement is checked against fixtures generated from
+// the UNMODIFIED reference (oracle/build_ref.sh -> oracle/_ref/*, committed as
+// tests/golden/*): P6 images + fp32 radiance, BVH node/primitive fingerprints,
+// RNG known-answer streams and a traversal KAT.  It is written from the
+// reference's behaviour, function by function; each function cites the
+// reference file:line it follows (paths relative to /root/reference/hw5).
+//
+// Float semantics: compile with -ffp-contract=off (no FMA contraction) on
+// x86-64 SSE2, like the reference's -O3 build.  glm 1.0.0's scalar op order is
+// restated explicitly (glm/detail/func_geometric.inl:48-54 dot, :68-78 cross,
+// :82-89 normalize; glm/detail/type_quat.inl:359-366 quat*vec).
+#include "pt_oracle.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+// ---------------------------------------------------------------- math ----
+struct V3 { float x, y, z; };
+struct Q4 { float x, y, z, w; };  // glm::quat, read as "x y z w" (src/quaternion.cpp:14-17)
+
+inline V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+inline V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline V3 operator*(V3 a, V3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+inline V3 operator/(V3 a, V3 b) { return {a.x / b.x, a.y / b.y, a.z / b.z}; }
+inline V3 operator*(float k, V3 a) { return {k * a.x, k * a.y, k * a.z}; }   // src/point.cpp:20-22
+inline V3 operator*(V3 a, float k) { return {a.x * k, a.y * k, a.z * k}; }   // glm vec*scalar
+inline V3 operator/(V3 a, float k) { return {a.x / k, a.y / k, a.z / k}; }   // glm vec/scalar
+inline float fdot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }  // ((x+y)+z)
+inline V3 fcross(V3 a, V3 b) {
+    return {a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y};
+}
+inline V3 fnormalize(V3 v) { return v * (1.f / std::sqrt(fdot(v, v))); }
+inline float flength(V3 v) { return std::sqrt(fdot(v, v)); }
+inline float fget(V3 v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+inline void fset(V3& v, int a, float f) { if (a == 0) v.x = f; else if (a == 1) v.y = f; else v.z = f; }
+// std::min / std::max exactly (libstdc++ stl_algobase.h): (b<a)?b:a, (a<b)?b:a
+inline float smin(float a, float b) { return (b < a) ? b : a; }
+inline float smax(float a, float b) { return (a < b) ? b : a; }
+
+inline Q4 conj(Q4 q) { return Q4{-q.x, -q.y, -q.z, q.w}; }  // glm/ext/quaternion_common.inl:113-116
+inline V3 qrot(Q4 q, V3 v) {                               // glm/detail/type_quat.inl:359-366
+    const V3 qv{q.x, q.y, q.z};
+    const V3 uv = fcross(qv, v);
+    const V3 uuv = fcross(qv, uv);
+    return v + ((uv * q.w) + uuv) * 2.f;
+}
+
+constexpr float INF = 1e18f;                 // include/bvh.h:9
+const float kPI = (float)std::acos(-1.0);    // include/distributions.h:14
+
+// ------------------------------------------------------------- RNG -------
+// libstdc++ (GCC 11): minstd_rand (random.tcc:116-124), generate_canonical<float,24>
+// (random.tcc:3348-3378), normal_distribution<float> Marsaglia polar with cache
+// (random.tcc:1802-1835).  Bundle mirrors RANDOM_t (include/distributions.h:16-20).
+struct Rng {
+    uint32_t x;
+    float saved;
+    bool saved_ok;
+    explicit Rng(uint32_t seed) : saved(0.f), saved_ok(false) {
+        uint32_t s = seed % 2147483647u;
+        x = (s == 0u) ? 1u : s;
+    }
+    uint32_t next() {
+        x = (uint32_t)(((uint64_t)x * 48271u) % 2147483647u);
+        return x;
+    }
+    float uniform() {
+        const float sum = (float)(next() - 1u);        // (urng() - min) * tmp(=1)
+        float r = sum / 2147483648.0f;                 // tmp *= (long double)(2^31-2) -> 2^31f
+        if (r >= 1.0f) r = std::nextafter(1.0f, 0.0f);
+        return r * 1.0f + 0.0f;                        // uniform_real_distribution a=0,b=1
+    }
+    float normal() {
+        if (saved_ok) { saved_ok = false; return saved * 1.0f + 0.0f; }
+        float x1, y1, r2;
+        do {
+            x1 = (float)(2.0f * uniform() - 1.0);
+            y1 = (float)(2.0f * uniform() - 1.0);
+            r2 = x1 * x1 + y1 * y1;
+        } while (r2 > 1.0 || r2 == 0.0);
+        const float mult = std::sqrt(-2 * std::log(r2) / r2);
+        saved = x1 * mult;
+        saved_ok = true;
+        return y1 * mult * 1.0f + 0.0f;
+    }
+};
+
+// ------------------------------------------------------------- scene -----
+enum PType : uint32_t { P_PLANE = 1, P_BOX = 2, P_ELLIPSOID = 4, P_TRIANGLE = 8 };  // include/primitives.h:13-18
+enum Mat : uint32_t { M_DIFFUSE = 0, M_METALLIC = 1, M_DIELECTRIC = 2 };            // include/materials.h:4-6
+
+struct Prim {                       // include/primitives.h:31-64
+    uint32_t type = 0;              // default ctor leaves it unset; 0 = invalid here
+    V3 col{0.f, 0.f, 0.f}, emission{0.f, 0.f, 0.f};
+    V3 pos{0.f, 0.f, 0.f};
+    Q4 rot{0.f, 0.f, 0.f, 1.f};     // {1.,0.,0.,0.} in glm's (w,x,y,z) constructor order
+    uint32_t mat = M_DIFFUSE;
+    float ior = 0.f;
+    V3 a{0.f, 0.f, 0.f}, b{0.f, 0.f, 0.f}, c{0.f, 0.f, 0.f};  // dop_data, dop_data1, dop_data2
+};
+
+struct Hit { float t; V3 n; bool interior; };
+
+struct Ray { V3 o, d; };
+
+// --- primitive intersection, src/primitives.cpp:55-66 ---
+bool isect_plane(const Ray& r, V3 n, Hit& h) {
+    const float t = -fdot(r.o, n) / fdot(r.d, n);
+    if (t > 1e5) return false;
+    if (t > 0) {
+        if (fdot(r.d, n) >= 0) { h = Hit{t, -1.f * n, true}; return true; }
+        h = Hit{t, n, false};
+        return true;
+    }
+    return false;
+}
+
+// src/primitives.cpp:70-117
+bool isect_box(const Ray& r, V3 s, Hit& h, bool want_normal = true) {
+    const V3 t1xyz = (-1.f * s - r.o) / r.d;
+    const V3 t2xyz = (s - r.o) / r.d;
+    const float t1x = smin(t1xyz.x, t2xyz.x), t2x = smax(t1xyz.x, t2xyz.x);
+    const float t1y = smin(t1xyz.y, t2xyz.y), t2y = smax(t1xyz.y, t2xyz.y);
+    const float t1z = smin(t1xyz.z, t2xyz.z), t2z = smax(t1xyz.z, t2xyz.z);
+    const float t1 = smax(smax(t1x, t1y), t1z);
+    const float t2 = smin(smin(t2x, t2y), t2z);
+    if (t1 > t2) return false;
+    if (t2 < 0) return false;
+    const bool interior = t1 < 0;
+    const float t = interior ? t2 : t1;
+    h.t = t;
+    h.interior = interior;
+    if (!want_normal) return true;
+    const V3 p = r.o + t * r.d;
+    V3 n = p / s;
+    if (interior) n = -1.f * n;
+    // std::max({fabs..}) -> max_element (first largest), fabs via ::fabs(double)
+    const double ax = std::fabs((double)n.x), ay = std::fabs((double)n.y), az = std::fabs((double)n.z);
+    double mx = ax;
+    if (mx < ay) mx = ay;
+    if (mx < az) mx = az;
+    if (ax != mx) n.x = 0;
+    if (ay != mx) n.y = 0;
+    if (az != mx) n.z = 0;
+    h.n = fnormalize(n);
+    return true;
+}
+
+// src/primitives.cpp:120-152
+bool isect_ellipsoid(const Ray& r, V3 rad, Hit& h) {
+    const float a = fdot(r.d / rad, r.d / rad);
+    const float b = 2 * fdot(r.o / rad, r.d / rad);
+    const float c = fdot(r.o / rad, r.o / rad) - 1;
+    const float d = b * b - 4 * a * c;
+    if (d <= 0) return false;
+    float x1 = (float)((-b - std::sqrt((double)d)) / (2 * a));
+    float x2 = (float)((-b + std::sqrt((double)d)) / (2 * a));
+    if (x1 > x2) std::swap(x1, x2);
+    if (x2 < 0) return false;
+    const bool interior = x1 < 0;
+    const float t = interior ? x2 : x1;
+    const V3 p = r.o + t * r.d;
+    V3 n = p / (rad * rad);
+    n = fnormalize(n);
+    if (interior) n = -1.f * n;
+    h = Hit{t, n, interior};
+    return true;
+}
+
+// src/primitives.cpp:155-174 (plane through the LOCAL ORIGIN)
+bool isect_triangle(const Ray& r, V3 a, V3 b, V3 c, Hit& h) {
+    const V3 n = fnormalize(fcross(b - a, c - a));
+    Hit ph;
+    if (!isect_plane(r, n, ph)) return false;
+    const V3 p = r.o + ph.t * r.d;
+    auto good = [](V3 u, V3 v, V3 nn) { return fdot(fcross(u, v), nn) > 0; };
+    if (!good(b - a, p - a, n) || !good(p - a, c - a, n) || !good(c - b, p - b, n)) return false;
+    h = ph;
+    return true;
+}
+
+// src/primitives.cpp:14-52
+bool prim_intersect(const Prim& pr, const Ray& ray, Hit& h) {
+    const Ray lr{ray.o + -1.f * pr.pos, ray.d};
+    const Q4 cq = conj(pr.rot);
+    const Ray rot{qrot(cq, lr.o), qrot(cq, lr.d)};
+    bool ok = false;
+    switch (pr.type) {
+        case P_PLANE: ok = isect_plane(rot, pr.a, h); break;
+        case P_BOX: ok = isect_box(rot, pr.a, h); break;
+        case P_ELLIPSOID: ok = isect_ellipsoid(rot, pr.a, h); break;
+        case P_TRIANGLE: ok = isect_triangle(rot, pr.a, pr.b, pr.c, h); break;
+        default: std::fprintf(stderr, "unexpected primitive type(%u) in intersection\n", pr.type); std::exit(1);
+    }
+    if (ok) h.n = fnormalize(qrot(pr.rot, h.n));
+    return ok;
+}
+
+// ------------------------------------------------------------- BVH -------
+struct AABB { V3 mn{INF, INF, INF}, mx{-INF, -INF, -INF}; };        // src/bvh.cpp:7-10
+inline void extend(AABB& bb, V3 p) {                                  // src/bvh.cpp:29-34
+    bb.mx.x = smax(bb.mx.x, p.x); bb.mn.x = smin(bb.mn.x, p.x);
+    bb.mx.y = smax(bb.mx.y, p.y); bb.mn.y = smin(bb.mn.y, p.y);
+    bb.mx.z = smax(bb.mx.z, p.z); bb.mn.z = smin(bb.mn.z, p.z);
+}
+inline void extend(AABB& bb, const AABB& o) { extend(bb, o.mx); extend(bb, o.mn); }  // :36-39
+inline float calc_s(const AABB& bb) {                                  // :23-27
+    const V3 d = bb.mx - bb.mn;
+    return 2.f * (d.x * d.y + d.x * d.z + d.y * d.z);
+}
+AABB prim_aabb(const Prim& p) {                                       // :41-87
+    V3 omn, omx;
+    switch (p.type) {
+        case P_BOX: case P_ELLIPSOID: omn = -1.f * p.a; omx = p.a; break;
+        case P_TRIANGLE: {
+            // std::min({..}) = min_element (first smallest), std::max({..}) = max_element
+            auto mn3 = [](float u, float v, float w) { float m = u; if (v < m) m = v; if (w < m) m = w; return m; };
+            auto mx3 = [](float u, float v, float w) { float m = u; if (m < v) m = v; if (m < w) m = w; return m; };
+            omn = v3(mn3(p.a.x, p.b.x, p.c.x), mn3(p.a.y, p.b.y, p.c.y), mn3(p.a.z, p.b.z, p.c.z));
+            omx = v3(mx3(p.a.x, p.b.x, p.c.x), mx3(p.a.y, p.b.y, p.c.y), mx3(p.a.z, p.b.z, p.c.z));
+            break;
+        }
+        default: throw std::runtime_error("AABB_T got bad primitive type in constructor");
+    }
+    AABB bb;
+    for (int mask = 0; mask < 8; ++mask) {
+        V3 vtx = omn;
+        for (int i = 0; i < 3; ++i) fset(vtx, i, (mask & (1 << i)) ? fget(omx, i) : fget(omn, i));
+        extend(bb, qrot(p.rot, vtx));
+    }
+    bb.mn = bb.mn + p.pos;
+    bb.mx = bb.mx + p.pos;
+    return bb;
+}
+
+struct Node { AABB bb; uint32_t left, right, first, count; };  // include/bvh.h:28-34
+
+struct BVH {
+    std::vector<Node> nodes;
+    std::vector<float> cut_qual;
+
+    uint32_t build(std::vector<Prim>& P, uint32_t first, uint32_t last) {  // src/bvh.cpp:105-179
+        AABB bb;
+        for (uint32_t i = first; i < last; i++) extend(bb, prim_aabb(P[i]));
+        Node cur{bb, 0xFFFFFFFFu, 0xFFFFFFFFu, first, last - first};
+        const uint32_t cur_pos = (uint32_t)nodes.size();
+        nodes.push_back(cur);
+        if (last - first == 1) return cur_pos;
+        float opt[3] = {INF, INF, INF};
+        uint32_t cuts[3] = {0, 0, 0};
+        for (int axis = 0; axis < 3; ++axis) {
+            std::sort(P.begin() + first, P.begin() + last,
+                      [axis](const Prim& u, const Prim& v) { return fget(u.pos, axis) < fget(v.pos, axis); });
+            AABB pref = prim_aabb(P[first]);
+            for (uint32_t cut = first + 1; cut < last; ++cut) {
+                cut_qual[cut] = calc_s(pref) * (float)(cut - first);
+                extend(pref, prim_aabb(P[cut]));
+            }
+            AABB suf;
+            for (uint32_t cut = last - 1; cut > first; --cut) {
+                extend(suf, prim_aabb(P[cut]));
+                cut_qual[cut] += calc_s(suf) * (float)(last - cut);
+            }
+            for (uint32_t cut = first + 1; cut < last; ++cut)
+                if (cut_qual[cut] < opt[axis]) { opt[axis] = cut_qual[cut]; cuts[axis] = cut; }
+        }
+        float optimum = opt[0];
+        if (opt[1] < optimum) optimum = opt[1];
+        if (opt[2] < optimum) optimum = opt[2];
+        const float without_cut = calc_s(cur.bb) * (float)cur.count;
+        if (optimum >= without_cut) return cur_pos;
+        uint32_t cut = 0;
+        for (int axis = 0; axis < 3; ++axis) {
+            if (optimum == opt[axis]) {
+                std::sort(P.begin() + first, P.begin() + last,
+                          [axis](const Prim& u, const Prim& v) { return fget(u.pos, axis) < fget(v.pos, axis); });
+                cut = cuts[axis];
+                break;
+            }
+        }
+        const uint32_t l = build(P, first, cut);
+        nodes[cur_pos].left = l;
+        const uint32_t r = build(P, cut, last);
+        nodes[cur_pos].right = r;
+        return cur_pos;
+    }
+};
+
+struct Counters {
+    std::atomic<uint64_t> rays{0}, nodes{0}, prim_tests{0}, plane_tests{0};
+};
+
+struct Scene {
+    unsigned W = 0, H = 0, ray_depth = 0, samples = 0;
+    V3 bg{0.f, 0.f, 0.f};
+    V3 cam_pos{0, 0, 0}, cam_up{0, 0, 0}, cam_right{0, 0, 0}, cam_fwd{0, 0, 0};
+    float fov_x = 0.f;
+    std::vector<Prim> prims;
+    BVH bvh;
+    uint32_t n_bvh = 0;
+    std::vector<uint32_t> emitters;  // indices into prims (post-InitScene order)
+    Counters ctr;
+};
+
+// ------------------------------------------------------------- loader ----
+// Restates std::stringstream extraction as used by src/sceneload.cpp: a failed
+// extraction leaves the stream failed (later reads leave values untouched);
+// an empty field stores 0 (libstdc++ __convert_to_v / _M_extract_int).
+struct LineStream {
+    std::string s;
+    size_t pos = 0;
+    bool fail = false;
+    explicit LineStream(std::string line) : s(std::move(line)) {}
+    void skip_ws() { while (pos < s.size() && std::isspace((unsigned char)s[pos])) ++pos; }
+    bool word(std::string& w) {
+        if (fail) return false;
+        skip_ws();
+        if (pos >= s.size()) { fail = true; return false; }
+        const size_t b = pos;
+        while (pos < s.size() && !std::isspace((unsigned char)s[pos])) ++pos;
+        w = s.substr(b, pos - b);
+        return true;
+    }
+    void get(float& v) {
+        if (fail) return;
+        skip_ws();
+        if (pos >= s.size()) { fail = true; return; }
+        // collect [+-]digits[.digits][(e|E)[+-]digits] like num_get::_M_extract_float
+        const size_t b = pos;
+        size_t p = pos;
+        if (p < s.size() && (s[p] == '+' || s[p] == '-')) ++p;
+        bool dig = false;
+        while (p < s.size() && std::isdigit((unsigned char)s[p])) { ++p; dig = true; }
+        if (p < s.size() && s[p] == '.') { ++p; while (p < s.size() && std::isdigit((unsigned char)s[p])) { ++p; dig = true; } }
+        if (dig && p < s.size() && (s[p] == 'e' || s[p] == 'E')) {
+            size_t q = p + 1;
+            if (q < s.size() && (s[q] == '+' || s[q] == '-')) ++q;
+            if (q < s.size() && std::isdigit((unsigned char)s[q])) { while (q < s.size() && std::isdigit((unsigned char)s[q])) ++q; p = q; }
+            else p = q;  // libstdc++ consumes the dangling exponent chars, then fails
+        }
+        pos = p;
+        const std::string tok = s.substr(b, p - b);
+        char* end = nullptr;
+        const float f = std::strtof(tok.c_str(), &end);
+        if (tok.empty() || end != tok.c_str() + tok.size()) { v = 0.f; fail = true; return; }
+        v = f;
+        if (pos >= s.size()) { /* eof reached: next read fails */ }
+    }
+    void get(unsigned& v) {
+        if (fail) return;
+        skip_ws();
+        if (pos >= s.size()) { fail = true; return; }
+        const size_t b = pos;
+        size_t p = pos;
+        bool neg = false;
+        if (p < s.size() && (s[p] == '+' || s[p] == '-')) { neg = s[p] == '-'; ++p; }
+        const size_t d0 = p;
+        unsigned long long acc = 0;
+        bool ovf = false;
+        while (p < s.size() && std::isdigit((unsigned char)s[p])) {
+            acc = acc * 10 + (unsigned)(s[p] - '0');
+            if (acc > 0xFFFFFFFFull) ovf = true;
+            ++p;
+        }
+        pos = p;
+        (void)b;
+        if (p == d0) { v = 0; fail = true; return; }
+        if (ovf) { v = 0xFFFFFFFFu; fail = true; return; }
+        v = neg ? (unsigned)(-(long long)acc) : (unsigned)acc;
+    }
+    void get(V3& p) { get(p.x); get(p.y); get(p.z); }
+    void get(Q4& q) { get(q.x); get(q.y); get(q.z); get(q.w); }
+};
+
+enum Cmd {
+    C_EMPTY, C_DIMENSIONS, C_BG_COLOR, C_CAMERA_POSITION, C_CAMERA_RIGHT, C_CAMERA_UP, C_CAMERA_FORWARD,
+    C_CAMERA_FOV_X, C_NEW_PRIMITIVE, C_PLANE, C_ELLIPSOID, C_BOX, C_POSITION, C_ROTATION, C_COLOR,
+    C_RAY_DEPTH, C_METALLIC, C_DIELECTRIC, C_IOR, C_SAMPLES, C_EMISSION, C_TRIANGLE, C_UNKNOWN
+};
+
+Cmd get_command(const std::string& c) {  // src/sceneload.cpp:8-33
+    if (c.empty()) return C_EMPTY;
+    static const std::pair<const char*, Cmd> tab[] = {
+        {"DIMENSIONS", C_DIMENSIONS}, {"BG_COLOR", C_BG_COLOR}, {"CAMERA_POSITION", C_CAMERA_POSITION},
+        {"CAMERA_RIGHT", C_CAMERA_RIGHT}, {"CAMERA_UP", C_CAMERA_UP}, {"CAMERA_FORWARD", C_CAMERA_FORWARD},
+        {"CAMERA_FOV_X", C_CAMERA_FOV_X}, {"NEW_PRIMITIVE", C_NEW_PRIMITIVE}, {"PLANE", C_PLANE},
+        {"ELLIPSOID", C_ELLIPSOID}, {"BOX", C_BOX}, {"POSITION", C_POSITION}, {"ROTATION", C_ROTATION},
+        {"COLOR", C_COLOR}, {"RAY_DEPTH", C_RAY_DEPTH}, {"METALLIC", C_METALLIC}, {"DIELECTRIC", C_DIELECTRIC},
+        {"IOR", C_IOR}, {"SAMPLES", C_SAMPLES}, {"EMISSION", C_EMISSION}, {"TRIANGLE", C_TRIANGLE}};
+    for (const auto& e : tab) if (c == e.first) return e.second;
+    return C_UNKNOWN;
+}
+
+struct LineReader {  // std::getline on the file: split on '\n'
+    const std::string& text;
+    size_t pos = 0;
+    explicit LineReader(const std::string& t) : text(t) {}
+    bool next(std::string& line) {
+        if (pos >= text.size()) return false;
+        const size_t e = text.find('\n', pos);
+        if (e == std::string::npos) { line = text.substr(pos); pos = text.size(); }
+        else { line = text.substr(pos, e - pos); pos = e + 1; }
+        return true;
+    }
+};
+
+// src/sceneload.cpp:35-110
+std::string load_primitive(LineReader& in, Prim& prim) {
+    std::string line;
+    while (in.next(line)) {
+        LineStream ss(line);
+        std::string name;
+        ss.word(name);
+        const Cmd cmd = get_command(name);
+        if (cmd == C_EMPTY) break;
+        switch (cmd) {
+            case C_ELLIPSOID: { V3 r{0, 0, 0}; ss.get(r); prim = Prim(); prim.type = P_ELLIPSOID; prim.a = r; break; }
+            case C_PLANE: { V3 n{0, 0, 0}; ss.get(n); prim = Prim(); prim.type = P_PLANE; prim.a = n; break; }
+            case C_BOX: { V3 s{0, 0, 0}; ss.get(s); prim = Prim(); prim.type = P_BOX; prim.a = s; break; }
+            case C_TRIANGLE: {
+                V3 a{0, 0, 0}, b{0, 0, 0}, c{0, 0, 0};
+                ss.get(a); ss.get(b); ss.get(c);
+                prim = Prim(); prim.type = P_TRIANGLE; prim.a = a; prim.b = b; prim.c = c;
+                break;
+            }
+            case C_COLOR: ss.get(prim.col); break;
+            case C_POSITION: ss.get(prim.pos); break;
+            case C_ROTATION: ss.get(prim.rot); break;
+            case C_METALLIC: prim.mat = M_METALLIC; break;
+            case C_DIELECTRIC: prim.mat = M_DIELECTRIC; break;
+            case C_IOR: ss.get(prim.ior); break;
+            case C_EMISSION: ss.get(prim.emission); break;
+            default: return name;
+        }
+    }
+    return "";
+}
+
+// src/sceneload.cpp:112-176
+void load_scene(Scene& S, const std::string& text) {
+    LineReader in(text);
+    std::string line;
+    while (in.next(line)) {
+        LineStream ss(line);
+        std::string name;
+        ss.word(name);
+    again:
+        const Cmd cmd = get_command(name);
+        if (cmd == C_EMPTY) continue;
+        switch (cmd) {
+            case C_DIMENSIONS: ss.get(S.W); ss.get(S.H); break;
+            case C_BG_COLOR: ss.get(S.bg); break;
+            case C_CAMERA_POSITION: ss.get(S.cam_pos); break;
+            case C_CAMERA_RIGHT: ss.get(S.cam_right); break;
+            case C_CAMERA_UP: ss.get(S.cam_up); break;
+            case C_CAMERA_FORWARD: ss.get(S.cam_fwd); break;
+            case C_CAMERA_FOV_X: ss.get(S.fov_x); break;
+            case C_NEW_PRIMITIVE: {
+                Prim p;
+                const std::string rest = load_primitive(in, p);
+                S.prims.push_back(p);
+                name = rest;
+                if (!name.empty()) goto again;  // stale `ss` is reused (quirk)
+                break;
+            }
+            case C_RAY_DEPTH: ss.get(S.ray_depth); break;
+            case C_SAMPLES: ss.get(S.samples); break;
+            default: std::fprintf(stderr, "unexpected command(%s)\n", name.c_str()); break;
+        }
+    }
+}
+
+// src/scene.cpp:7-40
+void init_scene(Scene& S) {
+    auto it = std::partition(S.prims.begin(), S.prims.end(), [](const Prim& p) { return p.type != P_PLANE; });
+    S.n_bvh = (uint32_t)(it - S.prims.begin());
+    for (const Prim& p : S.prims)
+        if (p.type != P_PLANE && p.type != P_BOX && p.type != P_ELLIPSOID && p.type != P_TRIANGLE)
+            throw std::runtime_error("bad primitive type");
+    if (S.n_bvh == 0) throw std::runtime_error("scene has no non-plane primitive (reference aborts)");
+    S.bvh.cut_qual.assign(S.n_bvh, 0.f);
+    S.bvh.nodes.reserve(S.n_bvh);
+    S.bvh.build(S.prims, 0, S.n_bvh);
+    S.emitters.clear();
+    for (uint32_t i = 0; i < (uint32_t)S.prims.size(); ++i) {
+        const Prim& p = S.prims[i];
+        if (!(p.emission.x > 0 || p.emission.y > 0 || p.emission.z > 0)) continue;
+        if (p.type == P_BOX || p.type == P_ELLIPSOID) S.emitters.push_back(i);
+    }
+}
+
+// ------------------------------------------------------------- render ----
+struct RHit { Hit h; int id; };
+
+// src/bvh.cpp:89-93
+inline bool aabb_intersect(const AABB& bb, const Ray& r, Hit& h) {
+    const V3 s = 0.5f * (bb.mx - bb.mn);
+    const V3 c = 0.5f * (bb.mx + bb.mn);
+    const Ray lr{r.o + -1.f * c, r.d};
+    return isect_box(lr, s, h, /*want_normal=*/false);
+}
+
+// src/bvh.cpp:185-225 (recursive, left-first)
+RHit bvh_isect(const Scene& S, const Ray& ray, float closest, uint32_t v, uint64_t& nodes, uint64_t& ptests) {
+    const Node& cur = S.bvh.nodes[v];
+    ++nodes;
+    Hit bh;
+    if (!aabb_intersect(cur.bb, ray, bh)) return RHit{Hit{}, -1};
+    if (closest < bh.t && !bh.interior) return RHit{Hit{}, -1};
+    RHit best{Hit{INF, V3{0, 0, 0}, false}, -1};
+    if (cur.left == 0xFFFFFFFFu) {
+        for (uint32_t i = cur.first; i < cur.first + cur.count; ++i) {
+            Hit h;
+            ++ptests;
+            if (prim_intersect(S.prims[i], ray, h) && h.t < best.h.t) best = RHit{h, (int)i};
+        }
+        return best;
+    }
+    const RHit l = bvh_isect(S, ray, closest, cur.left, nodes, ptests);
+    if (l.id != -1 && l.h.t < best.h.t) { closest = l.h.t; best = l; }
+    const RHit r = bvh_isect(S, ray, closest, cur.right, nodes, ptests);
+    if (r.id != -1 && r.h.t < best.h.t) best = r;
+    return best;
+}
+
+// src/scene.cpp:46-77
+RHit ray_intersection(const Scene& S, const Ray& ray, uint64_t* loc) {
+    RHit ret{Hit{}, -1};
+    float closest = INF;
+    for (uint32_t i = S.n_bvh; i < (uint32_t)S.prims.size(); ++i) {  // planes sit after partition
+        Hit h;
+        ++loc[3];
+        if (prim_intersect(S.prims[i], ray, h) && h.t < closest) { closest = h.t; ret = RHit{h, (int)i}; }
+    }
+    const RHit b = bvh_isect(S, ray, closest, 0, loc[1], loc[2]);
+    if (b.id != -1 && b.h.t < closest) ret = b;
+    return ret;
+}
+
+// --- distributions, src/distributions.cpp ---
+V3 normal01_vec(Rng& R) {                              // :102-110
+    const float f1 = R.normal(), f2 = R.normal(), f3 = R.normal();
+    return fnormalize(V3{f1, f2, f3});
+}
+V3 sample_cosine(Rng& R, V3 n) {                      // :144-159
+    V3 dir = normal01_vec(R);
+    dir = dir + n;
+    if (fdot(dir, n) <= 1e-8f) return n;
+    if (flength(dir) <= 1e-4) return n;
+    return fnormalize(dir);
+}
+inline float pdf_cosine(V3 n, V3 d) { return smax(0.f, 1.f / kPI * fdot(d, n)); }  // :161-164
+
+// :170-198
+int points_for_pdf(const Prim& pr, V3 x, V3 d, Hit& h1, Hit& h2) {
+    if (!prim_intersect(pr, Ray{x, d}, h1)) return 0;
+    const float t = h1.t;
+    if (t <= 1e-8) {
+        std::fprintf(stderr, "GetPointsForPdf unexpected intersection t(%g)\n", (double)t);
+        return 0;
+    }
+    const float eps = 1e-4f;
+    const V3 inner = x + (t + eps) * d;
+    if (!prim_intersect(pr, Ray{inner, d}, h2)) return 1;
+    h2.t += t + eps;
+    return 2;
+}
+
+V3 sample_box(Rng& R, const Prim& bx, V3 x) {        // :227-269
+    const V3 s = bx.a;
+    const float wx = s.x * s.x, wy = s.y * s.y, wz = s.z * s.z;
+    for (;;) {
+        float u = R.uniform();
+        const float side = (R.uniform() <= 0.5 ? 1 : -1);
+        u *= wx + wy + wz;
+        float c1 = R.uniform(), c2 = R.uniform(), c3 = R.uniform();
+        c1 = 2 * c1 - 1; c2 = 2 * c2 - 1; c3 = 2 * c3 - 1;
+        V3 pnt{c1 * s.x, c2 * s.y, c3 * s.z};
+        if (u < wx) pnt.x = side * s.x;
+        else if (u < wx + wy) pnt.y = side * s.y;
+        else pnt.z = side * s.z;
+        const V3 on_box = qrot(bx.rot, pnt) + bx.pos;
+        const V3 smp = fnormalize(on_box - x);
+        Hit h;
+        if (prim_intersect(bx, Ray{x, smp}, h)) return smp;
+    }
+}
+float pdf_point_box(const Prim& bx, float dist2, V3 n, V3 d) {  // :271-287
+    const V3 s = bx.a;
+    const float wx = s.x * s.x, wy = s.y * s.y, wz = s.z * s.z;
+    const float p_y = (float)(1. / (2 * 4 * (wx + wy + wz)));
+    return (float)((p_y * dist2) / std::fabs((double)fdot(d, n)));
+}
+float pdf_box(const Prim& bx, V3 x, V3 d) {                        // :289-312
+    Hit h1, h2;
+    const int k = points_for_pdf(bx, x, d, h1, h2);
+    if (k == 0) return 1e-9f;
+    const V3 cp = x + h1.t * d;
+    float sum = pdf_point_box(bx, fdot(x - cp, x - cp), h1.n, d);
+    if (k == 2) {
+        const V3 op = x + h2.t * d;
+        sum += pdf_point_box(bx, fdot(x - op, x - op), h2.n, d);
+    }
+    return sum;
+}
+V3 sample_ellipsoid(Rng& R, const Prim& el, V3 x) {               // :318-338
+    const V3 r = el.a;
+    for (;;) {
+        const V3 k = normal01_vec(R);
+        const V3 pnt = r * k;
+        const V3 on = qrot(el.rot, pnt) + el.pos;
+        const V3 smp = fnormalize(on - x);
+        Hit h;
+        if (prim_intersect(el, Ray{x, smp}, h)) return smp;
+    }
+}
+float pdf_point_ellipsoid(const Prim& el, float dist2, V3 y, V3 n_, V3 d) {  // :340-347
+    const V3 r = el.a;
+    const V3 n = qrot(conj(el.rot), y - el.pos) / r;
+    const float p_y = (float)(1. / (4 * kPI * flength(V3{n.x * r.y * r.z, r.x * n.y * r.z, r.x * r.y * n.z})));
+    return (float)((p_y * dist2) / std::fabs((double)fdot(d, n_)));
+}
+float pdf_ellipsoid(const Prim& el, V3 x, V3 d) {                  // :349-372
+    Hit h1, h2;
+    const int k = points_for_pdf(el, x, d, h1, h2);
+    if (k == 0) return 1e-9f;
+    const V3 cp = x + h1.t * d;
+    float sum = pdf_point_ellipsoid(el, fdot(x - cp, x - cp), cp, h1.n, d);
+    if (k == 2) {
+        const V3 op = x + h2.t * d;
+        sum += pdf_point_ellipsoid(el, fdot(x - op, x - op), op, h2.n, d);
+    }
+    return sum;
+}
+V3 sample_mix(const Scene& S, Rng& R, V3 x, V3 n) {               // :385-399
+    const float flip = R.uniform();
+    if (S.emitters.empty() || flip <= 0.5f) return sample_cosine(R, n);
+    const float fid = R.uniform();
+    const size_t id = (size_t)std::floor(fid * (float)S.emitters.size());
+    const Prim& e = S.prims[S.emitters[id]];
+    return e.type == P_BOX ? sample_box(R, e, x) : sample_ellipsoid(R, e, x);
+}
+float pdf_mix(const Scene& S, V3 x, V3 n, V3 d) {                  // :401-416
+    float sum = pdf_cosine(n, d);
+    if (!S.emitters.empty()) {
+        float ps = 0.f;
+        for (uint32_t ei : S.emitters) {
+            const Prim& e = S.prims[ei];
+            ps += e.type == P_BOX ? pdf_box(e, x, d) : pdf_ellipsoid(e, x, d);
+        }
+        ps *= 1.f / (float)S.emitters.size();
+        sum = 0.5f * sum + 0.5f * ps;
+    }
+    return sum;
+}
+
+inline V3 reflect(V3 n, V3 dir) { return dir - (2.0f * n) * fdot(n, dir); }  // src/scene.cpp:79-81
+
+// src/scene.cpp:83-178 (recursive, like the reference)
+V3 ray_trace(const Scene& S, Rng& R, const Ray& ray, unsigned depth, uint64_t* loc) {
+    if (depth == 0) return V3{0.f, 0.f, 0.f};
+    ++loc[0];
+    const RHit rh = ray_intersection(S, ray, loc);
+    if (rh.id == -1) return S.bg;
+    const float t = rh.h.t;
+    const V3 normal = rh.h.n;
+    const bool interior = rh.h.interior;
+    const Prim& pr = S.prims[(size_t)rh.id];
+    const V3 p = ray.o + t * ray.d;
+    const float eps = 1e-4f;
+    V3 other{0.f, 0.f, 0.f};
+    switch (pr.mat) {
+        case M_DIFFUSE: {
+            const V3 p_outer = p + eps * normal;
+            const V3 dir = sample_mix(S, R, p_outer, normal);
+            if (fdot(dir, normal) <= 0) break;
+            const float pw = pdf_mix(S, p_outer, normal, dir);
+            const V3 L = ray_trace(S, R, Ray{p + eps * dir, dir}, depth - 1, loc);
+            other = (pr.col / kPI) * L * fdot(dir, normal) * (1 / pw);
+            break;
+        }
+        case M_METALLIC: {
+            const V3 rd = reflect(normal, fnormalize(ray.d));
+            const V3 L = ray_trace(S, R, Ray{p + eps * rd, rd}, depth - 1, loc);
+            other = pr.col * L;
+            break;
+        }
+        case M_DIELECTRIC: {
+            float eta1 = 1.f, eta2 = pr.ior;
+            if (interior) std::swap(eta1, eta2);
+            const V3 dir = -1.f * fnormalize(ray.d);
+            const float cosn = fdot(normal, dir);
+            const float sin2 = (float)((double)(eta1 / eta2) * std::sqrt((double)smax(0.f, 1 - cosn * cosn)));
+            if (std::fabs((double)sin2) > 1.) {
+                const V3 rd = reflect(normal, fnormalize(ray.d));
+                other = ray_trace(S, R, Ray{p + eps * rd, rd}, depth - 1, loc);
+                break;
+            }
+            const float r0 = (float)std::pow((double)((eta1 - eta2) / (eta1 + eta2)), 2.);
+            const float rr = (float)((double)r0 + (double)(1 - r0) * std::pow((double)(1 - cosn), 5.));
+            if (R.uniform() < rr) {
+                const V3 rd = reflect(normal, fnormalize(ray.d));
+                other = ray_trace(S, R, Ray{p + eps * rd, rd}, depth - 1, loc);
+                break;
+            }
+            const float cos2 = (float)std::sqrt((double)(1 - sin2 * sin2));
+            const V3 rd = (eta1 / eta2) * (-1.f * dir) + (eta1 / eta2 * cosn - cos2) * normal;
+            V3 L = ray_trace(S, R, Ray{p + eps * rd, rd}, depth - 1, loc);
+            if (!interior) L = pr.col * L;
+            other = L;
+            break;
+        }
+        default: std::fprintf(stderr, "unknown material: primitive id(%d)\n", rh.id); break;
+    }
+    return pr.emission + other;
+}
+
+struct Cam { float tx, ty; };
+Cam camera_tans(const Scene& S) {                      // src/scene.cpp:181-182
+    Cam c;
+    c.tx = (float)std::tan((double)(S.fov_x / 2));
+    c.ty = c.tx * (float)S.H / (float)S.W;
+    return c;
+}
+Ray get_to_ray(const Scene& S, const Cam& c, float x, float y) {  // src/scene.cpp:180-187
+    const float nx = (2 * x / (float)S.W - 1) * c.tx;
+    const float ny = -1.f * (2 * y / (float)S.H - 1) * c.ty;
+    return Ray{S.cam_pos, nx * S.cam_right + ny * S.cam_up + 1.f * S.cam_fwd};
+}
+
+// src/scene.cpp:189-203
+V3 sample_pixel(const Scene& S, const Cam& c, Rng& R, unsigned x, unsigned y, unsigned spp, uint64_t* loc) {
+    V3 sum{0.f, 0.f, 0.f};
+    for (unsigned i = 0; i < spp; ++i) {
+        const float fx = (float)x + R.uniform();
+        const float fy = (float)y + R.uniform();
+        sum = sum + ray_trace(S, R, get_to_ray(S, c, fx, fy), S.ray_depth, loc);
+    }
+    return (1.f / (float)spp) * sum;
+}
+
+// src/color.cpp:19-49
+inline float saturate1(float v) { return smax(smin(1.f, v), 0.f); }
+void tonemap(V3 c, uint8_t out[3]) {
+    const float a = 2.51f, b = 0.03f, cc = 2.43f, d = 0.59f, e = 0.14f;
+    const V3 x = c;
+    const V3 num = x * (a * x + V3{b, b, b});
+    const V3 den = x * (cc * x + V3{d, d, d}) + V3{e, e, e};
+    const V3 s = num / den;
+    const float g = (float)(1. / 2.2);
+    const float r = std::pow(saturate1(s.x), g), gg = std::pow(saturate1(s.y), g), bb = std::pow(saturate1(s.z), g);
+    out[0] = (uint8_t)std::round(255 * r);
+    out[1] = (uint8_t)std::round(255 * gg);
+    out[2] = (uint8_t)std::round(255 * bb);
+}
+
+}  // namespace
+
+// ================================================================ C API ===
+struct oracle_scene { Scene s; };
+
+extern "C" {
+
+oracle_scene* oracle_load(const char* path) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return nullptr;
+    std::stringstream buf;
+    buf << f.rdbuf();
+    auto* o = new oracle_scene();
+    try {
+        load_scene(o->s, buf.str());
+        init_scene(o->s);
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "oracle_load: %s\n", e.what());
+        delete o;
+        return nullptr;
+    }
+    return o;
+}
+
+void oracle_free(oracle_scene* o) { delete o; }
+
+int oracle_info(const oracle_scene* o, uint32_t* out8) {
+    const Scene& S = o->s;
+    out8[0] = S.W; out8[1] = S.H; out8[2] = S.samples; out8[3] = S.ray_depth;
+    out8[4] = (uint32_t)S.prims.size(); out8[5] = S.n_bvh; out8[6] = (uint32_t)S.bvh.nodes.size();
+    out8[7] = (uint32_t)S.emitters.size();
+    return 0;
+}
+
+// node array: per node 6 f32 + 4 u32 (40 B); prims: u32 type + 12 f32 (52 B)
+int oracle_dump_bvh(const oracle_scene* o, void* nodes_out, void* prims_out) {
+    const Scene& S = o->s;
+    auto* nb = static_cast<unsigned char*>(nodes_out);
+    for (const Node& n : S.bvh.nodes) {
+        const float f[6] = {n.bb.mn.x, n.bb.mn.y, n.bb.mn.z, n.bb.mx.x, n.bb.mx.y, n.bb.mx.z};
+        const uint32_t u[4] = {n.left, n.right, n.first, n.count};
+        std::memcpy(nb, f, 24); std::memcpy(nb + 24, u, 16); nb += 40;
+    }
+    auto* pb = static_cast<unsigned char*>(prims_out);
+    for (const Prim& p : S.prims) {
+        const bool tri = p.type == P_TRIANGLE;
+        const float f[12] = {p.a.x, p.a.y, p.a.z, tri ? p.b.x : 0.f, tri ? p.b.y : 0.f, tri ? p.b.z : 0.f,
+                             tri ? p.c.x : 0.f, tri ? p.c.y : 0.f, tri ? p.c.z : 0.f, p.pos.x, p.pos.y, p.pos.z};
+        std::memcpy(pb, &p.type, 4); std::memcpy(pb + 4, f, 48); pb += 52;
+    }
+    return 0;
+}
+
+// Render window [x0,x0+w) x [y0,y0+h) with spp samples (0 = scene's SAMPLES).
+// rgb: w*h*3 u8 (may be NULL), rad: w*h*3 f32 mean radiance (may be NULL),
+// counters[4] (may be NULL): rays, node visits, leaf primitive tests, plane tests.
+int oracle_render(oracle_scene* o, uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, uint32_t spp,
+                  int nthreads, uint8_t* rgb, float* rad, uint64_t* counters) {
+    const Scene& S = o->s;
+    if (spp == 0) spp = S.samples;
+    const Cam cam = camera_tans(S);
+    const uint64_t total = (uint64_t)w * h;
+    std::atomic<uint64_t> next{0};
+    std::atomic<uint64_t> c_rays{0}, c_nodes{0}, c_pt{0}, c_pl{0};
+    if (nthreads <= 0) nthreads = (int)std::thread::hardware_concurrency();
+    if (nthreads <= 0) nthreads = 1;
+    auto worker = [&]() {
+        uint64_t loc[4] = {0, 0, 0, 0};
+        for (;;) {
+            const uint64_t k0 = next.fetch_add(64);
+            if (k0 >= total) break;
+            const uint64_t k1 = std::min<uint64_t>(total, k0 + 64);
+            for (uint64_t k = k0; k < k1; ++k) {
+                const uint32_t x = x0 + (uint32_t)(k % w), y = y0 + (uint32_t)(k / w);
+                Rng R(y * S.W + x);  // src/scene.cpp:216: minstd_rand rnd(i), i = y*W + x
+                const V3 c = sample_pixel(S, cam, R, x, y, spp, loc);
+                if (rad) { rad[k * 3] = c.x; rad[k * 3 + 1] = c.y; rad[k * 3 + 2] = c.z; }
+                if (rgb) tonemap(c, rgb + k * 3);
+            }
+        }
+        c_rays += loc[0]; c_nodes += loc[1]; c_pt += loc[2]; c_pl += loc[3];
+    };
+    std::vector<std::thread> th;
+    for (int i = 1; i < nthreads; ++i) th.emplace_back(worker);
+    worker();
+    for (auto& t : th) t.join();
+    if (counters) { counters[0] = c_rays; counters[1] = c_nodes; counters[2] = c_pt; counters[3] = c_pl; }
+    return 0;
+}
+
+// Closest-hit KAT: rays[n*6] (o,d) -> ids[n] (-1 miss), hit[n*5] (t, nx,ny,nz, interior)
+int oracle_ray_intersection(const oracle_scene* o, uint32_t n, const float* rays, int32_t* ids, float* hit) {
+    const Scene& S = o->s;
+    uint64_t loc[4] = {0, 0, 0, 0};
+    for (uint32_t i = 0; i < n; ++i) {
+        const Ray r{V3{rays[i * 6], rays[i * 6 + 1], rays[i * 6 + 2]}, V3{rays[i * 6 + 3], rays[i * 6 + 4], rays[i * 6 + 5]}};
+        const RHit h = ray_intersection(S, r, loc);
+        ids[i] = h.id;
+        const bool ok = h.id != -1;
+        hit[i * 5] = ok ? h.h.t : 0.f;
+        hit[i * 5 + 1] = ok ? h.h.n.x : 0.f; hit[i * 5 + 2] = ok ? h.h.n.y : 0.f; hit[i * 5 + 3] = ok ? h.h.n.z : 0.f;
+        hit[i * 5 + 4] = ok ? (h.h.interior ? 1.f : 0.f) : 0.f;
+    }
+    return 0;
+}
+
+// RNG KAT: n uniforms, n normals (fresh engine), n mixed (fresh), as ref_harness "rng"
+int oracle_rng(uint32_t seed, uint32_t n, float* out) {
+    { Rng R(seed); for (uint32_t k = 0; k < n; ++k) out[k] = R.uniform(); }
+    { Rng R(seed); for (uint32_t k = 0; k < n; ++k) out[n + k] = R.normal(); }
+    {
+        Rng R(seed);
+        for (uint32_t k = 0; k < n; ++k) {
+            const bool use_u = ((k * 2654435761u) >> 7) & 1u;
+            out[2 * n + k] = use_u ? R.uniform() : R.normal();
+        }
+    }
+    return 0;
+}
+
+void oracle_tonemap(uint32_t n, const float* rad, uint8_t* rgb) {
+    for (uint32_t i = 0; i < n; ++i) tonemap(V3{rad[i * 3], rad[i * 3 + 1], rad[i * 3 + 2]}, rgb + i * 3);
+}
+
+}  // extern "C"
+
+#ifdef ORACLE_MAIN
+// CLI mirroring hw5/src/main.cpp:6-17: pt_oracle <scene.txt> <out.ppm> [threads]
+int main(int argc, char** argv) {
+    if (argc < 3) { std::fprintf(stderr, "usage: pt_oracle scene.txt out.ppm [threads]\n"); return 2; }
+    oracle_scene* o = oracle_load(argv[1]);
+    if (!o) return 1;
+    const int nt = argc > 3 ? std::atoi(argv[3]) : 0;
+    const Scene& S = o->s;
+    std::vector<uint8_t> rgb((size_t)S.W * S.H * 3);
+    uint64_t ctr[4];
+    oracle_render(o, 0, 0, S.W, S.H, 0, nt, rgb.data(), nullptr, ctr);
+    std::ofstream out(argv[2], std::ios::binary);
+    out << "P6\n" << S.W << " " << S.H << "\n" << 255 << "\n";
+    out.write(reinterpret_cast<const char*>(rgb.data()), (std::streamsize)rgb.size());
+    std::fprintf(stderr, "rays=%llu nodes=%llu prim_tests=%llu plane_tests=%llu\n", (unsigned long long)ctr[0],
+                 (unsigned long long)ctr[1], (unsigned long long)ctr[2], (unsigned long long)ctr[3]);
+    oracle_free(o);
+    return 0;
+}
+#endif
