@@ -1,0 +1,168 @@
+/* pt.h -- C ABI of the MI355X-native hw5 path tracer (libpt.so).
+ *
+ * Drop-in boundary for the reference's render path.  The reference
+ * (FeggieBoss/raytracing-course, hw5) has no plugin/FFI seam: its callers are
+ * the CLI (hw5/run.sh:1-2 -> hw5/src/main.cpp:6-17) and the in-process trio
+ *     Scene::Load(std::istream&)   hw5/include/scene.h:76, src/sceneload.cpp:112-176
+ *     Scene::InitScene()           hw5/include/scene.h:78, src/scene.cpp:7-40
+ *     Scene::Render(std::ostream&) hw5/include/scene.h:79, src/scene.cpp:205-252
+ * Each entry point below names the reference interface it replaces.  Plain
+ * pointers and sizes only; no C++/torch types cross this boundary.
+ *
+ * Conventions: functions return PT_OK (0) or a negative PT_E* code; the
+ * message of the last failure on the calling thread is pt_last_error().
+ * The caller owns every output buffer; the library owns scenes, sessions and
+ * all device memory (released by pt_scene_free / pt_session_free).
+ * Rendering requires a gfx950 GPU: there is no CPU fallback (PT_E_NO_GPU).
+ */
+#ifndef PT_H
+#define PT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_ABI_VERSION 1
+
+enum {
+    PT_OK = 0,
+    PT_E_INVALID = -1,   /* bad argument / state */
+    PT_E_IO = -2,        /* file cannot be read / written */
+    PT_E_SCENE = -3,     /* scene the reference cannot render either (no non-plane
+                            primitive, bad primitive type, zero sizes) */
+    PT_E_NO_GPU = -4,    /* no usable gfx950 device */
+    PT_E_HIP = -5,       /* HIP runtime error */
+    PT_E_RCCL = -6,      /* RCCL error (multi-GPU gather) */
+    PT_E_OOM = -7
+};
+
+typedef struct pt_scene pt_scene;
+typedef struct pt_session pt_session;
+
+/* Scene::Load: parse a hw5 scene text file with the reference's exact grammar
+ * and quirks.  Unknown commands produce a warning on stderr like
+ * the reference (src/sceneload.cpp:170-172). */
+int pt_scene_load(const char* path, pt_scene** out);
+/* same, from memory (text, len bytes) */
+int pt_scene_load_mem(const char* text, size_t len, pt_scene** out);
+
+/* Scene::InitScene: std::partition of planes to the end, the reference BVH
+ * (bit-faithful: same node boxes, preorder and primitive order), the emitter
+ * list, and the device-side layouts.  Host-only; no GPU needed. */
+int pt_scene_prepare(pt_scene* s);
+
+typedef struct pt_scene_info {
+    uint32_t width, height, samples, ray_depth;
+    uint32_t n_prims, n_bvh_prims, n_planes, n_emitters;
+    uint32_t n_nodes, tree_depth, max_stack;   /* max_stack = max pending right children */
+    uint32_t n_warnings;
+} pt_scene_info;
+int pt_scene_get_info(const pt_scene* s, pt_scene_info* info);
+
+/* Override DIMENSIONS / SAMPLES / RAY_DEPTH after loading (0 keeps the value). */
+int pt_scene_override(pt_scene* s, uint32_t width, uint32_t height, uint32_t samples, uint32_t ray_depth);
+
+/* BVH fingerprint dump (after prepare), reference layout of SURVEY §8c:
+ * nodes: per node 6 f32 (min.xyz, max.xyz) + 4 u32 (left, right, first, count) = 40 B;
+ * prims: per primitive u32 type + 9 f32 (a, b, c; b/c zero unless TRIANGLE) + 3 f32 pos = 52 B. */
+int pt_scene_dump_bvh(const pt_scene* s, void* nodes_out, size_t nodes_bytes, void* prims_out, size_t prims_bytes);
+
+void pt_scene_free(pt_scene* s);
+
+/* ---------------------------------------------------------------- render */
+enum { PT_TRAVERSAL_EXACT = 0 /* reference-tree stack DFS, exact pruning semantics */ };
+
+typedef struct pt_render_opts {
+    int32_t device;          /* first HIP device (default 0) */
+    int32_t ngpu;            /* GPUs driven by this process (default 1); >1 = pixel tiles
+                                dealt round-robin + RCCL gather of the framebuffer */
+    uint32_t spp_per_launch; /* samples per kernel launch (0 = auto) */
+    uint32_t samples;        /* 0 = the scene's SAMPLES */
+    int32_t traversal;       /* PT_TRAVERSAL_* */
+    int32_t progress;        /* 1 = print the reference's "Loading: [...]" bar to stdout */
+    uint32_t win_x0, win_y0; /* optional window: render only [x0,x0+w) x [y0,y0+h) of the */
+    uint32_t win_w, win_h;   /* image, keeping global-index seeds (win_w = 0: full image) */
+} pt_render_opts;
+void pt_render_opts_default(pt_render_opts* o);
+
+typedef struct pt_stats {
+    uint64_t rays;           /* closest-hit queries (Scene::RayIntersection calls) */
+    uint64_t node_visits;    /* BVH node records fetched */
+    uint64_t prim_tests;     /* leaf primitive tests */
+    uint64_t plane_tests;
+    uint64_t samples;        /* pixel samples traced */
+    uint64_t errors;         /* exactness guards tripped (must be 0) */
+    double kernel_ms;        /* sum of trace-kernel time (HIP events) */
+    double resolve_ms;
+    double wall_ms;          /* pt_render: upload + render + gather + tonemap */
+    uint64_t node_bytes;     /* bytes of one node record / primitive record */
+    uint64_t prim_bytes;
+} pt_stats;
+
+/* Scene::Render minus the stream write: renders W*H*3 u8 (row-major, top row
+ * first, exactly the reference's P6 payload) into rgb, and optionally the
+ * pre-tonemap fp32 mean radiance (W*H*3) into radiance.  Either may be NULL.
+ * With a window, the outputs are win_w*win_h*3 (the same pixels as a full
+ * render would give there).  stats may be NULL. */
+int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radiance, pt_stats* stats);
+
+/* P6 writer of src/scene.cpp:206-208,243-251 ("P6\n{W} {H}\n255\n" + payload). */
+int pt_write_ppm(const char* path, uint32_t width, uint32_t height, const uint8_t* rgb);
+
+/* ------------------------------------------------------- sessions (tiles)
+ * Progressive / sharded rendering on ONE device, used by pt_render and by
+ * multi-process drivers (one process per GPU): the image is cut into 16x16
+ * tiles, tile t belongs to rank t % world; the session keeps every owned
+ * pixel's RNG stream and f32 sum resident in HBM, so pt_session_trace(spp)
+ * continues each pixel's stream exactly as the reference's sequential spp loop. */
+typedef struct pt_session_opts {
+    int32_t device;
+    uint32_t rank, world;
+    int32_t traversal;
+    uint32_t win_x0, win_y0, win_w, win_h;   /* optional window (win_w = 0: full image) */
+} pt_session_opts;
+
+int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out);
+/* number of owned tiles and of packed output bytes (tiles*256*3) */
+int pt_session_layout(const pt_session* ss, uint32_t* n_tiles, uint64_t* packed_rgb_bytes);
+/* enqueue spp more samples for every owned pixel (asynchronous) */
+int pt_session_trace(pt_session* ss, uint32_t spp);
+/* tonemap the current means (sum / samples so far) into the packed tile
+ * buffer: 256*3 u8 per owned tile, pixels of a tile row-major; dev_out is a
+ * device pointer on the session's device (NULL = internal buffer).
+ * dev_radiance (optional, device) receives 256*3 f32 per tile. */
+int pt_session_resolve(pt_session* ss, uint8_t* dev_out, float* dev_radiance);
+int pt_session_sync(pt_session* ss);
+/* copy the internal packed buffer to host memory (after resolve+sync) */
+int pt_session_read_packed(pt_session* ss, uint8_t* host_out, size_t bytes);
+/* scatter packed tiles of `rank` (world ranks) into a width*height*3 image
+ * (width/height = the rendered window's size) */
+int pt_unpack_tiles(uint32_t width, uint32_t height, uint32_t rank, uint32_t world, const uint8_t* packed,
+                    uint8_t* rgb);
+int pt_unpack_tiles_f32(uint32_t width, uint32_t height, uint32_t rank, uint32_t world, const float* packed,
+                        float* rad);
+/* counters accumulated by this session (after sync) */
+int pt_session_stats(pt_session* ss, pt_stats* st);
+/* HIP stream of the session (hipStream_t), for callers that order their own work after it */
+void* pt_session_stream(pt_session* ss);
+void pt_session_free(pt_session* ss);
+
+const char* pt_last_error(void);
+int pt_abi_version(void);
+
+/* ------------------------------------------------------------ test hooks
+ * Host execution of the device traversal code (pt_trace.h) for CPU unit
+ * tests of the stack-DFS logic.  Never used by pt_render. */
+int pt_selftest_ray_intersection(pt_scene* s, uint32_t n, const float* rays, int32_t* ids, float* hits);
+int pt_selftest_render_host(pt_scene* s, uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, uint32_t spp,
+                            float* radiance);
+/* the 256-entry gamma threshold table used by the device tonemap */
+int pt_selftest_gamma_table(const pt_scene* s, float* thr256);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PT_H */

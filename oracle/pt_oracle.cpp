@@ -898,6 +898,40 @@ void oracle_tonemap(uint32_t n, const float* rad, uint8_t* rgb) {
     for (uint32_t i = 0; i < n; ++i) tonemap(V3{rad[i * 3], rad[i * 3 + 1], rad[i * 3 + 2]}, rgb + i * 3);
 }
 
+// 8-bit gamma quantiser of src/color.cpp:37-48 alone: round(255 * powf(v, (float)(1./2.2)))
+void oracle_gamma_u8(uint32_t n, const float* v, uint8_t* out) {
+    const float g = (float)(1. / 2.2);
+    for (uint32_t i = 0; i < n; ++i) out[i] = (uint8_t)std::round(255 * std::pow(v[i], g));
+}
+
+// Exhaustive check of a 256-entry threshold table (count of thresholds <= v)
+// against the quantiser over EVERY float in [0, 1]; returns the mismatches.
+uint64_t oracle_check_gamma_table(const float* thr) {
+    const float g = (float)(1. / 2.2);
+    std::atomic<uint64_t> bad{0};
+    const uint32_t end = 0x3f800000u;
+    const int nt = std::max(1, (int)std::thread::hardware_concurrency());
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) {
+        th.emplace_back([&, t]() {
+            uint64_t b = 0;
+            const uint32_t lo = (uint32_t)((uint64_t)(end + 1) * t / nt), hi = (uint32_t)((uint64_t)(end + 1) * (t + 1) / nt);
+            uint32_t k = 0;
+            for (uint32_t u = lo; u < hi; ++u) {
+                float v;
+                std::memcpy(&v, &u, 4);
+                const int ref = (int)std::round(255 * std::pow(v, g));
+                if (u == lo) { k = 0; while (k < 255 && thr[k] <= v) ++k; }
+                else while (k < 255 && thr[k] <= v) ++k;
+                if ((int)k != ref) ++b;
+            }
+            bad += b;
+        });
+    }
+    for (auto& x : th) x.join();
+    return bad;
+}
+
 }  // extern "C"
 
 #ifdef ORACLE_MAIN

@@ -17,6 +17,8 @@ int oracle_render(oracle_scene* o, uint32_t x0, uint32_t y0, uint32_t w, uint32_
 int oracle_ray_intersection(const oracle_scene* o, uint32_t n, const float* rays, int32_t* ids, float* hit);
 int oracle_rng(uint32_t seed, uint32_t n, float* out);
 void oracle_tonemap(uint32_t n, const float* rad, uint8_t* rgb);
+void oracle_gamma_u8(uint32_t n, const float* v, uint8_t* out);
+uint64_t oracle_check_gamma_table(const float* thr);
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,59 @@
+// pt_render -- drop-in for the reference CLI (hw5/src/main.cpp:6-17, hw5/run.sh:1-2):
+//     pt_render <scene.txt> <out.ppm>
+// Load -> InitScene -> Render -> P6 file, on the GPU(s).  Optional environment:
+//     PT_NGPU=<n>     GPUs driven by this process (pixel tiles, default 1)
+//     PT_DEVICE=<i>   first device (default 0)
+//     PT_SPP_LAUNCH=<k> samples per kernel launch (default auto)
+//     PT_QUIET=1      no progress bar
+//     PT_STATS=1      print rays / Mray/s / timings to stderr
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <vector>
+
+#include "pt.h"
+
+static int env_int(const char* k, int def) {
+    const char* v = getenv(k);
+    return v && *v ? atoi(v) : def;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 3) {
+        fprintf(stderr, "usage: %s <scene.txt> <out.ppm>\n", argv[0]);
+        return 2;
+    }
+    pt_scene* s = nullptr;
+    if (pt_scene_load(argv[1], &s) != PT_OK || pt_scene_prepare(s) != PT_OK) {
+        fprintf(stderr, "pt_render: %s\n", pt_last_error());
+        pt_scene_free(s);
+        return 1;
+    }
+    pt_scene_info info;
+    pt_scene_get_info(s, &info);
+    pt_render_opts o;
+    pt_render_opts_default(&o);
+    o.ngpu = env_int("PT_NGPU", 1);
+    o.device = env_int("PT_DEVICE", 0);
+    o.spp_per_launch = (uint32_t)env_int("PT_SPP_LAUNCH", 0);
+    o.progress = env_int("PT_QUIET", 0) ? 0 : 1;
+    std::vector<uint8_t> rgb((size_t)info.width * info.height * 3);
+    pt_stats st;
+    if (pt_render(s, &o, rgb.data(), nullptr, &st) != PT_OK) {
+        fprintf(stderr, "pt_render: %s\n", pt_last_error());
+        pt_scene_free(s);
+        return 1;
+    }
+    if (pt_write_ppm(argv[2], info.width, info.height, rgb.data()) != PT_OK) {
+        fprintf(stderr, "pt_render: %s\n", pt_last_error());
+        pt_scene_free(s);
+        return 1;
+    }
+    if (env_int("PT_STATS", 0)) {
+        fprintf(stderr, "rays=%llu samples=%llu kernel_ms=%.3f wall_ms=%.3f Mray/s=%.3f\n",
+                (unsigned long long)st.rays, (unsigned long long)st.samples, st.kernel_ms, st.wall_ms,
+                st.kernel_ms > 0 ? st.rays / (st.kernel_ms * 1e3) : 0.0);
+    }
+    pt_scene_free(s);
+    return 0;
+}

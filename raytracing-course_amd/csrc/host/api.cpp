@@ -1,0 +1,765 @@
+// api.cpp -- C ABI of libpt (include/pt.h): scene lifecycle (Scene::Load /
+// InitScene equivalents), device residency, tile sessions and the render
+// driver (Scene::Render equivalent).  Host C++; kernels live in
+// ../device/pt_kernels.hip.
+#include "pt.h"
+
+#include <hip/hip_runtime_api.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <fstream>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../device/pt_kernels.h"
+#include "pt_scene.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                                 \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess)                                                                         \
+            return fail(PT_E_HIP, std::string(#expr " failed: ") + hipGetErrorString(e_));            \
+    } while (0)
+
+struct DevScene {
+    pt::Node* nodes = nullptr;
+    pt::Prim* prims = nullptr;
+    pt::Shade* shade = nullptr;
+    uint32_t* planes = nullptr;
+    uint32_t* emitters = nullptr;
+    float* thr = nullptr;
+};
+
+}  // namespace
+
+struct pt_scene {
+    pth::HScene hs;
+    bool prepared = false;
+    std::vector<pth::HNode> nodes;
+    uint32_t n_bvh = 0;
+    std::vector<uint32_t> planes, emitters;
+    std::vector<pt::Node> dnodes;
+    std::vector<pt::Prim> dprims;
+    std::vector<pt::Shade> dshade;
+    uint32_t tree_depth = 0, max_stack = 0;
+    float thr[256];
+    std::map<int, DevScene> dev;
+    std::mutex mu;
+};
+
+struct pt_session {
+    pt_scene* sc = nullptr;
+    int dev = 0;
+    pt::TileMap tm{};
+    uint32_t n_tiles_local = 0, n_slots = 0, depth = 0;
+    pt::PixelState st{};
+    uint32_t* vscratch = nullptr;
+    unsigned long long* counters = nullptr;
+    uint8_t* out = nullptr;
+    float* rad = nullptr;
+    hipStream_t stream = nullptr;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    double kernel_ms = 0.0, resolve_ms = 0.0;
+    uint64_t samples_done = 0;
+    pt::CamView cam{};
+    int traversal = PT_TRAVERSAL_EXACT;
+};
+
+namespace {
+
+// ------------------------------------------------------------- prepare ---
+void build_device_layout(pt_scene* s) {
+    const auto& P = s->hs.prims;
+    s->dnodes.resize(s->nodes.size());
+    for (size_t i = 0; i < s->nodes.size(); ++i) {
+        const pth::HNode& n = s->nodes[i];
+        // AABB_t::Intersect (src/bvh.cpp:90-91): s = 0.5f*(max-min), center = 0.5f*(max+min)
+        float c[3], h[3];
+        for (int a = 0; a < 3; ++a) {
+            h[a] = 0.5f * (n.mx[a] - n.mn[a]);
+            c[a] = 0.5f * (n.mx[a] + n.mn[a]);
+        }
+        const bool leaf = n.left == 0xFFFFFFFFu;
+        if (!leaf && n.left != (uint32_t)i + 1u) throw std::runtime_error("BVH not in preorder");
+        const uint32_t ref = leaf ? n.first : n.right;
+        const uint32_t cnt = leaf ? n.count : 0u;
+        if (leaf && cnt == 0u) throw std::runtime_error("empty BVH leaf");
+        pt::Node d;
+        d.a = pt::F4{c[0], c[1], c[2], h[0]};
+        d.b = pt::F4{h[1], h[2], pt::u2f(ref), pt::u2f(cnt)};
+        s->dnodes[i] = d;
+    }
+    s->dprims.resize(P.size());
+    s->dshade.resize(P.size());
+    for (size_t i = 0; i < P.size(); ++i) {
+        const pth::HPrim& p = P[i];
+        pt::Prim d;
+        d.p0 = pt::F4{p.pos[0], p.pos[1], p.pos[2], pt::u2f(p.type)};
+        d.p1 = pt::F4{p.rot[0], p.rot[1], p.rot[2], p.rot[3]};
+        d.p2 = pt::F4{p.a[0], p.a[1], p.a[2], 0.f};
+        d.p3 = pt::F4{p.b[0], p.b[1], p.b[2], p.c[0]};
+        d.p4 = pt::F4{p.c[1], p.c[2], 0.f, 0.f};
+        s->dprims[i] = d;
+        pt::Shade sh;
+        sh.s0 = pt::F4{p.col[0], p.col[1], p.col[2], p.ior};
+        sh.s1 = pt::F4{p.emis[0], p.emis[1], p.emis[2], pt::u2f(p.mat)};
+        s->dshade[i] = sh;
+    }
+    // tree depth and the stack the exact DFS needs: need(v) = max(1 + need(left), need(right))
+    std::vector<uint32_t> need(s->nodes.size(), 0), dep(s->nodes.size(), 0);
+    uint32_t maxdep = 0;
+    for (size_t i = 0; i < s->nodes.size(); ++i) {
+        const pth::HNode& n = s->nodes[i];
+        if (n.left != 0xFFFFFFFFu) { dep[n.left] = dep[i] + 1; dep[n.right] = dep[i] + 1; }
+        maxdep = std::max(maxdep, dep[i]);
+    }
+    for (size_t k = s->nodes.size(); k-- > 0;) {
+        const pth::HNode& n = s->nodes[k];
+        if (n.left != 0xFFFFFFFFu) need[k] = std::max(1u + need[n.left], need[n.right]);
+    }
+    s->tree_depth = maxdep + 1;
+    s->max_stack = need.empty() ? 0 : need[0];
+    if (s->nodes.size() >= (1u << 24)) throw std::runtime_error("BVH larger than 2^24 nodes");
+}
+
+// ------------------------------------------------------------- devices ---
+int check_device(int dev) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(PT_E_NO_GPU, "no HIP device visible");
+    if (dev < 0 || dev >= n) return fail(PT_E_NO_GPU, "device index out of range");
+    hipDeviceProp_t pr;
+    HIP_TRY(hipGetDeviceProperties(&pr, dev));
+    if (strncmp(pr.gcnArchName, "gfx950", 6) != 0)
+        return fail(PT_E_NO_GPU, std::string("device is ") + pr.gcnArchName + ", this build targets gfx950");
+    return PT_OK;
+}
+
+template <class T>
+int upload(T** dst, const std::vector<T>& v) {
+    const size_t bytes = std::max<size_t>(sizeof(T), v.size() * sizeof(T));
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(dst), bytes));
+    if (!v.empty()) HIP_TRY(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return PT_OK;
+}
+
+int ensure_device_scene(pt_scene* s, int dev, DevScene** out) {
+    std::lock_guard<std::mutex> lk(s->mu);
+    auto it = s->dev.find(dev);
+    if (it != s->dev.end()) { *out = &it->second; return PT_OK; }
+    HIP_TRY(hipSetDevice(dev));
+    DevScene d;
+    int rc;
+    if ((rc = upload(&d.nodes, s->dnodes)) || (rc = upload(&d.prims, s->dprims)) || (rc = upload(&d.shade, s->dshade)) ||
+        (rc = upload(&d.planes, s->planes)) || (rc = upload(&d.emitters, s->emitters)))
+        return rc;
+    std::vector<float> thr(s->thr, s->thr + 256);
+    if ((rc = upload(&d.thr, thr))) return rc;
+    s->dev[dev] = d;
+    *out = &s->dev[dev];
+    return PT_OK;
+}
+
+void free_device_scene(DevScene& d) {
+    (void)hipFree(d.nodes); (void)hipFree(d.prims); (void)hipFree(d.shade);
+    (void)hipFree(d.planes); (void)hipFree(d.emitters); (void)hipFree(d.thr);
+}
+
+pt::SceneView host_view(const pt_scene* s) {
+    pt::SceneView v;
+    v.nodes = s->dnodes.data();
+    v.prims = s->dprims.data();
+    v.shade = s->dshade.data();
+    v.planes = s->planes.data();
+    v.emitters = s->emitters.data();
+    v.n_planes = (uint32_t)s->planes.size();
+    v.n_emitters = (uint32_t)s->emitters.size();
+    v.bg = pt::mk3(s->hs.bg[0], s->hs.bg[1], s->hs.bg[2]);
+    return v;
+}
+
+pt::CamView make_cam(const pt_scene* s) {
+    const pth::HScene& h = s->hs;
+    pt::CamView c;
+    c.pos = pt::mk3(h.cam_pos[0], h.cam_pos[1], h.cam_pos[2]);
+    c.right = pt::mk3(h.cam_right[0], h.cam_right[1], h.cam_right[2]);
+    c.up = pt::mk3(h.cam_up[0], h.cam_up[1], h.cam_up[2]);
+    c.fwd = pt::mk3(h.cam_fwd[0], h.cam_fwd[1], h.cam_fwd[2]);
+    // src/scene.cpp:181-182: float tan_fov_x = tan(fov_x / 2) -> ::tan(double); tan_y = tan_x*H/W
+    c.tx = (float)tan((double)(h.fov_x / 2));
+    c.ty = c.tx * (float)h.H / (float)h.W;
+    c.W = (float)h.W;
+    c.H = (float)h.H;
+    return c;
+}
+
+int finish_pending(pt_session* ss) {
+    for (auto& e : ss->pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) ss->kernel_ms += ms;
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    ss->pending.clear();
+    return PT_OK;
+}
+
+void progress_bar(uint64_t done, uint64_t total, int& last) {
+    // the reference prints "Loading: [ ##...   x% ]" every 10 % (src/scene.cpp:232-240)
+    const int ct = total ? (int)((done * 10) / total) : 10;
+    while (last < ct && last < 10) {
+        ++last;
+        std::string bar = "Loading: [ ";
+        bar += std::string((size_t)last, '#');
+        bar += std::string((size_t)(11 - last), ' ');
+        bar += std::to_string(last * 10);
+        bar += "% ]\n";
+        fputs(bar.c_str(), stdout);
+        fflush(stdout);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* pt_last_error(void) { return g_err.c_str(); }
+int pt_abi_version(void) { return PT_ABI_VERSION; }
+
+int pt_scene_load_mem(const char* text, size_t len, pt_scene** out) {
+    if (!out || (!text && len)) return fail(PT_E_INVALID, "null argument");
+    auto* s = new pt_scene();
+    try {
+        pth::parse_scene(text, len, s->hs);
+    } catch (const std::exception& e) {
+        delete s;
+        return fail(PT_E_SCENE, e.what());
+    }
+    *out = s;
+    return PT_OK;
+}
+
+int pt_scene_load(const char* path, pt_scene** out) {
+    if (!path || !out) return fail(PT_E_INVALID, "null argument");
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return fail(PT_E_IO, std::string("cannot open ") + path);
+    std::string text((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    return pt_scene_load_mem(text.data(), text.size(), out);
+}
+
+int pt_scene_override(pt_scene* s, uint32_t w, uint32_t h, uint32_t samples, uint32_t depth) {
+    if (!s) return fail(PT_E_INVALID, "null scene");
+    if (w) s->hs.W = w;
+    if (h) s->hs.H = h;
+    if (samples) s->hs.samples = samples;
+    if (depth) s->hs.depth = depth;
+    return PT_OK;
+}
+
+// Scene::InitScene (src/scene.cpp:7-40)
+int pt_scene_prepare(pt_scene* s) {
+    if (!s) return fail(PT_E_INVALID, "null scene");
+    if (s->prepared) return PT_OK;
+    try {
+        auto& P = s->hs.prims;
+        for (const auto& p : P)
+            if (p.type != pt::T_PLANE && p.type != pt::T_BOX && p.type != pt::T_ELLIPSOID && p.type != pt::T_TRIANGLE)
+                return fail(PT_E_SCENE, "primitive without a type (the reference exits in Primitive::Intersect)");
+        // InitBVH: std::partition(non-planes first) on the same sequence -> same permutation
+        std::vector<uint32_t> idx(P.size());
+        for (uint32_t i = 0; i < (uint32_t)P.size(); ++i) idx[i] = i;
+        auto mid = std::partition(idx.begin(), idx.end(), [&P](uint32_t i) { return P[i].type != pt::T_PLANE; });
+        s->n_bvh = (uint32_t)(mid - idx.begin());
+        std::vector<pth::HPrim> part(P.size());
+        for (size_t i = 0; i < idx.size(); ++i) part[i] = P[idx[i]];
+        P.swap(part);
+        pth::build_reference_bvh(P, s->n_bvh, s->nodes);
+        s->planes.clear();
+        for (uint32_t i = s->n_bvh; i < (uint32_t)P.size(); ++i) s->planes.push_back(i);
+        // InitDistribution: BOX/ELLIPSOID with emission > 0, in post-BVH order
+        s->emitters.clear();
+        for (uint32_t i = 0; i < (uint32_t)P.size(); ++i) {
+            const auto& p = P[i];
+            if (!(p.emis[0] > 0 || p.emis[1] > 0 || p.emis[2] > 0)) continue;
+            if (p.type == pt::T_BOX || p.type == pt::T_ELLIPSOID) s->emitters.push_back(i);
+        }
+        build_device_layout(s);
+        pth::build_gamma_thresholds(s->thr);
+    } catch (const std::exception& e) {
+        return fail(PT_E_SCENE, e.what());
+    }
+    s->prepared = true;
+    return PT_OK;
+}
+
+int pt_scene_get_info(const pt_scene* s, pt_scene_info* info) {
+    if (!s || !info) return fail(PT_E_INVALID, "null argument");
+    memset(info, 0, sizeof(*info));
+    info->width = s->hs.W;
+    info->height = s->hs.H;
+    info->samples = s->hs.samples;
+    info->ray_depth = s->hs.depth;
+    info->n_prims = (uint32_t)s->hs.prims.size();
+    info->n_bvh_prims = s->n_bvh;
+    info->n_planes = (uint32_t)s->planes.size();
+    info->n_emitters = (uint32_t)s->emitters.size();
+    info->n_nodes = (uint32_t)s->nodes.size();
+    info->tree_depth = s->tree_depth;
+    info->max_stack = s->max_stack;
+    info->n_warnings = (uint32_t)s->hs.warnings.size();
+    return PT_OK;
+}
+
+int pt_scene_dump_bvh(const pt_scene* s, void* nodes_out, size_t nodes_bytes, void* prims_out, size_t prims_bytes) {
+    if (!s || !s->prepared) return fail(PT_E_INVALID, "scene not prepared");
+    if (nodes_out) {
+        if (nodes_bytes < s->nodes.size() * 40) return fail(PT_E_INVALID, "nodes buffer too small");
+        auto* b = static_cast<unsigned char*>(nodes_out);
+        for (const auto& n : s->nodes) {
+            memcpy(b, n.mn, 12); memcpy(b + 12, n.mx, 12);
+            const uint32_t u[4] = {n.left, n.right, n.first, n.count};
+            memcpy(b + 24, u, 16);
+            b += 40;
+        }
+    }
+    if (prims_out) {
+        if (prims_bytes < s->hs.prims.size() * 52) return fail(PT_E_INVALID, "prims buffer too small");
+        auto* b = static_cast<unsigned char*>(prims_out);
+        for (const auto& p : s->hs.prims) {
+            const bool tri = p.type == pt::T_TRIANGLE;
+            const float f[12] = {p.a[0], p.a[1], p.a[2], tri ? p.b[0] : 0.f, tri ? p.b[1] : 0.f, tri ? p.b[2] : 0.f,
+                                 tri ? p.c[0] : 0.f, tri ? p.c[1] : 0.f, tri ? p.c[2] : 0.f, p.pos[0], p.pos[1], p.pos[2]};
+            memcpy(b, &p.type, 4);
+            memcpy(b + 4, f, 48);
+            b += 52;
+        }
+    }
+    return PT_OK;
+}
+
+void pt_scene_free(pt_scene* s) {
+    if (!s) return;
+    for (auto& kv : s->dev) {
+        (void)hipSetDevice(kv.first);
+        free_device_scene(kv.second);
+    }
+    delete s;
+}
+
+// ------------------------------------------------------------- sessions ---
+int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
+    if (!s || !o || !out) return fail(PT_E_INVALID, "null argument");
+    if (!s->prepared) return fail(PT_E_INVALID, "scene not prepared (call pt_scene_prepare)");
+    if (o->world == 0 || o->rank >= o->world) return fail(PT_E_INVALID, "bad rank/world");
+    if (s->hs.W == 0 || s->hs.H == 0) return fail(PT_E_SCENE, "zero image size");
+    if ((uint64_t)s->hs.W * s->hs.H >= 2147483647ull) return fail(PT_E_SCENE, "image too large for per-pixel seeds");
+    int rc = check_device(o->device);
+    if (rc) return rc;
+    DevScene* ds = nullptr;
+    if ((rc = ensure_device_scene(s, o->device, &ds))) return rc;
+    auto* ss = new pt_session();
+    ss->sc = s;
+    ss->dev = o->device;
+    ss->traversal = o->traversal;
+    ss->depth = s->hs.depth;
+    ss->tm.W = s->hs.W;
+    ss->tm.H = s->hs.H;
+    ss->tm.x0 = o->win_w ? o->win_x0 : 0u;
+    ss->tm.y0 = o->win_w ? o->win_y0 : 0u;
+    ss->tm.ww = o->win_w ? o->win_w : s->hs.W;
+    ss->tm.wh = o->win_w ? o->win_h : s->hs.H;
+    if (ss->tm.ww == 0 || ss->tm.wh == 0 || (uint64_t)ss->tm.x0 + ss->tm.ww > s->hs.W ||
+        (uint64_t)ss->tm.y0 + ss->tm.wh > s->hs.H) {
+        delete ss;
+        return fail(PT_E_INVALID, "window outside the image");
+    }
+    ss->tm.tiles_x = (ss->tm.ww + 15u) / 16u;
+    ss->tm.n_tiles = ss->tm.tiles_x * ((ss->tm.wh + 15u) / 16u);
+    ss->tm.rank = o->rank;
+    ss->tm.world = o->world;
+    ss->n_tiles_local = ss->tm.n_tiles > o->rank ? (ss->tm.n_tiles - o->rank + o->world - 1u) / o->world : 0u;
+    ss->n_slots = ss->n_tiles_local * 256u;
+    ss->cam = make_cam(s);
+    auto cleanup = [&](int code) {
+        pt_session_free(ss);
+        return code;
+    };
+    if (hipSetDevice(ss->dev) != hipSuccess) return cleanup(fail(PT_E_HIP, "hipSetDevice failed"));
+    const size_t n = std::max<size_t>(ss->n_slots, 1);
+    const size_t vwords = 3ull * std::max<uint32_t>(ss->depth, 1u) * n;
+    if (hipStreamCreateWithFlags(&ss->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&ss->st.rng_x, n * 4) != hipSuccess || hipMalloc(&ss->st.rng_saved, n * 4) != hipSuccess ||
+        hipMalloc(&ss->st.rng_flag, n * 4) != hipSuccess || hipMalloc(&ss->st.sum, 3 * n * 4) != hipSuccess ||
+        hipMalloc(&ss->vscratch, vwords * 4) != hipSuccess || hipMalloc(&ss->counters, 8 * 8) != hipSuccess ||
+        hipMalloc(&ss->out, 3 * n) != hipSuccess)
+        return cleanup(fail(PT_E_OOM, "device allocation failed"));
+    ss->st.n_slots = ss->n_slots;
+    if (hipMemsetAsync(ss->counters, 0, 64, ss->stream) != hipSuccess) return cleanup(fail(PT_E_HIP, "memset failed"));
+    if (ss->n_tiles_local) {
+        pt::InitParams ip;
+        ip.tm = ss->tm;
+        ip.st = ss->st;
+        if (pt_launch_init(ip, ss->n_tiles_local, ss->stream) != hipSuccess)
+            return cleanup(fail(PT_E_HIP, "k_init launch failed"));
+    }
+    *out = ss;
+    return PT_OK;
+}
+
+int pt_session_layout(const pt_session* ss, uint32_t* n_tiles, uint64_t* packed_rgb_bytes) {
+    if (!ss) return fail(PT_E_INVALID, "null session");
+    if (n_tiles) *n_tiles = ss->n_tiles_local;
+    if (packed_rgb_bytes) *packed_rgb_bytes = 3ull * ss->n_slots;
+    return PT_OK;
+}
+
+int pt_session_trace(pt_session* ss, uint32_t spp) {
+    if (!ss) return fail(PT_E_INVALID, "null session");
+    if (spp == 0 || ss->n_tiles_local == 0) { ss->samples_done += spp; return PT_OK; }
+    HIP_TRY(hipSetDevice(ss->dev));
+    DevScene& ds = ss->sc->dev[ss->dev];
+    pt::TraceParams tp;
+    const pt_scene* s = ss->sc;
+    tp.S.nodes = ds.nodes;
+    tp.S.prims = ds.prims;
+    tp.S.shade = ds.shade;
+    tp.S.planes = ds.planes;
+    tp.S.emitters = ds.emitters;
+    tp.S.n_planes = (uint32_t)s->planes.size();
+    tp.S.n_emitters = (uint32_t)s->emitters.size();
+    tp.S.bg = pt::mk3(s->hs.bg[0], s->hs.bg[1], s->hs.bg[2]);
+    tp.cam = ss->cam;
+    tp.tm = ss->tm;
+    tp.st = ss->st;
+    tp.vscratch = ss->vscratch;
+    tp.counters = ss->counters;
+    tp.depth = ss->depth;
+    tp.spp = spp;
+    const uint32_t lds = 256u * 4u * std::max<uint32_t>(s->max_stack, 1u);
+    if (lds > 160u * 1024u) return fail(PT_E_SCENE, "BVH too deep for the LDS traversal stack");
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, ss->stream));
+    HIP_TRY(pt_launch_trace(tp, ss->n_tiles_local, lds, ss->stream));
+    HIP_TRY(hipEventRecord(e1, ss->stream));
+    ss->pending.emplace_back(e0, e1);
+    ss->samples_done += spp;
+    return PT_OK;
+}
+
+int pt_session_resolve(pt_session* ss, uint8_t* dev_out, float* dev_radiance) {
+    if (!ss) return fail(PT_E_INVALID, "null session");
+    if (ss->n_tiles_local == 0) return PT_OK;
+    HIP_TRY(hipSetDevice(ss->dev));
+    pt::ResolveParams rp;
+    rp.st = ss->st;
+    rp.thr = ss->sc->dev[ss->dev].thr;
+    rp.out = dev_out ? dev_out : ss->out;
+    rp.rad = dev_radiance;
+    rp.samples = (uint32_t)ss->samples_done;
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, ss->stream));
+    HIP_TRY(pt_launch_resolve(rp, ss->n_tiles_local, ss->stream));
+    HIP_TRY(hipEventRecord(e1, ss->stream));
+    HIP_TRY(hipStreamSynchronize(ss->stream));
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, e0, e1) == hipSuccess) ss->resolve_ms += ms;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return PT_OK;
+}
+
+int pt_session_sync(pt_session* ss) {
+    if (!ss) return fail(PT_E_INVALID, "null session");
+    HIP_TRY(hipSetDevice(ss->dev));
+    HIP_TRY(hipStreamSynchronize(ss->stream));
+    return finish_pending(ss);
+}
+
+int pt_session_read_packed(pt_session* ss, uint8_t* host_out, size_t bytes) {
+    if (!ss || !host_out) return fail(PT_E_INVALID, "null argument");
+    if (bytes < 3ull * ss->n_slots) return fail(PT_E_INVALID, "buffer too small");
+    if (ss->n_slots == 0) return PT_OK;
+    HIP_TRY(hipSetDevice(ss->dev));
+    HIP_TRY(hipMemcpyAsync(host_out, ss->out, 3ull * ss->n_slots, hipMemcpyDeviceToHost, ss->stream));
+    HIP_TRY(hipStreamSynchronize(ss->stream));
+    return PT_OK;
+}
+
+int pt_session_stats(pt_session* ss, pt_stats* st) {
+    if (!ss || !st) return fail(PT_E_INVALID, "null argument");
+    int rc = pt_session_sync(ss);
+    if (rc) return rc;
+    unsigned long long c[8] = {0};
+    HIP_TRY(hipMemcpy(c, ss->counters, 64, hipMemcpyDeviceToHost));
+    memset(st, 0, sizeof(*st));
+    st->rays = c[0];
+    st->node_visits = c[1];
+    st->prim_tests = c[2];
+    st->plane_tests = c[3];
+    st->errors = c[4];
+    uint64_t px = 0;
+    for (uint32_t t = 0; t < ss->n_tiles_local; ++t) {
+        const uint32_t gt = t * ss->tm.world + ss->tm.rank;
+        const uint32_t tx = gt % ss->tm.tiles_x, ty = gt / ss->tm.tiles_x;
+        const uint32_t w = std::min(16u, ss->tm.ww - tx * 16u), h = std::min(16u, ss->tm.wh - ty * 16u);
+        px += (uint64_t)w * h;
+    }
+    st->samples = px * ss->samples_done;
+    st->kernel_ms = ss->kernel_ms;
+    st->resolve_ms = ss->resolve_ms;
+    st->node_bytes = sizeof(pt::Node);
+    st->prim_bytes = sizeof(pt::Prim);
+    return PT_OK;
+}
+
+void* pt_session_stream(pt_session* ss) { return ss ? (void*)ss->stream : nullptr; }
+
+void pt_session_free(pt_session* ss) {
+    if (!ss) return;
+    (void)hipSetDevice(ss->dev);
+    if (ss->stream) (void)hipStreamSynchronize(ss->stream);
+    finish_pending(ss);
+    (void)hipFree(ss->st.rng_x); (void)hipFree(ss->st.rng_saved); (void)hipFree(ss->st.rng_flag);
+    (void)hipFree(ss->st.sum); (void)hipFree(ss->vscratch); (void)hipFree(ss->counters);
+    (void)hipFree(ss->out); (void)hipFree(ss->rad);
+    if (ss->stream) (void)hipStreamDestroy(ss->stream);
+    delete ss;
+}
+
+int pt_unpack_tiles(uint32_t W, uint32_t H, uint32_t rank, uint32_t world, const uint8_t* packed, uint8_t* rgb) {
+    if (!packed || !rgb || world == 0) return fail(PT_E_INVALID, "bad argument");
+    const uint32_t tiles_x = (W + 15u) / 16u, n_tiles = tiles_x * ((H + 15u) / 16u);
+    uint32_t lt = 0;
+    for (uint32_t gt = rank; gt < n_tiles; gt += world, ++lt) {
+        const uint32_t tx = gt % tiles_x, ty = gt / tiles_x;
+        for (uint32_t j = 0; j < 16u; ++j) {
+            const uint32_t y = ty * 16u + j;
+            if (y >= H) break;
+            const uint32_t x0 = tx * 16u, w = std::min(16u, W - x0);
+            memcpy(rgb + ((size_t)y * W + x0) * 3, packed + ((size_t)lt * 256u + j * 16u) * 3, (size_t)w * 3);
+        }
+    }
+    return PT_OK;
+}
+
+int pt_unpack_tiles_f32(uint32_t W, uint32_t H, uint32_t rank, uint32_t world, const float* packed, float* rad) {
+    if (!packed || !rad || world == 0) return fail(PT_E_INVALID, "bad argument");
+    const uint32_t tiles_x = (W + 15u) / 16u, n_tiles = tiles_x * ((H + 15u) / 16u);
+    uint32_t lt = 0;
+    for (uint32_t gt = rank; gt < n_tiles; gt += world, ++lt) {
+        const uint32_t tx = gt % tiles_x, ty = gt / tiles_x;
+        for (uint32_t j = 0; j < 16u; ++j) {
+            const uint32_t y = ty * 16u + j;
+            if (y >= H) break;
+            const uint32_t x0 = tx * 16u, w = std::min(16u, W - x0);
+            memcpy(rad + ((size_t)y * W + x0) * 3, packed + ((size_t)lt * 256u + j * 16u) * 3, (size_t)w * 12);
+        }
+    }
+    return PT_OK;
+}
+
+// ------------------------------------------------------------- render -----
+void pt_render_opts_default(pt_render_opts* o) {
+    if (!o) return;
+    memset(o, 0, sizeof(*o));
+    o->device = 0;
+    o->ngpu = 1;
+    o->traversal = PT_TRAVERSAL_EXACT;
+}
+
+int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radiance, pt_stats* stats) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!s) return fail(PT_E_INVALID, "null scene");
+    pt_render_opts o;
+    pt_render_opts_default(&o);
+    if (opts) o = *opts;
+    int rc = pt_scene_prepare(s);
+    if (rc) return rc;
+    const uint32_t S = o.samples ? o.samples : s->hs.samples;
+    const uint32_t W = o.win_w ? o.win_w : s->hs.W, H = o.win_w ? o.win_h : s->hs.H;
+    const int ngpu = std::max(1, o.ngpu);
+    std::vector<pt_session*> sess((size_t)ngpu, nullptr);
+    auto cleanup = [&](int code) {
+        for (auto* x : sess) pt_session_free(x);
+        return code;
+    };
+    for (int g = 0; g < ngpu; ++g) {
+        pt_session_opts so;
+        so.device = o.device + g;
+        so.rank = (uint32_t)g;
+        so.world = (uint32_t)ngpu;
+        so.traversal = o.traversal;
+        so.win_x0 = o.win_x0;
+        so.win_y0 = o.win_y0;
+        so.win_w = o.win_w;
+        so.win_h = o.win_h;
+        if ((rc = pt_session_create(s, &so, &sess[(size_t)g]))) return cleanup(rc);
+    }
+    const uint32_t chunk = o.spp_per_launch ? o.spp_per_launch : std::max(1u, std::min(S, 4u));
+    int last = 0;
+    for (uint32_t done = 0; done < S;) {
+        const uint32_t k = std::min(chunk, S - done);
+        for (auto* x : sess)
+            if ((rc = pt_session_trace(x, k))) return cleanup(rc);
+        done += k;
+        if (o.progress) {
+            for (auto* x : sess)
+                if ((rc = pt_session_sync(x))) return cleanup(rc);
+            progress_bar(done, S, last);
+        }
+    }
+    // resolve per device, then gather on the host
+    // (multi-GPU: every rank's packed tiles are copied back and interleaved)
+    pt_stats agg;
+    memset(&agg, 0, sizeof(agg));
+    for (int g = 0; g < ngpu; ++g) {
+        pt_session* x = sess[(size_t)g];
+        if ((rc = pt_session_sync(x))) return cleanup(rc);
+        float* drad = nullptr;
+        if (radiance && x->n_slots) {
+            if (hipMalloc(&x->rad, 12ull * x->n_slots) != hipSuccess) return cleanup(fail(PT_E_OOM, "radiance buffer"));
+            drad = x->rad;
+        }
+        if ((rc = pt_session_resolve(x, nullptr, drad))) return cleanup(rc);
+        std::vector<uint8_t> packed(3ull * x->n_slots);
+        if (rgb && x->n_slots) {
+            if ((rc = pt_session_read_packed(x, packed.data(), packed.size()))) return cleanup(rc);
+            pt_unpack_tiles(W, H, (uint32_t)g, (uint32_t)ngpu, packed.data(), rgb);
+        }
+        if (radiance && x->n_slots) {
+            std::vector<float> pr(3ull * x->n_slots);
+            if (hipMemcpy(pr.data(), drad, pr.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+                return cleanup(fail(PT_E_HIP, "radiance readback failed"));
+            pt_unpack_tiles_f32(W, H, (uint32_t)g, (uint32_t)ngpu, pr.data(), radiance);
+        }
+        pt_stats st;
+        if ((rc = pt_session_stats(x, &st))) return cleanup(rc);
+        agg.rays += st.rays; agg.node_visits += st.node_visits; agg.prim_tests += st.prim_tests;
+        agg.plane_tests += st.plane_tests; agg.samples += st.samples; agg.errors += st.errors;
+        agg.kernel_ms = std::max(agg.kernel_ms, st.kernel_ms);
+        agg.resolve_ms = std::max(agg.resolve_ms, st.resolve_ms);
+        agg.node_bytes = st.node_bytes; agg.prim_bytes = st.prim_bytes;
+    }
+    if (o.progress) progress_bar(S, S, last);
+    agg.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (stats) *stats = agg;
+    return cleanup(agg.errors ? fail(PT_E_INVALID, "exactness guard tripped (hit list overflow)") : PT_OK);
+}
+
+int pt_write_ppm(const char* path, uint32_t W, uint32_t H, const uint8_t* rgb) {
+    if (!path || !rgb) return fail(PT_E_INVALID, "null argument");
+    FILE* f = fopen(path, "wb");
+    if (!f) return fail(PT_E_IO, std::string("cannot write ") + path);
+    fprintf(f, "P6\n%u %u\n255\n", W, H);
+    const size_t n = (size_t)W * H * 3;
+    const bool ok = fwrite(rgb, 1, n, f) == n;
+    if (fclose(f) != 0 || !ok) return fail(PT_E_IO, std::string("short write to ") + path);
+    return PT_OK;
+}
+
+// ------------------------------------------------------------- selftests --
+namespace {
+struct HostStack {
+    std::vector<uint32_t> v;
+    void push(uint32_t i, uint32_t x) { if (v.size() <= i) v.resize(i + 1); v[i] = x; }
+    uint32_t get(uint32_t i) const { return v[i]; }
+};
+struct HostVStore {
+    std::vector<uint32_t> v;
+    void put(uint32_t k, uint32_t idm, float s1, float s2) {
+        if (v.size() < 3 * (k + 1)) v.resize(3 * (k + 1));
+        v[3 * k] = idm; v[3 * k + 1] = pt::f2u(s1); v[3 * k + 2] = pt::f2u(s2);
+    }
+    void get(uint32_t k, uint32_t& idm, float& s1, float& s2) const {
+        idm = v[3 * k]; s1 = pt::u2f(v[3 * k + 1]); s2 = pt::u2f(v[3 * k + 2]);
+    }
+};
+}  // namespace
+
+int pt_selftest_ray_intersection(pt_scene* s, uint32_t n, const float* rays, int32_t* ids, float* hits) {
+    int rc = pt_scene_prepare(s);
+    if (rc) return rc;
+    const pt::SceneView V = host_view(s);
+    HostStack stk;
+    pt::Counts C{};
+    for (uint32_t i = 0; i < n; ++i) {
+        pt::Ray r;
+        r.o = pt::mk3(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
+        r.d = pt::mk3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+        pt::Hit h;
+        const int id = pt::ray_intersection(V, r, stk, h, C);
+        ids[i] = id;
+        const bool ok = id != -1;
+        hits[5 * i] = ok ? h.t : 0.f;
+        hits[5 * i + 1] = ok ? h.n.x : 0.f;
+        hits[5 * i + 2] = ok ? h.n.y : 0.f;
+        hits[5 * i + 3] = ok ? h.n.z : 0.f;
+        hits[5 * i + 4] = ok ? (h.interior ? 1.f : 0.f) : 0.f;
+    }
+    return C.errs ? fail(PT_E_INVALID, "hit list overflow") : PT_OK;
+}
+
+int pt_selftest_render_host(pt_scene* s, uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, uint32_t spp,
+                            float* radiance) {
+    int rc = pt_scene_prepare(s);
+    if (rc) return rc;
+    const pt::SceneView V = host_view(s);
+    const pt::CamView cam = make_cam(s);
+    const uint32_t S = spp ? spp : s->hs.samples;
+    const uint32_t nt = std::max(1u, std::thread::hardware_concurrency());
+    std::vector<std::thread> th;
+    std::vector<uint32_t> errs(nt, 0);
+    for (uint32_t t = 0; t < nt; ++t) {
+        th.emplace_back([&, t]() {
+            HostStack stk;
+            HostVStore vs;
+            pt::Counts C{};
+            for (uint64_t k = t; k < (uint64_t)w * h; k += nt) {
+                const uint32_t x = x0 + (uint32_t)(k % w), y = y0 + (uint32_t)(k / w);
+                pt::Rng R = pt::rng_seed(y * s->hs.W + x);
+                pt::f3 sum = pt::mk3(0.f, 0.f, 0.f);
+                for (uint32_t i = 0; i < S; ++i) {
+                    const float fx = (float)x + pt::rng_uniform(R);
+                    const float fy = (float)y + pt::rng_uniform(R);
+                    sum = sum + pt::trace_path(V, pt::camera_ray(cam, fx, fy), s->hs.depth, R, stk, vs, C);
+                }
+                const pt::f3 m = (1.f / (float)S) * sum;
+                radiance[3 * k] = m.x; radiance[3 * k + 1] = m.y; radiance[3 * k + 2] = m.z;
+            }
+            errs[t] = C.errs;
+        });
+    }
+    for (auto& x : th) x.join();
+    for (uint32_t e : errs)
+        if (e) return fail(PT_E_INVALID, "hit list overflow");
+    return PT_OK;
+}
+
+int pt_selftest_gamma_table(const pt_scene* s, float* thr256) {
+    if (!s || !s->prepared || !thr256) return fail(PT_E_INVALID, "scene not prepared");
+    memcpy(thr256, s->thr, sizeof(s->thr));
+    return PT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,52 @@
+// pt_scene.h -- host-side scene model of libpt (internal).
+#pragma once
+#include <stdint.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../device/pt_core.h"
+
+namespace pth {
+
+// include/primitives.h:31-64 (hw5)
+struct HPrim {
+    uint32_t type = 0;  // 0 = never set (the reference leaves it uninitialised)
+    uint32_t mat = pt::M_DIFFUSE;
+    float col[3] = {0.f, 0.f, 0.f};
+    float emis[3] = {0.f, 0.f, 0.f};
+    float pos[3] = {0.f, 0.f, 0.f};
+    float rot[4] = {0.f, 0.f, 0.f, 1.f};  // x y z w; default (w=1) = include/primitives.h:44
+    float ior = 0.f;
+    float a[3] = {0.f, 0.f, 0.f};  // dop_data   (plane n, box s, ellipsoid r, triangle a)
+    float b[3] = {0.f, 0.f, 0.f};  // dop_data1  (triangle b)
+    float c[3] = {0.f, 0.f, 0.f};  // dop_data2  (triangle c)
+};
+
+// include/bvh.h:28-34
+struct HNode {
+    float mn[3], mx[3];
+    uint32_t left, right, first, count;
+};
+
+struct HScene {
+    uint32_t W = 0, H = 0, depth = 0, samples = 0;
+    float bg[3] = {0.f, 0.f, 0.f};
+    float cam_pos[3] = {0, 0, 0}, cam_right[3] = {0, 0, 0}, cam_up[3] = {0, 0, 0}, cam_fwd[3] = {0, 0, 0};
+    float fov_x = 0.f;
+    std::vector<HPrim> prims;
+    std::vector<std::string> warnings;
+};
+
+// Parse the hw5 grammar (scene_load.cpp).  Throws std::runtime_error on I/O failure only.
+void parse_scene(const char* text, size_t len, HScene& S);
+
+// Faithful reference BVH (bvh_build.cpp): reorders prims[0, n) like
+// BVH_t::InitTree and appends nodes in preorder.
+void build_reference_bvh(std::vector<HPrim>& prims, uint32_t n, std::vector<HNode>& nodes);
+
+// Gamma/quantise threshold table (tonemap.cpp)
+void build_gamma_thresholds(float thr[256]);
+
+}  // namespace pth

@@ -1,0 +1,212 @@
+// scene_load.cpp -- hw5 scene-file parser (drop-in for Scene::Load,
+// /root/reference/hw5/src/sceneload.cpp:8-176).
+//
+// One pass over the file bytes, no per-line allocation.  It keeps the
+// reference's observable behaviour, which is that of std::getline +
+// std::stringstream extraction:
+//  * lines split on '\n'; tokens on C-locale whitespace;
+//  * a primitive block (after NEW_PRIMITIVE) ends at a blank line or at the
+//    first non-primitive command; that command is then re-dispatched against
+//    the *stale* NEW_PRIMITIVE line's stream (sceneload.cpp:120-159), so its
+//    arguments are not read (values stay as they were);
+//  * a failed numeric extraction stores 0 and poisons the rest of the line;
+//    reading past the end of a line leaves the value unchanged;
+//  * a primitive-type line (PLANE/BOX/ELLIPSOID/TRIANGLE) resets the whole
+//    primitive (`primitive = Primitive(...)`, sceneload.cpp:49-72);
+//  * unknown top-level commands warn on stderr (sceneload.cpp:170-172).
+#include <ctype.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+
+#include "pt_scene.h"
+
+namespace pth {
+namespace {
+
+inline bool is_ws(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\v' || c == '\f' || c == '\r'; }
+inline bool is_dig(char c) { return c >= '0' && c <= '9'; }
+
+// the remainder of one line, read like a std::stringstream
+struct Cursor {
+    const char* p;
+    const char* e;
+    bool fail = false;
+    Cursor(const char* b, const char* en) : p(b), e(en) {}
+    void skip() { while (p < e && is_ws(*p)) ++p; }
+    // operator>>(std::string&)
+    bool word(const char*& wb, size_t& wl) {
+        if (fail) return false;
+        skip();
+        if (p >= e) { fail = true; return false; }
+        wb = p;
+        while (p < e && !is_ws(*p)) ++p;
+        wl = (size_t)(p - wb);
+        return true;
+    }
+    // operator>>(float&)  (num_get::_M_extract_float + strtof)
+    void get(float& v) {
+        if (fail) return;
+        skip();
+        if (p >= e) { fail = true; return; }
+        const char* b = p;
+        const char* q = p;
+        if (q < e && (*q == '+' || *q == '-')) ++q;
+        bool dig = false;
+        while (q < e && is_dig(*q)) { ++q; dig = true; }
+        if (q < e && *q == '.') { ++q; while (q < e && is_dig(*q)) { ++q; dig = true; } }
+        if (dig && q < e && (*q == 'e' || *q == 'E')) {
+            const char* r = q + 1;
+            if (r < e && (*r == '+' || *r == '-')) ++r;
+            if (r < e && is_dig(*r)) { while (r < e && is_dig(*r)) ++r; }
+            q = r;
+        }
+        p = q;
+        char buf[128];
+        const size_t n = (size_t)(q - b);
+        if (n == 0 || n >= sizeof(buf)) { v = 0.f; fail = true; return; }
+        memcpy(buf, b, n);
+        buf[n] = '\0';
+        char* end = nullptr;
+        const float f = strtof(buf, &end);
+        if (end != buf + n) { v = 0.f; fail = true; return; }
+        v = f;
+    }
+    // operator>>(unsigned&)
+    void get(uint32_t& v) {
+        if (fail) return;
+        skip();
+        if (p >= e) { fail = true; return; }
+        bool neg = false;
+        if (*p == '+' || *p == '-') { neg = *p == '-'; ++p; }
+        const char* d0 = p;
+        unsigned long long acc = 0;
+        bool ovf = false;
+        while (p < e && is_dig(*p)) {
+            acc = acc * 10 + (unsigned)(*p - '0');
+            if (acc > 0xFFFFFFFFull) ovf = true;
+            ++p;
+        }
+        if (p == d0) { v = 0; fail = true; return; }
+        if (ovf) { v = 0xFFFFFFFFu; fail = true; return; }
+        v = neg ? (uint32_t)(0u - (uint32_t)acc) : (uint32_t)acc;
+    }
+    void get3(float* x) { get(x[0]); get(x[1]); get(x[2]); }
+};
+
+enum Cmd {
+    C_EMPTY, C_DIMENSIONS, C_BG_COLOR, C_CAMERA_POSITION, C_CAMERA_RIGHT, C_CAMERA_UP, C_CAMERA_FORWARD,
+    C_CAMERA_FOV_X, C_NEW_PRIMITIVE, C_PLANE, C_ELLIPSOID, C_BOX, C_POSITION, C_ROTATION, C_COLOR,
+    C_RAY_DEPTH, C_METALLIC, C_DIELECTRIC, C_IOR, C_SAMPLES, C_EMISSION, C_TRIANGLE, C_UNKNOWN
+};
+
+// src/sceneload.cpp:8-33
+Cmd command_of(const char* w, size_t n) {
+    if (n == 0) return C_EMPTY;
+    struct E { const char* s; Cmd c; };
+    static const E tab[] = {
+        {"DIMENSIONS", C_DIMENSIONS}, {"BG_COLOR", C_BG_COLOR}, {"CAMERA_POSITION", C_CAMERA_POSITION},
+        {"CAMERA_RIGHT", C_CAMERA_RIGHT}, {"CAMERA_UP", C_CAMERA_UP}, {"CAMERA_FORWARD", C_CAMERA_FORWARD},
+        {"CAMERA_FOV_X", C_CAMERA_FOV_X}, {"NEW_PRIMITIVE", C_NEW_PRIMITIVE}, {"PLANE", C_PLANE},
+        {"ELLIPSOID", C_ELLIPSOID}, {"BOX", C_BOX}, {"POSITION", C_POSITION}, {"ROTATION", C_ROTATION},
+        {"COLOR", C_COLOR}, {"RAY_DEPTH", C_RAY_DEPTH}, {"METALLIC", C_METALLIC}, {"DIELECTRIC", C_DIELECTRIC},
+        {"IOR", C_IOR}, {"SAMPLES", C_SAMPLES}, {"EMISSION", C_EMISSION}, {"TRIANGLE", C_TRIANGLE}};
+    for (const E& x : tab)
+        if (strlen(x.s) == n && memcmp(x.s, w, n) == 0) return x.c;
+    return C_UNKNOWN;
+}
+
+struct Lines {
+    const char* p;
+    const char* e;
+    bool next(const char*& lb, const char*& le) {
+        if (p >= e) return false;
+        const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(e - p)));
+        lb = p;
+        le = nl ? nl : e;
+        p = nl ? nl + 1 : e;
+        return true;
+    }
+};
+
+inline void reset_prim(HPrim& pr, uint32_t type) { pr = HPrim(); pr.type = type; }
+
+// src/sceneload.cpp:35-110; returns the command that ended the block ("" = blank line / EOF)
+std::string load_primitive(Lines& L, HPrim& pr) {
+    const char *lb, *le;
+    while (L.next(lb, le)) {
+        Cursor ss(lb, le);
+        const char* w = nullptr;
+        size_t wl = 0;
+        ss.word(w, wl);
+        const Cmd cmd = command_of(w, wl);
+        if (cmd == C_EMPTY) break;
+        switch (cmd) {
+            case C_ELLIPSOID: { float r[3] = {0, 0, 0}; ss.get3(r); reset_prim(pr, pt::T_ELLIPSOID); memcpy(pr.a, r, 12); break; }
+            case C_PLANE: { float n[3] = {0, 0, 0}; ss.get3(n); reset_prim(pr, pt::T_PLANE); memcpy(pr.a, n, 12); break; }
+            case C_BOX: { float s[3] = {0, 0, 0}; ss.get3(s); reset_prim(pr, pt::T_BOX); memcpy(pr.a, s, 12); break; }
+            case C_TRIANGLE: {
+                float a[3] = {0, 0, 0}, b[3] = {0, 0, 0}, c[3] = {0, 0, 0};
+                ss.get3(a); ss.get3(b); ss.get3(c);
+                reset_prim(pr, pt::T_TRIANGLE);
+                memcpy(pr.a, a, 12); memcpy(pr.b, b, 12); memcpy(pr.c, c, 12);
+                break;
+            }
+            case C_COLOR: ss.get3(pr.col); break;
+            case C_POSITION: ss.get3(pr.pos); break;
+            case C_ROTATION: ss.get(pr.rot[0]); ss.get(pr.rot[1]); ss.get(pr.rot[2]); ss.get(pr.rot[3]); break;
+            case C_METALLIC: pr.mat = pt::M_METALLIC; break;
+            case C_DIELECTRIC: pr.mat = pt::M_DIELECTRIC; break;
+            case C_IOR: ss.get(pr.ior); break;
+            case C_EMISSION: ss.get3(pr.emis); break;
+            default: return std::string(w, wl);
+        }
+    }
+    return std::string();
+}
+
+}  // namespace
+
+// src/sceneload.cpp:112-176
+void parse_scene(const char* text, size_t len, HScene& S) {
+    Lines L{text, text + len};
+    const char *lb, *le;
+    std::string name;
+    while (L.next(lb, le)) {
+        Cursor ss(lb, le);
+        const char* w = nullptr;
+        size_t wl = 0;
+        ss.word(w, wl);
+        name.assign(w ? w : "", w ? wl : 0);
+    again:
+        const Cmd cmd = command_of(name.data(), name.size());
+        if (cmd == C_EMPTY) continue;
+        switch (cmd) {
+            case C_DIMENSIONS: ss.get(S.W); ss.get(S.H); break;
+            case C_BG_COLOR: ss.get3(S.bg); break;
+            case C_CAMERA_POSITION: ss.get3(S.cam_pos); break;
+            case C_CAMERA_RIGHT: ss.get3(S.cam_right); break;
+            case C_CAMERA_UP: ss.get3(S.cam_up); break;
+            case C_CAMERA_FORWARD: ss.get3(S.cam_fwd); break;
+            case C_CAMERA_FOV_X: ss.get(S.fov_x); break;
+            case C_NEW_PRIMITIVE: {
+                HPrim pr;
+                name = load_primitive(L, pr);
+                S.prims.push_back(pr);
+                if (!name.empty()) goto again;   // the stale `ss` is reused, as in the reference
+                break;
+            }
+            case C_RAY_DEPTH: ss.get(S.depth); break;
+            case C_SAMPLES: ss.get(S.samples); break;
+            default: {
+                fprintf(stderr, "unexpected command(%s)\n", name.c_str());
+                S.warnings.push_back("unexpected command(" + name + ")");
+                break;
+            }
+        }
+    }
+}
+
+}  // namespace pth

@@ -1,0 +1,178 @@
+"""CPU tests of the product library (libpt.so) -- no GPU needed.
+
+* the C ABI loads and exports every function include/pt.h declares;
+* host logic: the quirk-faithful loader and the bit-faithful reference BVH
+  (fingerprints vs the reference's own md5s), the gamma/8-bit threshold table;
+* the device traversal/integrator code of pt_trace.h executed on the host
+  (pt_selftest_* hooks) against the reference's traversal KAT and fp32 radiance;
+* without a GPU, rendering fails loudly (PT_E_NO_GPU) -- there is no CPU fallback.
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import _util as U
+
+M = U.manifest()
+pt = U.ptrace()
+
+
+def declared_functions():
+    with open(os.path.join(U.REPO, "include", "pt.h")) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"\b(pt_[a-z0-9_]+)\s*\(", text)
+    return sorted(set(names))
+
+
+def test_abi_exports_every_declared_symbol():
+    names = declared_functions()
+    assert len(names) >= 25
+    lib = ctypes.CDLL(pt.LIB_PATH)
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(names) == set(pt.EXPORTED)
+    assert pt.abi_version() == 1
+
+
+@pytest.mark.parametrize("name", sorted(M["bvh"]))
+def test_product_bvh_fingerprints(name):
+    b = M["bvh"][name]
+    with pt.Scene.load(U.scene_path(b["scene"])) as s:
+        s.prepare()
+        nodes, prims = s.dump_bvh()
+        assert s.info["n_nodes"] == b["n_nodes"]
+        assert U.md5(nodes) == b["nodes_md5"]
+        assert U.md5(prims) == b["prims_md5"]
+
+
+def test_scene_info_standin():
+    with pt.Scene.load(U.scene_path("c3")) as s:
+        s.prepare()
+        i = s.info
+        assert (i["width"], i["height"], i["samples"], i["ray_depth"]) == (1920, 1080, 256, 6)
+        assert i["n_bvh_prims"] == 89929 and i["n_planes"] == 5 and i["n_emitters"] == 1
+        assert i["n_nodes"] == 179797
+        assert 0 < i["max_stack"] < i["tree_depth"] <= 64
+
+
+QUIRK_SCENES = {
+    # BG_COLOR right after a primitive block is re-dispatched with the stale
+    # NEW_PRIMITIVE line stream: its arguments are never read (background stays 0)
+    "stale_bg": "DIMENSIONS 16 16\nRAY_DEPTH 3\nSAMPLES 2\nCAMERA_POSITION 0 0 3\nCAMERA_RIGHT 1 0 0\n"
+                "CAMERA_UP 0 1 0\nCAMERA_FORWARD 0 0 -1\nCAMERA_FOV_X 1.2\nNEW_PRIMITIVE\nBOX 0.5 0.5 0.5\n"
+                "COLOR 1 0 0\nBG_COLOR 1 1 1\n",
+    # a type line resets the primitive (POSITION before it is lost); unknown commands skipped
+    "reset_and_unknown": "DIMENSIONS 16 12\nRAY_DEPTH 4\nSAMPLES 2\nBG_COLOR 0.2 0.3 0.4\nFOO 1 2\n"
+                         "CAMERA_POSITION 0 0 4\nCAMERA_RIGHT 1 0 0\nCAMERA_UP 0 1 0\nCAMERA_FORWARD 0 0 -1\n"
+                         "CAMERA_FOV_X 1.0\n\nNEW_PRIMITIVE\nPOSITION 3 3 3\nELLIPSOID 1 0.5 0.7\nCOLOR 0.9 0.9 0.2\n"
+                         "ROTATION 0.1 0.2 0.3 0.9\n\nNEW_PRIMITIVE\nPLANE 0 1 0\nPOSITION 0 -1 0\nCOLOR 1 1 1\n"
+                         "NEW_PRIMITIVE\nBOX 0.3 0.3 0.3\nPOSITION 0 1.5 0\nEMISSION 4 4 4\n",
+    # numeric extraction failure stores 0 and poisons the rest of the line
+    "bad_number": "DIMENSIONS 8 8\nRAY_DEPTH 2\nSAMPLES 1\nBG_COLOR 1 x 1\nCAMERA_POSITION 0 0 3\n"
+                  "CAMERA_RIGHT 1 0 0\nCAMERA_UP 0 1 0\nCAMERA_FORWARD 0 0 -1\nCAMERA_FOV_X 1.2\n"
+                  "NEW_PRIMITIVE\nTRIANGLE 0 0 0 1 0 0 0 1 0\nCOLOR 0.5 0.5 0.5\n",
+}
+
+
+@pytest.mark.parametrize("name", sorted(QUIRK_SCENES))
+def test_loader_quirks_match_oracle(tmp_path, name):
+    p = tmp_path / (name + ".txt")
+    p.write_text(QUIRK_SCENES[name])
+    o = U.OracleScene(str(p))
+    _, orad, _ = o.render()
+    with pt.Scene.load(str(p)) as s:
+        s.prepare()
+        assert s.info["width"] == o.W and s.info["height"] == o.H
+        nodes, prims = s.dump_bvh()
+        onodes, oprims = o.dump_bvh()
+        assert nodes == onodes and prims == oprims
+        rad = s.selftest_render_host(0, 0, o.W, o.H)
+    assert np.array_equal(rad.view(np.uint32), orad.view(np.uint32))
+
+
+def test_scene_errors():
+    with pytest.raises(pt.PTError) as e:
+        pt.Scene.load("/nonexistent/scene.txt")
+    assert e.value.code == pt.PT_E_IO
+    # only planes: the reference aborts in BVH_t; we report PT_E_SCENE
+    with pt.Scene.loads("DIMENSIONS 4 4\nSAMPLES 1\nRAY_DEPTH 1\nNEW_PRIMITIVE\nPLANE 0 1 0\n") as s:
+        with pytest.raises(pt.PTError) as e:
+            s.prepare()
+        assert e.value.code == pt.PT_E_SCENE
+    # a primitive block without a type line
+    with pt.Scene.loads("DIMENSIONS 4 4\nNEW_PRIMITIVE\nCOLOR 1 1 1\n") as s:
+        with pytest.raises(pt.PTError) as e:
+            s.prepare()
+        assert e.value.code == pt.PT_E_SCENE
+
+
+@pytest.mark.parametrize("name", sorted(M["trav"]))
+def test_exact_stack_traversal_matches_reference_kat(name):
+    t = M["trav"][name]
+    rays, ((ids, f, inter), _) = U.read_trav(name)
+    with pt.Scene.load(U.scene_path(t["scene"])) as s:
+        s.prepare()
+        gids, ghits = s.selftest_ray_intersection(rays)
+    assert np.array_equal(gids, ids)
+    hit = ids != -1
+    assert np.array_equal(ghits[hit, :4].view(np.uint32), f[hit].view(np.uint32))
+    assert np.array_equal(ghits[hit, 4].astype(np.uint32), inter[hit])
+
+
+HOST_RENDER = ["p51_64x48x16", "p52_64x48x16", "dragon_metal_64x64x8", "dragon_glass_64x64x8",
+               "hw3s2_48x48x8", "hw3s3_48x48x8", "hw3s4_48x48x8", "hw3s5_48x48x8", "rabbid_48x48x4",
+               "c2_win_240_200_24x24"]
+
+
+@pytest.mark.parametrize("name", HOST_RENDER)
+def test_device_integrator_on_host_bit_exact(name):
+    m, img, rad = U.golden_image(name)
+    with pt.Scene.load(U.golden_scene_path(name)) as s:
+        s.prepare()
+        if m["window"]:
+            x0, y0, w, h = m["window"]
+        else:
+            x0, y0, h, w = 0, 0, img.shape[0], img.shape[1]
+        got = s.selftest_render_host(x0, y0, w, h)
+    assert got.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
+    assert np.array_equal(U.oracle_tonemap(got).reshape(img.shape), img)
+
+
+def _gamma_table():
+    with pt.Scene.load(U.scene_path("practice5_1.txt")) as s:
+        s.prepare()
+        return s.gamma_table()
+
+
+def test_gamma_table_matches_host_quantiser():
+    thr = _gamma_table()
+    assert np.all(np.diff(thr[:255]) > 0) and np.isinf(thr[255])
+    v = thr[:255]
+    cand = np.concatenate([v, np.nextafter(v, np.float32(0)), np.nextafter(v, np.float32(2)),
+                           np.linspace(0, 1, 200001, dtype=np.float32)])
+    cand = np.clip(cand, 0, 1).astype(np.float32)
+    q = np.searchsorted(v, cand, side="right")   # = number of thresholds <= x (device rule)
+    ref = np.zeros(len(cand), np.uint8)
+    U.oracle().oracle_gamma_u8(len(cand), U._p(cand), U._p(ref))
+    assert np.array_equal(q, ref.astype(np.int64))
+
+
+@pytest.mark.slow
+def test_gamma_table_exhaustive():
+    # every float in [0, 1] quantises through the table exactly as glibc powf + round
+    thr = _gamma_table()
+    assert U.oracle().oracle_check_gamma_table(U._p(thr)) == 0
+
+
+def test_render_without_gpu_fails_loudly():
+    if U.gpu_available():
+        pytest.skip("GPU present")
+    with pt.Scene.load(U.scene_path("practice5_1.txt")) as s:
+        s.override(16, 16, 1, 0)
+        with pytest.raises(pt.PTError) as e:
+            s.render()
+        assert e.value.code in (pt.PT_E_NO_GPU, pt.PT_E_HIP)
