@@ -24,6 +24,16 @@ PT_OK = 0
 PT_E_INVALID, PT_E_IO, PT_E_SCENE, PT_E_NO_GPU, PT_E_HIP, PT_E_RCCL, PT_E_OOM = -1, -2, -3, -4, -5, -6, -7
 TRAVERSAL_EXACT = 0
 
+# One HIP runtime per process: PyTorch bundles its own libamdhip64 (soname
+# libamdhip64.so.7, but its users link the unversioned name), so loading
+# libpt.so first would map the system copy and torch would then map a second
+# runtime that cannot share the device.  Importing torch first makes libpt's
+# DT_NEEDED libamdhip64.so.7 bind to torch's already-loaded runtime.
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 if not os.path.exists(LIB_PATH):
     raise ImportError("libpt.so not built at %s (run `make -C raytracing-course_amd` or "
                       "`python -c 'import __graft_entry__ as g; g.build()'`)" % LIB_PATH)

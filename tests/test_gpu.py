@@ -113,3 +113,14 @@ def test_determinism_repeat(pt):
         a, ra, _ = s.render(radiance=True)
         b, rb, _ = s.render(radiance=True)
     assert np.array_equal(a, b) and np.array_equal(ra.view(np.uint32), rb.view(np.uint32))
+
+
+def test_cli_drop_in_config1(pt, tmp_path):
+    # build.sh/run.sh surface: `pt_render scene.txt out.ppm` (hw5/run.sh:1-2)
+    import subprocess
+    out = tmp_path / "c1.ppm"
+    exe = U.os.path.join(U.PKG, "build", "pt_render")
+    r = subprocess.run([exe, U.scene_path("c1"), str(out)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "Loading: [ ########## 100% ]" in r.stdout
+    assert U.md5(out.read_bytes()) == M["full"]["c1"]["md5"]
