@@ -131,6 +131,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, nargs=2, default=[480, 270])
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
+    ap.add_argument("--traversal", default="replay", choices=["replay", "exact"])
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -161,7 +162,8 @@ def main():
     t_sess = time.perf_counter()
     info = scene.info
     W, H = info["width"], info["height"]
-    ss = pt.Session(scene, device=local, rank=rank, world=world)
+    trav = pt.TRAVERSAL_REPLAY if args.traversal == "replay" else pt.TRAVERSAL_EXACT
+    ss = pt.Session(scene, device=local, rank=rank, world=world, traversal=trav)
     ss.sync()
     t_ready = time.perf_counter()
     for _ in range(args.warmup):
@@ -185,10 +187,12 @@ def main():
     rays = st1["rays"] - st0["rays"]
     nodes = st1["node_visits"] - st0["node_visits"]
     ptests = st1["prim_tests"] - st0["prim_tests"]
+    auxv = st1["aux_visits"] - st0["aux_visits"]
+    fb = st1["fallbacks"] - st0["fallbacks"]
     kms = st1["kernel_ms"] - st0["kernel_ms"]
     errs = st1["errors"]
-    t = torch.tensor([elapsed, float(rays), float(nodes), float(ptests), kms, float(errs)], dtype=torch.float64,
-                     device=device)
+    t = torch.tensor([elapsed, float(rays), float(nodes), float(ptests), kms, float(errs), float(auxv), float(fb)],
+                     dtype=torch.float64, device=device)
     if world > 1:
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -201,7 +205,7 @@ def main():
         total_rays = float(tsum[1])
         # roofline of k_trace: algorithmic bytes per launch / mean launch time (rank 0's launches)
         launches = args.steps
-        alg_bytes = (nodes * st1["node_bytes"] + ptests * st1["prim_bytes"]) / launches
+        alg_bytes = (nodes * st1["node_bytes"] + ptests * st1["prim_bytes"] + auxv * st1["aux_bytes"]) / launches
         launch_s = (kms / 1e3) / launches
         achieved = alg_bytes / launch_s / 1e9 if launch_s > 0 else 0.0
         traffic = None
@@ -228,19 +232,23 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: md5-pinned 89,928-triangle dragon stand-in (SURVEY §8d), per-pixel reference seeds",
-            "config": {"workload": "config 3: %s %dx%d, %d spp per step (of 256), RAY_DEPTH %d; exact reference-tree "
-                                   "traversal" % (args.config, W, H, args.spp_per_step, info["ray_depth"]),
+            "config": {"workload": "config 3: %s %dx%d, %d spp per step (of 256), RAY_DEPTH %d; %s traversal of the "
+                                   "reference tree (bit-exact)" % (args.config, W, H, args.spp_per_step,
+                                                                   info["ray_depth"], args.traversal),
                        "pixels": W * H, "samples_per_step": W * H * args.spp_per_step,
                        "parallelism": "pixel tiles x%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_trace", "alg_bytes_per_launch": alg_bytes, "launch_ms": launch_s * 1e3,
                          "traffic_source": traffic_src,
-                         "note": "algorithmic = node records (32 B) + leaf primitive records (80 B) fetched; "
-                                 "working set is L2/MALL-resident so DRAM traffic << algorithmic"},
+                         "note": "algorithmic = reference node records (32 B) + aux BVH nodes (64 B) + leaf "
+                                 "primitive records (80 B) fetched; the ~24 MB working set is L2/MALL-resident, "
+                                 "so DRAM traffic << algorithmic"},
             "rays": total_rays,
             "msamples_per_s": W * H * args.spp_per_step * args.steps / T / 1e6,
             "node_visits_per_ray": float(tsum[2]) / max(total_rays, 1),
+            "aux_visits_per_ray": float(tsum[6]) / max(total_rays, 1),
+            "fallback_rate": float(tsum[7]) / max(total_rays, 1),
             "exactness_errors": int(tsum[5]),
             "wall": {"load_s": t_prep - t_load, "prepare_bvh_s": t_sess - t_prep, "session_upload_s": t_ready - t_sess},
             "framebuffer_gathered": img is not None and img.shape == (H, W, 3),

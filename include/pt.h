@@ -58,6 +58,7 @@ typedef struct pt_scene_info {
     uint32_t width, height, samples, ray_depth;
     uint32_t n_prims, n_bvh_prims, n_planes, n_emitters;
     uint32_t n_nodes, tree_depth, max_stack;   /* max_stack = max pending right children */
+    uint32_t n_aux_nodes, aux_depth;
     uint32_t n_warnings;
 } pt_scene_info;
 int pt_scene_get_info(const pt_scene* s, pt_scene_info* info);
@@ -73,7 +74,12 @@ int pt_scene_dump_bvh(const pt_scene* s, void* nodes_out, size_t nodes_bytes, vo
 void pt_scene_free(pt_scene* s);
 
 /* ---------------------------------------------------------------- render */
-enum { PT_TRAVERSAL_EXACT = 0 /* reference-tree stack DFS, exact pruning semantics */ };
+enum {
+    PT_TRAVERSAL_REPLAY = 0, /* default: candidate replay -- auxiliary BVH enumerates the reference
+                                leaves the ray can reach, the reference's exact pruning is replayed
+                                on their root paths only (bit-identical results) */
+    PT_TRAVERSAL_EXACT = 1   /* full reference-tree stack DFS, exact pruning semantics */
+};
 
 typedef struct pt_render_opts {
     int32_t device;          /* first HIP device (default 0) */
@@ -95,11 +101,14 @@ typedef struct pt_stats {
     uint64_t plane_tests;
     uint64_t samples;        /* pixel samples traced */
     uint64_t errors;         /* exactness guards tripped (must be 0) */
+    uint64_t aux_visits;     /* auxiliary BVH node visits (replay traversal) */
+    uint64_t fallbacks;      /* queries that took the exact stack DFS under replay */
     double kernel_ms;        /* sum of trace-kernel time (HIP events) */
     double resolve_ms;
     double wall_ms;          /* pt_render: upload + render + gather + tonemap */
-    uint64_t node_bytes;     /* bytes of one node record / primitive record */
+    uint64_t node_bytes;     /* bytes of one node record / primitive record / aux node */
     uint64_t prim_bytes;
+    uint64_t aux_bytes;
 } pt_stats;
 
 /* Scene::Render minus the stream write: renders W*H*3 u8 (row-major, top row
@@ -156,9 +165,10 @@ int pt_abi_version(void);
 /* ------------------------------------------------------------ test hooks
  * Host execution of the device traversal code (pt_trace.h) for CPU unit
  * tests of the stack-DFS logic.  Never used by pt_render. */
-int pt_selftest_ray_intersection(pt_scene* s, uint32_t n, const float* rays, int32_t* ids, float* hits);
-int pt_selftest_render_host(pt_scene* s, uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, uint32_t spp,
-                            float* radiance);
+int pt_selftest_ray_intersection(pt_scene* s, int32_t traversal, uint32_t n, const float* rays, int32_t* ids,
+                                 float* hits, uint64_t* counters8);
+int pt_selftest_render_host(pt_scene* s, int32_t traversal, uint32_t x0, uint32_t y0, uint32_t w, uint32_t h,
+                            uint32_t spp, float* radiance);
 /* the 256-entry gamma threshold table used by the device tonemap */
 int pt_selftest_gamma_table(const pt_scene* s, float* thr256);
 

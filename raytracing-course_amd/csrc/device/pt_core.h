@@ -164,19 +164,26 @@ PT_HD float rng_normal(Rng& r) {
 // Device records (built by host/bvh_build.cpp, uploaded once per device):
 //  Node  (32 B, reference preorder; left child of an interior node = index+1)
 //    a = {center.x, center.y, center.z, s.x}   center = 0.5f*(max+min), s = 0.5f*(max-min)
-//    b = {s.y, s.z, u32 ref, u32 count}        interior: ref = right child, count = 0
-//                                              leaf:     ref = first prim, count >= 1
+//    b = {s.y, s.z, u32 ref, u32 info}         interior: ref = right child, info = 0x80000000 | end
+//                                                        (end = one past the subtree in preorder)
+//                                              leaf:     ref = first prim, info = count (>= 1)
+//  AuxNode (64 B): auxiliary BVH2 over the reference leaf boxes (host/aux_bvh.cpp)
+//    a = {c0.lo.xyz, c0.hi.x}, b = {c0.hi.yz, c1.lo.xy}, c = {c1.lo.z, c1.hi.xyz},
+//    d = {code0, code1, -, -}: code = aux node index, or 0x80000000 | reference leaf node, or ~0 (none)
 //  Prim  (80 B): p0 = {pos.xyz, type}, p1 = {rot.xyzw}, p2 = {a.xyz, -}, p3 = {b.xyz, c.x}, p4 = {c.y, c.z, -, -}
 //  Shade (32 B): s0 = {col.xyz, ior}, s1 = {emission.xyz, material}
 enum : uint32_t { T_PLANE = 1, T_BOX = 2, T_ELLIPSOID = 4, T_TRIANGLE = 8 };  // include/primitives.h:13-18
 enum : uint32_t { M_DIFFUSE = 0, M_METALLIC = 1, M_DIELECTRIC = 2 };         // include/materials.h:4-6
 
 struct Node { F4 a, b; };
+struct AuxNode { F4 a, b, c, d; };
+#define PT_NODE_INTERIOR 0x80000000u
 struct Prim { F4 p0, p1, p2, p3, p4; };
 struct Shade { F4 s0, s1; };
 
 struct SceneView {
     const Node* nodes;
+    const AuxNode* aux;         // auxiliary BVH (may be null: exact stack DFS only)
     const Prim* prims;
     const Shade* shade;
     const uint32_t* planes;     // prim indices of planes (tested first, in order)

@@ -38,7 +38,8 @@ struct TraceParams {
     TileMap tm;
     PixelState st;
     uint32_t* vscratch;          // 3 * depth * n_slots
-    unsigned long long* counters; // rays, nodes, prim tests, plane tests, errors
+    unsigned long long* counters; // rays, nodes, prim tests, plane tests, errors, aux visits, fallbacks
+    ReplayCfg cfg;
     uint32_t depth;
     uint32_t spp;
 };

@@ -4,7 +4,8 @@
 //   k_trace    advance every owned pixel by `spp` samples (src/scene.cpp:189-203):
 //              one pixel per lane, 16x16-pixel tiles per 256-thread workgroup
 //              (a wave = 16x4 pixels: neighbouring rays walk the same nodes);
-//              the traversal stack lives in LDS ([entry][lane], conflict-free),
+//              per-lane traversal state (aux stack, candidate list, or the exact
+//              DFS stack) lives in LDS ([word][lane], conflict-free),
 //              the per-vertex fold records in a lane-strided HBM scratch
 //   k_resolve  mean = (1/S)*sum, ACES + saturate (f32) and the exact gamma/8-bit
 //              threshold table, packed per tile for the framebuffer gather
@@ -17,9 +18,10 @@
 
 namespace pt {
 
-struct LdsStack {
+// per-lane word memory in LDS, [word][lane] (consecutive lanes -> consecutive banks)
+struct LdsMem {
     uint32_t* base;
-    __device__ __forceinline__ void push(uint32_t i, uint32_t v) { base[i * 256u] = v; }
+    __device__ __forceinline__ void set(uint32_t i, uint32_t v) { base[i * 256u] = v; }
     __device__ __forceinline__ uint32_t get(uint32_t i) const { return base[i * 256u]; }
 };
 
@@ -73,7 +75,7 @@ __global__ void __launch_bounds__(256) k_trace(TraceParams P) {
     uint32_t x, y;
     const bool ok = slot_pixel(P.tm, blockIdx.x, threadIdx.x, x, y);
     Counts C;
-    C.rays = C.nodes = C.ptests = C.planes = 0ull;
+    C.rays = C.nodes = C.ptests = C.planes = C.aux = C.fallbacks = 0ull;
     C.errs = 0u;
     if (ok) {
         Rng R;
@@ -81,14 +83,14 @@ __global__ void __launch_bounds__(256) k_trace(TraceParams P) {
         R.saved = P.st.rng_saved[slot];
         R.saved_ok = P.st.rng_flag[slot];
         f3 sum = mk3(P.st.sum[slot], P.st.sum[P.st.n_slots + slot], P.st.sum[2u * P.st.n_slots + slot]);
-        LdsStack stk{lds_stack + threadIdx.x};
+        LdsMem stk{lds_stack + threadIdx.x};
         HbmVStore vs{P.vscratch + slot, P.st.n_slots};
         const float fxb = (float)x, fyb = (float)y;
         for (uint32_t s = 0; s < P.spp; ++s) {
             const float fx = fxb + rng_uniform(R);
             const float fy = fyb + rng_uniform(R);
             const Ray ray = camera_ray(P.cam, fx, fy);
-            sum = sum + trace_path(P.S, ray, P.depth, R, stk, vs, C);
+            sum = sum + trace_path(P.S, P.cfg, ray, P.depth, R, stk, vs, C);
         }
         P.st.rng_x[slot] = R.x;
         P.st.rng_saved[slot] = R.saved;
@@ -102,6 +104,8 @@ __global__ void __launch_bounds__(256) k_trace(TraceParams P) {
     wave_add_u64(P.counters + 2, C.ptests);
     wave_add_u64(P.counters + 3, C.planes);
     wave_add_u64(P.counters + 4, (unsigned long long)C.errs);
+    wave_add_u64(P.counters + 5, C.aux);
+    wave_add_u64(P.counters + 6, C.fallbacks);
 }
 
 __global__ void __launch_bounds__(256) k_resolve(ResolveParams P) {

@@ -29,6 +29,8 @@ struct Counts {
     uint64_t nodes;       // BVH node records fetched + slab-tested
     uint64_t ptests;      // leaf primitive tests
     uint64_t planes;      // plane tests
+    uint64_t aux;         // auxiliary BVH node visits (candidate replay)
+    uint64_t fallbacks;   // rays that took the exact stack DFS although replay was enabled
     uint32_t errs;        // hit-list overflow (must stay 0; the result is then not exact)
 };
 
@@ -50,7 +52,7 @@ PT_HD Ray camera_ray(const CamView& c, float x, float y) {
 
 #define PT_HITLIST 6
 
-// Exact reference traversal.  `stk` provides push(i, v) / get(i) of u32.
+// Exact reference traversal.  `stk` is per-lane word memory: set(i, v) / get(i).
 template <class Stack>
 PT_HD int bvh_exact(const SceneView& S, const Ray& ray, float cb, Stack& stk, Hit& best, Counts& C) {
     int best_id = -1;
@@ -73,7 +75,7 @@ PT_HD int bvh_exact(const SceneView& S, const Ray& ray, float cb, Stack& stk, Hi
         bool descend = false;
         if (hit && !(cb < t && !interior)) {
             const uint32_t ref = f2u(nd.b.z), cnt = f2u(nd.b.w);
-            if (cnt != 0u) {
+            if (!(cnt & PT_NODE_INTERIOR)) {
                 // leaf: first-min over its primitives (strict <), src/bvh.cpp:205-213
                 Hit lb;
                 lb.t = PT_INF;
@@ -105,7 +107,7 @@ PT_HD int bvh_exact(const SceneView& S, const Ray& ray, float cb, Stack& stk, Hi
                     if (lb.t < best.t) { best = lb; best_id = lid; }
                 }
             } else {
-                stk.push(sp++, ref | (nh << 24));
+                stk.set(sp++, ref | (nh << 24));
                 node = node + 1u;
                 descend = true;
             }
@@ -126,9 +128,196 @@ PT_HD int bvh_exact(const SceneView& S, const Ray& ray, float cb, Stack& stk, Hi
     return best_id;
 }
 
+// ---------------------------------------------------------------------------
+// Candidate replay: the same traversal semantics, evaluated only where they can
+// matter.  A reference leaf can contribute a hit only if its own slab test
+// passes, so (1) the auxiliary BVH enumerates every leaf whose exact slab test
+// passes (conservative fast box tests, then the exact test), (2) the leaves are
+// processed in reference preorder (= the DFS order of BVH_t::Intersect_), and
+// (3) for each one the root->leaf path is replayed with the reference's tests
+// and bounds: a node is skipped iff slab miss or (bound < t_entry && !interior);
+// going right at node a sets bound = min{hits in leaves (a, right(a))} if any,
+// else keeps bound(a).  Subtrees without candidates return no hit in the
+// reference, so they change neither the result nor any bound.  Result and
+// pruning are therefore identical to the full recursion (proof: DESIGN.md §4).
+// Per-lane word memory `L`: [0, as) aux traversal stack, [as, as+cap) candidates.
+#define PT_REPLAY_HITS 4
+
+struct ReplayCfg {
+    uint32_t as;    // aux stack words
+    uint32_t cap;   // candidate list words per pass
+};
+
+// conservative ray/box test on an inflated auxiliary box (o*inv precomputed)
+PT_HD bool aux_box(float lx, float ly, float lz, float hx, float hy, float hz, f3 inv, f3 oinv) {
+    const float ax = fmaf(lx, inv.x, -oinv.x), bx = fmaf(hx, inv.x, -oinv.x);
+    const float ay = fmaf(ly, inv.y, -oinv.y), by = fmaf(hy, inv.y, -oinv.y);
+    const float az = fmaf(lz, inv.z, -oinv.z), bz = fmaf(hz, inv.z, -oinv.z);
+    const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    return tn <= tf && tf >= 0.f;
+}
+
+// exact reference slab test of node `n` (AABB_t::Intersect, src/bvh.cpp:89-93)
+PT_HD bool node_slab(const Node& nd, const Ray& ray, float& t, uint32_t& interior) {
+    const f3 c = mk3(nd.a.x, nd.a.y, nd.a.z);
+    const f3 s = mk3(nd.a.w, nd.b.x, nd.b.y);
+    return slab(ray.o + -1.f * c, ray.d, s, t, interior);
+}
+
+PT_HD bool replay_ok_ray(const Ray& r) {
+    // rays with a (near-)zero or non-finite direction component, or a non-finite
+    // origin, take the exact stack DFS (NaN/inf slab semantics)
+    const float m = 1e-30f, big = 3e38f;
+    return fabsf(r.d.x) > m && fabsf(r.d.y) > m && fabsf(r.d.z) > m && fabsf(r.d.x) < big &&
+           fabsf(r.d.y) < big && fabsf(r.d.z) < big && fabsf(r.o.x) < big && fabsf(r.o.y) < big &&
+           fabsf(r.o.z) < big;
+}
+
+// returns best hit id (-1 none); sets `fallback` when the exact DFS must be used instead
+template <class Mem>
+PT_HD int bvh_replay(const SceneView& S, const ReplayCfg& cfg, const Ray& ray, float P, Mem& L, Hit& best,
+                     Counts& C, bool& fallback) {
+    fallback = false;
+    int best_id = -1;
+    best.t = PT_INF;
+    const f3 inv = mk3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
+    const f3 oinv = mk3(ray.o.x * inv.x, ray.o.y * inv.y, ray.o.z * inv.z);
+    uint32_t h_idx[PT_REPLAY_HITS];
+    float h_t[PT_REPLAY_HITS];
+    uint32_t nh = 0;
+    uint32_t lb = 0;  // every candidate below lb has been processed
+    for (;;) {
+        // ---- pass: collect the `cap` smallest candidate leaves >= lb (unsorted), track overflow
+        uint32_t n = 0, mx = 0, mxpos = 0;
+        bool overflow = false;
+        uint32_t sp = 0;
+        uint32_t node = 0;
+        for (;;) {
+            const AuxNode an = S.aux[node];
+            C.aux++;
+            const uint32_t c0 = f2u(an.d.x), c1 = f2u(an.d.y);
+            const bool h0 = c0 != 0xffffffffu && aux_box(an.a.x, an.a.y, an.a.z, an.a.w, an.b.x, an.b.y, inv, oinv);
+            const bool h1 = c1 != 0xffffffffu && aux_box(an.b.z, an.b.w, an.c.x, an.c.y, an.c.z, an.c.w, inv, oinv);
+            uint32_t next = 0xffffffffu;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const bool hk = k == 0 ? h0 : h1;
+                const uint32_t code = k == 0 ? c0 : c1;
+                if (!hk) continue;
+                if (code & 0x80000000u) {
+                    const uint32_t leaf = code & 0x7fffffffu;
+                    if (leaf < lb) continue;
+                    float t;
+                    uint32_t in;
+                    C.nodes++;
+                    if (!node_slab(S.nodes[leaf], ray, t, in)) continue;
+                    if (n < cfg.cap) {
+                        L.set(cfg.as + n, leaf);
+                        if (leaf > mx || n == 0) { mx = leaf; mxpos = n; }
+                        ++n;
+                    } else {
+                        overflow = true;
+                        if (leaf < mx) {   // keep the cap smallest: replace the largest
+                            L.set(cfg.as + mxpos, leaf);
+                            mx = 0;
+                            for (uint32_t q = 0; q < n; ++q) {
+                                const uint32_t v = L.get(cfg.as + q);
+                                if (v >= mx) { mx = v; mxpos = q; }
+                            }
+                        }
+                    }
+                } else if (next == 0xffffffffu) {
+                    next = code;
+                } else {
+                    L.set(sp++, code);
+                }
+            }
+            if (next != 0xffffffffu) { node = next; continue; }
+            if (sp == 0u) break;
+            node = L.get(--sp);
+        }
+        if (n == 0u) break;
+        // ---- sort the candidates (insertion sort, ascending preorder index)
+        for (uint32_t i = 1; i < n; ++i) {
+            const uint32_t v = L.get(cfg.as + i);
+            uint32_t j = i;
+            while (j > 0u) {
+                const uint32_t u = L.get(cfg.as + j - 1u);
+                if (u <= v) break;
+                L.set(cfg.as + j, u);
+                --j;
+            }
+            L.set(cfg.as + j, v);
+        }
+        // ---- replay root -> candidate paths in preorder
+        uint32_t skip = lb;
+        for (uint32_t k = 0; k < n; ++k) {
+            const uint32_t cand = L.get(cfg.as + k);
+            if (cand < skip) continue;
+            uint32_t a = 0;
+            float bound = P;
+            for (;;) {
+                const Node nd = S.nodes[a];
+                C.nodes++;
+                float t;
+                uint32_t in;
+                const bool hit = node_slab(nd, ray, t, in);
+                const uint32_t ref = f2u(nd.b.z), info = f2u(nd.b.w);
+                if (!hit || (bound < t && !in)) {
+                    skip = (info & PT_NODE_INTERIOR) ? (info & 0x7fffffffu) : a + 1u;
+                    break;
+                }
+                if (a == cand) {
+                    // leaf reached: first-min over its primitives (src/bvh.cpp:205-213)
+                    Hit lbh;
+                    lbh.t = PT_INF;
+                    int lid = -1;
+                    for (uint32_t i = ref; i < ref + info; ++i) {
+                        Hit h;
+                        C.ptests++;
+                        if (prim_intersect(S.prims[i], ray, h) && h.t < lbh.t) { lbh = h; lid = (int)i; }
+                    }
+                    if (lid >= 0) {
+                        if (nh == PT_REPLAY_HITS) { fallback = true; return -1; }
+#pragma unroll
+                        for (int q = 0; q < PT_REPLAY_HITS; ++q)
+                            if ((uint32_t)q == nh) { h_idx[q] = cand; h_t[q] = lbh.t; }
+                        ++nh;
+                        if (lbh.t < best.t) { best = lbh; best_id = lid; }
+                    }
+                    skip = cand + 1u;
+                    break;
+                }
+                if (cand < ref) {
+                    a = a + 1u;                      // left child: same bound
+                } else {
+                    // right child: bound = best hit of the left sibling's subtree, if any
+                    float m = bound;
+                    bool any = false;
+#pragma unroll
+                    for (int q = 0; q < PT_REPLAY_HITS; ++q) {
+                        if ((uint32_t)q < nh && h_idx[q] > a && h_idx[q] < ref) {
+                            if (!any || h_t[q] < m) m = h_t[q];
+                            any = true;
+                        }
+                    }
+                    bound = m;
+                    a = ref;
+                }
+            }
+        }
+        if (!overflow) break;
+        const uint32_t last = L.get(cfg.as + n - 1u) + 1u;
+        lb = skip > last ? skip : last;
+    }
+    return best_id;
+}
+
 // src/scene.cpp:46-77: planes first (strict <), then the BVH bounded by the plane t
 template <class Stack>
-PT_HD int ray_intersection(const SceneView& S, const Ray& ray, Stack& stk, Hit& out, Counts& C) {
+PT_HD int ray_intersection(const SceneView& S, const ReplayCfg& cfg, const Ray& ray, Stack& stk, Hit& out,
+                           Counts& C) {
     int id = -1;
     float closest = PT_INF;
     for (uint32_t k = 0; k < S.n_planes; ++k) {
@@ -138,7 +327,13 @@ PT_HD int ray_intersection(const SceneView& S, const Ray& ray, Stack& stk, Hit& 
         if (prim_intersect(S.prims[pi], ray, h) && h.t < closest) { closest = h.t; out = h; id = (int)pi; }
     }
     Hit bh;
-    const int bid = bvh_exact(S, ray, closest, stk, bh, C);
+    int bid;
+    bool fallback = true;
+    if (S.aux && replay_ok_ray(ray)) bid = bvh_replay(S, cfg, ray, closest, stk, bh, C, fallback);
+    if (fallback) {
+        if (S.aux) C.fallbacks++;
+        bid = bvh_exact(S, ray, closest, stk, bh, C);
+    }
     if (bid != -1 && bh.t < closest) { out = bh; id = bid; }
     return id;
 }
@@ -149,7 +344,8 @@ enum : uint32_t { V_TERM = 0u, V_DIFFUSE = 1u, V_COL = 2u, V_IDENT = 3u };
 // One camera sample: src/scene.cpp:189-203 (inner) + RayTrace :83-178.
 // `vs` provides put(k, idmode, s1, s2) / get(k, idmode, s1, s2) for k < depth.
 template <class Stack, class VStore>
-PT_HD f3 trace_path(const SceneView& S, Ray ray, uint32_t depth, Rng& R, Stack& stk, VStore& vs, Counts& C) {
+PT_HD f3 trace_path(const SceneView& S, const ReplayCfg& cfg, Ray ray, uint32_t depth, Rng& R, Stack& stk, VStore& vs,
+                    Counts& C) {
     const float eps = 1e-4f;  // Scene::eps, include/scene.h:56
     uint32_t nv = 0;
     f3 leaf = mk3(0.f, 0.f, 0.f);
@@ -157,7 +353,7 @@ PT_HD f3 trace_path(const SceneView& S, Ray ray, uint32_t depth, Rng& R, Stack& 
         if (rem == 0u) { leaf = mk3(0.f, 0.f, 0.f); break; }
         C.rays++;
         Hit h;
-        const int id = ray_intersection(S, ray, stk, h, C);
+        const int id = ray_intersection(S, cfg, ray, stk, h, C);
         if (id == -1) { leaf = S.bg; break; }
         const Shade sh = S.shade[id];
         const uint32_t mat = f2u(sh.s1.w);

@@ -46,7 +46,10 @@ struct DevScene {
     uint32_t* planes = nullptr;
     uint32_t* emitters = nullptr;
     float* thr = nullptr;
+    pt::AuxNode* aux = nullptr;
 };
+
+constexpr uint32_t kCandCap = 24;   // candidate-list words per lane (per replay pass)
 
 }  // namespace
 
@@ -59,7 +62,8 @@ struct pt_scene {
     std::vector<pt::Node> dnodes;
     std::vector<pt::Prim> dprims;
     std::vector<pt::Shade> dshade;
-    uint32_t tree_depth = 0, max_stack = 0;
+    std::vector<pt::AuxNode> aux;
+    uint32_t tree_depth = 0, max_stack = 0, aux_depth = 0;
     float thr[256];
     std::map<int, DevScene> dev;
     std::mutex mu;
@@ -80,7 +84,7 @@ struct pt_session {
     double kernel_ms = 0.0, resolve_ms = 0.0;
     uint64_t samples_done = 0;
     pt::CamView cam{};
-    int traversal = PT_TRAVERSAL_EXACT;
+    int traversal = PT_TRAVERSAL_REPLAY;
 };
 
 namespace {
@@ -88,6 +92,10 @@ namespace {
 // ------------------------------------------------------------- prepare ---
 void build_device_layout(pt_scene* s) {
     const auto& P = s->hs.prims;
+    // end[i] = one past node i's subtree in preorder
+    std::vector<uint32_t> end(s->nodes.size());
+    for (size_t k = s->nodes.size(); k-- > 0;)
+        end[k] = s->nodes[k].left == 0xFFFFFFFFu ? (uint32_t)k + 1u : end[s->nodes[k].right];
     s->dnodes.resize(s->nodes.size());
     for (size_t i = 0; i < s->nodes.size(); ++i) {
         const pth::HNode& n = s->nodes[i];
@@ -100,8 +108,8 @@ void build_device_layout(pt_scene* s) {
         const bool leaf = n.left == 0xFFFFFFFFu;
         if (!leaf && n.left != (uint32_t)i + 1u) throw std::runtime_error("BVH not in preorder");
         const uint32_t ref = leaf ? n.first : n.right;
-        const uint32_t cnt = leaf ? n.count : 0u;
-        if (leaf && cnt == 0u) throw std::runtime_error("empty BVH leaf");
+        const uint32_t cnt = leaf ? n.count : (PT_NODE_INTERIOR | end[i]);
+        if (leaf && (cnt == 0u || (cnt & PT_NODE_INTERIOR))) throw std::runtime_error("bad BVH leaf size");
         pt::Node d;
         d.a = pt::F4{c[0], c[1], c[2], h[0]};
         d.b = pt::F4{h[1], h[2], pt::u2f(ref), pt::u2f(cnt)};
@@ -172,6 +180,7 @@ int ensure_device_scene(pt_scene* s, int dev, DevScene** out) {
         return rc;
     std::vector<float> thr(s->thr, s->thr + 256);
     if ((rc = upload(&d.thr, thr))) return rc;
+    if ((rc = upload(&d.aux, s->aux))) return rc;
     s->dev[dev] = d;
     *out = &s->dev[dev];
     return PT_OK;
@@ -179,11 +188,25 @@ int ensure_device_scene(pt_scene* s, int dev, DevScene** out) {
 
 void free_device_scene(DevScene& d) {
     (void)hipFree(d.nodes); (void)hipFree(d.prims); (void)hipFree(d.shade);
-    (void)hipFree(d.planes); (void)hipFree(d.emitters); (void)hipFree(d.thr);
+    (void)hipFree(d.planes); (void)hipFree(d.emitters); (void)hipFree(d.thr); (void)hipFree(d.aux);
 }
 
-pt::SceneView host_view(const pt_scene* s) {
+// per-lane LDS words: replay needs [aux stack | candidates], the exact DFS its stack
+pt::ReplayCfg replay_cfg(const pt_scene* s) {
+    pt::ReplayCfg c;
+    c.as = std::max<uint32_t>(s->aux_depth, 1u);
+    c.cap = kCandCap;
+    return c;
+}
+uint32_t lane_words(const pt_scene* s, int traversal) {
+    const pt::ReplayCfg c = replay_cfg(s);
+    const uint32_t dfs = std::max<uint32_t>(s->max_stack, 1u);
+    return traversal == PT_TRAVERSAL_EXACT ? dfs : std::max(dfs, c.as + c.cap);
+}
+
+pt::SceneView host_view(const pt_scene* s, int traversal) {
     pt::SceneView v;
+    v.aux = traversal == PT_TRAVERSAL_EXACT ? nullptr : s->aux.data();
     v.nodes = s->dnodes.data();
     v.prims = s->dprims.data();
     v.shade = s->dshade.data();
@@ -301,6 +324,7 @@ int pt_scene_prepare(pt_scene* s) {
             if (p.type == pt::T_BOX || p.type == pt::T_ELLIPSOID) s->emitters.push_back(i);
         }
         build_device_layout(s);
+        pth::build_aux_bvh(s->nodes, s->aux, s->aux_depth);
         pth::build_gamma_thresholds(s->thr);
     } catch (const std::exception& e) {
         return fail(PT_E_SCENE, e.what());
@@ -323,6 +347,8 @@ int pt_scene_get_info(const pt_scene* s, pt_scene_info* info) {
     info->n_nodes = (uint32_t)s->nodes.size();
     info->tree_depth = s->tree_depth;
     info->max_stack = s->max_stack;
+    info->n_aux_nodes = (uint32_t)s->aux.size();
+    info->aux_depth = s->aux_depth;
     info->n_warnings = (uint32_t)s->hs.warnings.size();
     return PT_OK;
 }
@@ -437,6 +463,8 @@ int pt_session_trace(pt_session* ss, uint32_t spp) {
     DevScene& ds = ss->sc->dev[ss->dev];
     pt::TraceParams tp;
     const pt_scene* s = ss->sc;
+    tp.S.aux = ss->traversal == PT_TRAVERSAL_EXACT ? nullptr : ds.aux;
+    tp.cfg = replay_cfg(s);
     tp.S.nodes = ds.nodes;
     tp.S.prims = ds.prims;
     tp.S.shade = ds.shade;
@@ -452,7 +480,7 @@ int pt_session_trace(pt_session* ss, uint32_t spp) {
     tp.counters = ss->counters;
     tp.depth = ss->depth;
     tp.spp = spp;
-    const uint32_t lds = 256u * 4u * std::max<uint32_t>(s->max_stack, 1u);
+    const uint32_t lds = 256u * 4u * lane_words(s, ss->traversal);
     if (lds > 160u * 1024u) return fail(PT_E_SCENE, "BVH too deep for the LDS traversal stack");
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
@@ -518,6 +546,8 @@ int pt_session_stats(pt_session* ss, pt_stats* st) {
     st->prim_tests = c[2];
     st->plane_tests = c[3];
     st->errors = c[4];
+    st->aux_visits = c[5];
+    st->fallbacks = c[6];
     uint64_t px = 0;
     for (uint32_t t = 0; t < ss->n_tiles_local; ++t) {
         const uint32_t gt = t * ss->tm.world + ss->tm.rank;
@@ -530,6 +560,7 @@ int pt_session_stats(pt_session* ss, pt_stats* st) {
     st->resolve_ms = ss->resolve_ms;
     st->node_bytes = sizeof(pt::Node);
     st->prim_bytes = sizeof(pt::Prim);
+    st->aux_bytes = sizeof(pt::AuxNode);
     return PT_OK;
 }
 
@@ -657,6 +688,7 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
         if ((rc = pt_session_stats(x, &st))) return cleanup(rc);
         agg.rays += st.rays; agg.node_visits += st.node_visits; agg.prim_tests += st.prim_tests;
         agg.plane_tests += st.plane_tests; agg.samples += st.samples; agg.errors += st.errors;
+        agg.aux_visits += st.aux_visits; agg.fallbacks += st.fallbacks; agg.aux_bytes = st.aux_bytes;
         agg.kernel_ms = std::max(agg.kernel_ms, st.kernel_ms);
         agg.resolve_ms = std::max(agg.resolve_ms, st.resolve_ms);
         agg.node_bytes = st.node_bytes; agg.prim_bytes = st.prim_bytes;
@@ -682,7 +714,7 @@ int pt_write_ppm(const char* path, uint32_t W, uint32_t H, const uint8_t* rgb) {
 namespace {
 struct HostStack {
     std::vector<uint32_t> v;
-    void push(uint32_t i, uint32_t x) { if (v.size() <= i) v.resize(i + 1); v[i] = x; }
+    void set(uint32_t i, uint32_t x) { if (v.size() <= i) v.resize(i + 1); v[i] = x; }
     uint32_t get(uint32_t i) const { return v[i]; }
 };
 struct HostVStore {
@@ -697,10 +729,12 @@ struct HostVStore {
 };
 }  // namespace
 
-int pt_selftest_ray_intersection(pt_scene* s, uint32_t n, const float* rays, int32_t* ids, float* hits) {
+int pt_selftest_ray_intersection(pt_scene* s, int32_t traversal, uint32_t n, const float* rays, int32_t* ids,
+                                 float* hits, uint64_t* counters8) {
     int rc = pt_scene_prepare(s);
     if (rc) return rc;
-    const pt::SceneView V = host_view(s);
+    const pt::SceneView V = host_view(s, traversal);
+    const pt::ReplayCfg cfg = replay_cfg(s);
     HostStack stk;
     pt::Counts C{};
     for (uint32_t i = 0; i < n; ++i) {
@@ -708,7 +742,7 @@ int pt_selftest_ray_intersection(pt_scene* s, uint32_t n, const float* rays, int
         r.o = pt::mk3(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
         r.d = pt::mk3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
         pt::Hit h;
-        const int id = pt::ray_intersection(V, r, stk, h, C);
+        const int id = pt::ray_intersection(V, cfg, r, stk, h, C);
         ids[i] = id;
         const bool ok = id != -1;
         hits[5 * i] = ok ? h.t : 0.f;
@@ -717,14 +751,19 @@ int pt_selftest_ray_intersection(pt_scene* s, uint32_t n, const float* rays, int
         hits[5 * i + 3] = ok ? h.n.z : 0.f;
         hits[5 * i + 4] = ok ? (h.interior ? 1.f : 0.f) : 0.f;
     }
+    if (counters8) {
+        const uint64_t c[8] = {C.rays, C.nodes, C.ptests, C.planes, C.errs, C.aux, C.fallbacks, 0};
+        memcpy(counters8, c, sizeof(c));
+    }
     return C.errs ? fail(PT_E_INVALID, "hit list overflow") : PT_OK;
 }
 
-int pt_selftest_render_host(pt_scene* s, uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, uint32_t spp,
-                            float* radiance) {
+int pt_selftest_render_host(pt_scene* s, int32_t traversal, uint32_t x0, uint32_t y0, uint32_t w, uint32_t h,
+                            uint32_t spp, float* radiance) {
     int rc = pt_scene_prepare(s);
     if (rc) return rc;
-    const pt::SceneView V = host_view(s);
+    const pt::SceneView V = host_view(s, traversal);
+    const pt::ReplayCfg cfg = replay_cfg(s);
     const pt::CamView cam = make_cam(s);
     const uint32_t S = spp ? spp : s->hs.samples;
     const uint32_t nt = std::max(1u, std::thread::hardware_concurrency());
@@ -742,7 +781,7 @@ int pt_selftest_render_host(pt_scene* s, uint32_t x0, uint32_t y0, uint32_t w, u
                 for (uint32_t i = 0; i < S; ++i) {
                     const float fx = (float)x + pt::rng_uniform(R);
                     const float fy = (float)y + pt::rng_uniform(R);
-                    sum = sum + pt::trace_path(V, pt::camera_ray(cam, fx, fy), s->hs.depth, R, stk, vs, C);
+                    sum = sum + pt::trace_path(V, cfg, pt::camera_ray(cam, fx, fy), s->hs.depth, R, stk, vs, C);
                 }
                 const pt::f3 m = (1.f / (float)S) * sum;
                 radiance[3 * k] = m.x; radiance[3 * k + 1] = m.y; radiance[3 * k + 2] = m.z;

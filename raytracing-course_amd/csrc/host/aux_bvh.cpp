@@ -1,0 +1,170 @@
+// aux_bvh.cpp -- auxiliary spatial BVH over the reference tree's LEAF boxes.
+//
+// Used only to enumerate, per ray, the reference leaves whose box the ray's
+// line meets (the "candidates"); the exact reference traversal is then
+// replayed over those candidates alone (pt_trace.h: bvh_replay).  Its boxes
+// are the reference leaf boxes inflated outward (relative + absolute margin)
+// so that the fast, inverse-direction box test is conservative with respect
+// to the reference's exact center/half-size slab test; every candidate is
+// re-checked with that exact test before it is used.
+//
+// Build: binned SAH (32 bins, centroid axis), BVH2, one reference leaf per
+// auxiliary leaf slot, nodes in DFS preorder.
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <stdexcept>
+#include <vector>
+
+#include "pt_scene.h"
+
+namespace pth {
+namespace {
+
+struct Box {
+    float lo[3], hi[3];
+};
+
+inline void grow(Box& b, const Box& o) {
+    for (int a = 0; a < 3; ++a) {
+        b.lo[a] = std::min(b.lo[a], o.lo[a]);
+        b.hi[a] = std::max(b.hi[a], o.hi[a]);
+    }
+}
+inline Box empty_box() {
+    Box b;
+    for (int a = 0; a < 3; ++a) { b.lo[a] = INFINITY; b.hi[a] = -INFINITY; }
+    return b;
+}
+inline float area(const Box& b) {
+    const float dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
+    if (!(dx >= 0.f)) return 0.f;
+    return dx * dy + dx * dz + dy * dz;
+}
+// outward inflation: |x| * 2^-16 + 2^-17 (~1.5e-5 relative, 7.6e-6 absolute)
+inline float down(float x) { return (float)((double)x - fabs((double)x) * 1.52587890625e-05 - 7.62939453125e-06); }
+inline float up(float x) { return (float)((double)x + fabs((double)x) * 1.52587890625e-05 + 7.62939453125e-06); }
+
+struct Builder {
+    std::vector<Box> box;        // per item (reference leaf)
+    std::vector<float> cen[3];
+    std::vector<uint32_t> item;  // reference leaf node index per item
+    std::vector<pt::AuxNode>& out;
+    uint32_t max_depth = 0;
+
+    explicit Builder(std::vector<pt::AuxNode>& o) : out(o) {}
+
+    static void set_child(pt::AuxNode& n, int k, const Box& b, uint32_t code) {
+        float* f = reinterpret_cast<float*>(&n);
+        // layout: a = {c0.lo.xyz, c0.hi.x}, b = {c0.hi.yz, c1.lo.xy}, c = {c1.lo.z, c1.hi.xyz}, d = {code0, code1, -, -}
+        if (k == 0) {
+            f[0] = b.lo[0]; f[1] = b.lo[1]; f[2] = b.lo[2]; f[3] = b.hi[0]; f[4] = b.hi[1]; f[5] = b.hi[2];
+        } else {
+            f[6] = b.lo[0]; f[7] = b.lo[1]; f[8] = b.lo[2]; f[9] = b.hi[0]; f[10] = b.hi[1]; f[11] = b.hi[2];
+        }
+        uint32_t* u = reinterpret_cast<uint32_t*>(&n);
+        u[12 + k] = code;
+    }
+
+    // returns the child code of the subtree over items [b, e) and its bounds
+    uint32_t build(uint32_t b, uint32_t e, Box& bounds, uint32_t depth) {
+        bounds = empty_box();
+        for (uint32_t i = b; i < e; ++i) grow(bounds, box[i]);
+        if (e - b == 1) return 0x80000000u | item[b];
+        max_depth = std::max(max_depth, depth + 1);
+        // centroid bounds
+        float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (uint32_t i = b; i < e; ++i)
+            for (int a = 0; a < 3; ++a) { clo[a] = std::min(clo[a], cen[a][i]); chi[a] = std::max(chi[a], cen[a][i]); }
+        constexpr int NB = 32;
+        float best_cost = INFINITY;
+        int best_axis = -1, best_split = 0;
+        for (int a = 0; a < 3; ++a) {
+            const float ext = chi[a] - clo[a];
+            if (!(ext > 0.f)) continue;
+            Box bb[NB];
+            uint32_t cnt[NB] = {0};
+            for (int k = 0; k < NB; ++k) bb[k] = empty_box();
+            const float sc = NB / ext;
+            for (uint32_t i = b; i < e; ++i) {
+                int k = (int)((cen[a][i] - clo[a]) * sc);
+                k = std::min(std::max(k, 0), NB - 1);
+                grow(bb[k], box[i]);
+                cnt[k]++;
+            }
+            Box lb[NB];
+            uint32_t lc[NB];
+            Box acc = empty_box();
+            uint32_t c = 0;
+            for (int k = 0; k < NB; ++k) { grow(acc, bb[k]); c += cnt[k]; lb[k] = acc; lc[k] = c; }
+            acc = empty_box();
+            c = 0;
+            for (int k = NB - 1; k >= 1; --k) {
+                grow(acc, bb[k]);
+                c += cnt[k];
+                if (lc[k - 1] == 0 || c == 0) continue;
+                const float cost = area(lb[k - 1]) * (float)lc[k - 1] + area(acc) * (float)c;
+                if (cost < best_cost) { best_cost = cost; best_axis = a; best_split = k; }
+            }
+        }
+        uint32_t mid;
+        if (best_axis < 0) {
+            mid = b + (e - b) / 2;  // all centroids coincide: median split by index
+        } else {
+            const float ext = chi[best_axis] - clo[best_axis];
+            const float sc = NB / ext;
+            uint32_t i = b, j = e;
+            while (i < j) {
+                int k = (int)((cen[best_axis][i] - clo[best_axis]) * sc);
+                k = std::min(std::max(k, 0), NB - 1);
+                if (k < best_split) { ++i; continue; }
+                --j;
+                std::swap(box[i], box[j]);
+                std::swap(item[i], item[j]);
+                for (int a = 0; a < 3; ++a) std::swap(cen[a][i], cen[a][j]);
+            }
+            mid = i;
+            if (mid == b || mid == e) mid = b + (e - b) / 2;
+        }
+        const uint32_t self = (uint32_t)out.size();
+        out.emplace_back();
+        Box b0, b1;
+        const uint32_t c0 = build(b, mid, b0, depth + 1);
+        const uint32_t c1 = build(mid, e, b1, depth + 1);
+        set_child(out[self], 0, b0, c0);
+        set_child(out[self], 1, b1, c1);
+        return self;
+    }
+};
+
+}  // namespace
+
+void build_aux_bvh(const std::vector<HNode>& nodes, std::vector<pt::AuxNode>& out, uint32_t& max_depth) {
+    out.clear();
+    Builder B(out);
+    for (uint32_t i = 0; i < (uint32_t)nodes.size(); ++i) {
+        const HNode& n = nodes[i];
+        if (n.left != 0xFFFFFFFFu) continue;
+        Box bx;
+        for (int a = 0; a < 3; ++a) { bx.lo[a] = down(n.mn[a]); bx.hi[a] = up(n.mx[a]); }
+        B.box.push_back(bx);
+        for (int a = 0; a < 3; ++a) B.cen[a].push_back(0.5f * (bx.lo[a] + bx.hi[a]));
+        B.item.push_back(i);
+    }
+    if (B.item.empty()) throw std::runtime_error("no BVH leaves");
+    Box root;
+    if (B.item.size() == 1) {
+        pt::AuxNode n;
+        memset(&n, 0, sizeof(n));
+        Builder::set_child(n, 0, B.box[0], 0x80000000u | B.item[0]);
+        Builder::set_child(n, 1, empty_box(), 0xFFFFFFFFu);
+        out.push_back(n);
+        max_depth = 1;
+        return;
+    }
+    B.build(0, (uint32_t)B.item.size(), root, 0);
+    max_depth = B.max_depth;
+}
+
+}  // namespace pth

@@ -46,6 +46,9 @@ void parse_scene(const char* text, size_t len, HScene& S);
 // BVH_t::InitTree and appends nodes in preorder.
 void build_reference_bvh(std::vector<HPrim>& prims, uint32_t n, std::vector<HNode>& nodes);
 
+// Auxiliary BVH2 over the reference leaf boxes (aux_bvh.cpp)
+void build_aux_bvh(const std::vector<HNode>& nodes, std::vector<pt::AuxNode>& out, uint32_t& max_depth);
+
 // Gamma/quantise threshold table (tonemap.cpp)
 void build_gamma_thresholds(float thr[256]);
 

@@ -22,7 +22,8 @@ LIB_PATH = os.environ.get("PT_LIB", os.path.join(HERE, "build", "libpt.so"))
 
 PT_OK = 0
 PT_E_INVALID, PT_E_IO, PT_E_SCENE, PT_E_NO_GPU, PT_E_HIP, PT_E_RCCL, PT_E_OOM = -1, -2, -3, -4, -5, -6, -7
-TRAVERSAL_EXACT = 0
+TRAVERSAL_REPLAY = 0
+TRAVERSAL_EXACT = 1
 
 # One HIP runtime per process: PyTorch bundles its own libamdhip64 (soname
 # libamdhip64.so.7, but its users link the unversioned name), so loading
@@ -43,7 +44,7 @@ _lib = C.CDLL(LIB_PATH)
 class SceneInfo(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in (
         "width", "height", "samples", "ray_depth", "n_prims", "n_bvh_prims", "n_planes", "n_emitters",
-        "n_nodes", "tree_depth", "max_stack", "n_warnings")]
+        "n_nodes", "tree_depth", "max_stack", "n_aux_nodes", "aux_depth", "n_warnings")]
 
 
 class RenderOpts(C.Structure):
@@ -55,8 +56,9 @@ class RenderOpts(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("node_visits", C.c_uint64), ("prim_tests", C.c_uint64),
                 ("plane_tests", C.c_uint64), ("samples", C.c_uint64), ("errors", C.c_uint64),
+                ("aux_visits", C.c_uint64), ("fallbacks", C.c_uint64),
                 ("kernel_ms", C.c_double), ("resolve_ms", C.c_double), ("wall_ms", C.c_double),
-                ("node_bytes", C.c_uint64), ("prim_bytes", C.c_uint64)]
+                ("node_bytes", C.c_uint64), ("prim_bytes", C.c_uint64), ("aux_bytes", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -92,8 +94,9 @@ _sig = {
     "pt_session_free": (None, [_P]),
     "pt_last_error": (C.c_char_p, []),
     "pt_abi_version": (C.c_int, []),
-    "pt_selftest_ray_intersection": (C.c_int, [_P, C.c_uint32, _P, _P, _P]),
-    "pt_selftest_render_host": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P]),
+    "pt_selftest_ray_intersection": (C.c_int, [_P, C.c_int32, C.c_uint32, _P, _P, _P, _P]),
+    "pt_selftest_render_host": (C.c_int, [_P, C.c_int32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                          C.c_uint32, _P]),
     "pt_selftest_gamma_table": (C.c_int, [_P, _P]),
 }
 for _name, (_res, _args) in _sig.items():
@@ -174,7 +177,8 @@ class Scene:
         _check(_lib.pt_scene_dump_bvh(self._h, _ptr(nb), nb.nbytes, _ptr(pb), pb.nbytes))
         return nb.tobytes(), pb.tobytes()
 
-    def render(self, device=0, ngpu=1, samples=0, spp_per_launch=0, radiance=False, progress=False, window=None):
+    def render(self, device=0, ngpu=1, samples=0, spp_per_launch=0, radiance=False, progress=False, window=None,
+               traversal=TRAVERSAL_REPLAY):
         """Render on the GPU(s): returns (rgb u8 HxWx3, radiance f32 HxWx3 | None, stats).
 
         window=(x0, y0, w, h) renders only those pixels (global-index seeds kept)."""
@@ -185,6 +189,7 @@ class Scene:
         o = RenderOpts()
         _lib.pt_render_opts_default(C.byref(o))
         o.device, o.ngpu, o.samples, o.spp_per_launch, o.progress = device, ngpu, samples, spp_per_launch, int(progress)
+        o.traversal = traversal
         if window:
             o.win_x0, o.win_y0, o.win_w, o.win_h = window
         st = Stats()
@@ -192,16 +197,19 @@ class Scene:
         return rgb, rad, st.as_dict()
 
     # test hooks (host execution of the device traversal code; not a render path)
-    def selftest_ray_intersection(self, rays):
+    def selftest_ray_intersection(self, rays, traversal=TRAVERSAL_REPLAY):
         rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
         ids = np.zeros(len(rays), np.int32)
         hits = np.zeros((len(rays), 5), np.float32)
-        _check(_lib.pt_selftest_ray_intersection(self._h, len(rays), _ptr(rays), _ptr(ids), _ptr(hits)))
-        return ids, hits
+        ctr = np.zeros(8, np.uint64)
+        _check(_lib.pt_selftest_ray_intersection(self._h, traversal, len(rays), _ptr(rays), _ptr(ids), _ptr(hits),
+                                                 _ptr(ctr)))
+        return ids, hits, {"nodes": int(ctr[1]), "prim_tests": int(ctr[2]), "aux": int(ctr[5]),
+                           "fallbacks": int(ctr[6])}
 
-    def selftest_render_host(self, x0, y0, w, h, spp=0):
+    def selftest_render_host(self, x0, y0, w, h, spp=0, traversal=TRAVERSAL_REPLAY):
         rad = np.zeros((h, w, 3), np.float32)
-        _check(_lib.pt_selftest_render_host(self._h, x0, y0, w, h, spp, _ptr(rad)))
+        _check(_lib.pt_selftest_render_host(self._h, traversal, x0, y0, w, h, spp, _ptr(rad)))
         return rad
 
     def gamma_table(self):
@@ -213,7 +221,7 @@ class Scene:
 class Session:
     """Tile-sharded progressive renderer on one device (include/pt.h sessions)."""
 
-    def __init__(self, scene, device=0, rank=0, world=1, traversal=TRAVERSAL_EXACT, window=None):
+    def __init__(self, scene, device=0, rank=0, world=1, traversal=TRAVERSAL_REPLAY, window=None):
         self.scene = scene
         o = SessionOpts(device, rank, world, traversal, *(window or (0, 0, 0, 0)))
         self._h = _P()

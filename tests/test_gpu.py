@@ -20,13 +20,17 @@ def pt():
     return mod
 
 
+TRAVERSALS = {"replay": 0, "exact": 1}
+
+
+@pytest.mark.parametrize("trav", sorted(TRAVERSALS))
 @pytest.mark.parametrize("name", sorted(M["images"]))
-def test_golden_images_bit_exact(pt, name):
+def test_golden_images_bit_exact(pt, name, trav):
     m, img, rad = U.golden_image(name)
     with pt.Scene.load(U.golden_scene_path(name)) as s:
         s.prepare()
         win = tuple(m["window"]) if m["window"] else None
-        rgb, r, st = s.render(radiance=True, window=win)
+        rgb, r, st = s.render(radiance=True, window=win, traversal=TRAVERSALS[trav])
     assert st["errors"] == 0
     assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
     assert np.array_equal(rgb, img)
@@ -63,13 +67,18 @@ def test_standin_windows_vs_oracle_with_counters(pt):
         for _ in range(3):
             x0, y0 = int(rng.integers(0, 1920 - 24)), int(rng.integers(0, 1080 - 16))
             orgb, orad, octr = o.render(x0, y0, 24, 16, spp=2)
-            rgb, rad, st = s.render(samples=2, radiance=True, window=(x0, y0, 24, 16))
+            rgb, rad, st = s.render(samples=2, radiance=True, window=(x0, y0, 24, 16), traversal=1)
             assert rad.view(np.uint32).tolist() == orad.view(np.uint32).tolist()
             assert np.array_equal(rgb, orgb)
             assert st["rays"] == octr["rays"]
             assert st["node_visits"] == octr["nodes"]
             assert st["prim_tests"] == octr["prim_tests"]
             assert st["plane_tests"] == octr["planes"]
+            # candidate replay: same image, same rays, far fewer node records
+            rgb2, rad2, st2 = s.render(samples=2, radiance=True, window=(x0, y0, 24, 16), traversal=0)
+            assert np.array_equal(rad2.view(np.uint32), orad.view(np.uint32))
+            assert st2["rays"] == octr["rays"] and st2["errors"] == 0
+            assert st2["node_visits"] * 10 < st["node_visits"]
 
 
 @pytest.mark.parametrize("variant", ["metal", "glass"])

@@ -110,13 +110,17 @@ def test_scene_errors():
         assert e.value.code == pt.PT_E_SCENE
 
 
+TRAVERSALS = {"replay": 0, "exact": 1}
+
+
+@pytest.mark.parametrize("trav", sorted(TRAVERSALS))
 @pytest.mark.parametrize("name", sorted(M["trav"]))
-def test_exact_stack_traversal_matches_reference_kat(name):
+def test_traversal_matches_reference_kat(name, trav):
     t = M["trav"][name]
     rays, ((ids, f, inter), _) = U.read_trav(name)
     with pt.Scene.load(U.scene_path(t["scene"])) as s:
         s.prepare()
-        gids, ghits = s.selftest_ray_intersection(rays)
+        gids, ghits, ctr = s.selftest_ray_intersection(rays, traversal=TRAVERSALS[trav])
     assert np.array_equal(gids, ids)
     hit = ids != -1
     assert np.array_equal(ghits[hit, :4].view(np.uint32), f[hit].view(np.uint32))
@@ -128,8 +132,9 @@ HOST_RENDER = ["p51_64x48x16", "p52_64x48x16", "dragon_metal_64x64x8", "dragon_g
                "c2_win_240_200_24x24"]
 
 
+@pytest.mark.parametrize("trav", sorted(TRAVERSALS))
 @pytest.mark.parametrize("name", HOST_RENDER)
-def test_device_integrator_on_host_bit_exact(name):
+def test_device_integrator_on_host_bit_exact(name, trav):
     m, img, rad = U.golden_image(name)
     with pt.Scene.load(U.golden_scene_path(name)) as s:
         s.prepare()
@@ -137,7 +142,7 @@ def test_device_integrator_on_host_bit_exact(name):
             x0, y0, w, h = m["window"]
         else:
             x0, y0, h, w = 0, 0, img.shape[0], img.shape[1]
-        got = s.selftest_render_host(x0, y0, w, h)
+        got = s.selftest_render_host(x0, y0, w, h, traversal=TRAVERSALS[trav])
     assert got.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
     assert np.array_equal(U.oracle_tonemap(got).reshape(img.shape), img)
 
