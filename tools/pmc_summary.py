@@ -1,0 +1,107 @@
+#!/usr/bin/env python3
+"""Summarise a tools/gpu_profile.sh run (rocprofv3 kernel trace + PMC passes)
+into a committed profile summary and the per-launch HBM traffic table that
+bench.py reads (profiles/traffic.json).
+
+    python tools/pmc_summary.py gpurun_out/prof profiles/r01_<tag> [--key c3_spp1_n1]
+
+Counter conventions (MI355X_MICROARCH.md, HBM/rocprofv3 section):
+  * FETCH_SIZE / WRITE_SIZE are in KiB and count the L2's memory-side requests
+    (Infinity-Cache hits included).
+  * gfx950: FETCH_SIZE reports half the bytes of 128-B requests -> doubled here.
+    Cross-checked against TCC_MISS_sum x 128 B from a separate pass.
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+import shutil
+
+
+def per_kernel(path):
+    vals = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(set)
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"]
+        vals[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        disp[k].add(r["Dispatch_Id"])
+    return {k: ({c: v for c, v in d.items()}, len(disp[k])) for k, d in vals.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("prof")
+    ap.add_argument("out")
+    ap.add_argument("--kernel", default="pt::k_trace")
+    ap.add_argument("--key", default="c3_spp1_n1")
+    ap.add_argument("--traffic-json", default=os.path.join(os.path.dirname(__file__), "..", "profiles",
+                                                            "traffic.json"))
+    a = ap.parse_args()
+    os.makedirs(a.out, exist_ok=True)
+    kt = os.path.join(a.prof, "kt")
+    for f in ("run_kernel_stats.csv",):
+        shutil.copy(os.path.join(kt, f), os.path.join(a.out, "kernel_stats.csv"))
+    lines = ["# rocprofv3 summary (%s)" % os.path.basename(os.path.normpath(a.out)), ""]
+    lines.append("## kernel trace (--kernel-trace --stats)")
+    lines.append("")
+    lines.append("| kernel | calls | avg ms | total ms | % |")
+    lines.append("|---|---|---|---|---|")
+    avg_ns = None
+    for r in csv.DictReader(open(os.path.join(kt, "run_kernel_stats.csv"))):
+        lines.append("| `%s` | %s | %.3f | %.3f | %s |" % (r["Name"][:60], r["Calls"], float(r["AverageNs"]) / 1e6,
+                                                          float(r["TotalDurationNs"]) / 1e6, r["Percentage"]))
+        if r["Name"].startswith(a.kernel):
+            avg_ns = float(r["AverageNs"])
+    # resources of the kernel from the trace
+    for r in csv.DictReader(open(os.path.join(kt, "run_kernel_trace.csv"))):
+        if r["Kernel_Name"].startswith(a.kernel):
+            lines += ["", "`%s`: VGPR %s, SGPR %s, scratch %s B, LDS (static) %s B, grid %s x wg %s" % (
+                a.kernel, r["VGPR_Count"], r["SGPR_Count"], r["Scratch_Size"], r["LDS_Block_Size"],
+                r["Grid_Size_X"], r["Workgroup_Size_X"])]
+            break
+    pmc = {}
+    for sub in sorted(os.listdir(a.prof)):
+        p = os.path.join(a.prof, sub, "run_counter_collection.csv")
+        if sub.startswith("pmc") and os.path.exists(p):
+            for k, (d, n) in per_kernel(p).items():
+                if k.startswith(a.kernel):
+                    for c, v in d.items():
+                        pmc[c] = v / n
+    lines += ["", "## PMC, per %s launch (separate --pmc passes)" % a.kernel, ""]
+    for c, v in sorted(pmc.items()):
+        lines.append("* %s = %.6g" % (c, v))
+    res = {}
+    if "FETCH_SIZE" in pmc:
+        fetch = pmc["FETCH_SIZE"] * 1024.0 * 2.0
+        write = pmc.get("WRITE_SIZE", 0.0) * 1024.0
+        res = {"hbm_bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+               "source": "rocprofv3 --pmc FETCH_SIZE (KiB, x2 gfx950 correction) + WRITE_SIZE (KiB), per launch; "
+                         "L2 memory-side bytes (Infinity-Cache hits included)"}
+        if "TCC_MISS_sum" in pmc:
+            res["tcc_miss_x128_bytes"] = pmc["TCC_MISS_sum"] * 128.0
+            res["l2_hit_rate"] = pmc["TCC_HIT_sum"] / (pmc["TCC_HIT_sum"] + pmc["TCC_MISS_sum"])
+        if avg_ns:
+            res["avg_launch_ms"] = avg_ns / 1e6
+            res["traffic_GBps"] = res["hbm_bytes_per_launch"] / avg_ns
+        lines += ["", "## derived", ""]
+        for k, v in res.items():
+            lines.append("* %s = %s" % (k, v if isinstance(v, str) else "%.6g" % v))
+    if "SQ_INSTS_VALU" in pmc and "SQ_WAVES" in pmc:
+        lines.append("* VALU instructions per wave = %.6g" % (pmc["SQ_INSTS_VALU"] / pmc["SQ_WAVES"]))
+    open(os.path.join(a.out, "SUMMARY.md"), "w").write("\n".join(lines) + "\n")
+    for f in os.listdir(a.prof):
+        if f.endswith(".json"):
+            shutil.copy(os.path.join(a.prof, f), os.path.join(a.out, f))
+    if res:
+        tj = {}
+        if os.path.exists(a.traffic_json):
+            tj = json.load(open(a.traffic_json))
+        res["profile"] = os.path.relpath(a.out, os.path.dirname(os.path.abspath(a.traffic_json)))
+        tj[a.key] = res
+        json.dump(tj, open(a.traffic_json, "w"), indent=1)
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
