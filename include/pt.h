@@ -78,7 +78,9 @@ enum {
     PT_TRAVERSAL_REPLAY = 0, /* default: candidate replay -- auxiliary BVH enumerates the reference
                                 leaves the ray can reach, the reference's exact pruning is replayed
                                 on their root paths only (bit-identical results) */
-    PT_TRAVERSAL_EXACT = 1   /* full reference-tree stack DFS, exact pruning semantics */
+    PT_TRAVERSAL_EXACT = 1,  /* full reference-tree stack DFS, exact pruning semantics */
+    PT_TRAVERSAL_REPLAY_DIV = 2 /* candidate replay with the reference's IEEE-division slab test at
+                                   every node (the unfiltered form; same results, slower) */
 };
 
 typedef struct pt_render_opts {

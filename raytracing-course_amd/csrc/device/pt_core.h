@@ -68,16 +68,23 @@ PT_HD float u2f(uint32_t u) { union { float f; uint32_t u; } c; c.u = u; return 
 // an exhaustive comparison against the host libm over every float in (0, 1]
 // (the only range the polar method feeds it).
 struct LogfEntry { double invc, logc; };
+// table in constant memory on the device (a dynamically indexed local array
+// would be materialised in 32 VGPRs)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PT_TABLE __constant__
+#else
+#define PT_TABLE
+#endif
+PT_TABLE static const LogfEntry kLogfT[16] = {
+    {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2}, {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2},
+    {0x1.49539f0f010bp+0, -0x1.01eae7f513a67p-2},  {0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3},
+    {0x1.30d190c8864a5p+0, -0x1.6574f0ac07758p-3}, {0x1.25e227b0b8eap+0, -0x1.1aa2bc79c81p-3},
+    {0x1.1bb4a4a1a343fp+0, -0x1.a4e76ce8c0e5ep-4}, {0x1.12358f08ae5bap+0, -0x1.1973c5a611cccp-4},
+    {0x1.0953f419900a7p+0, -0x1.252f438e10c1ep-5}, {0x1p+0, 0x0p+0},
+    {0x1.e608cfd9a47acp-1, 0x1.aa5aa5df25984p-5},  {0x1.ca4b31f026aap-1, 0x1.c5e53aa362eb4p-4},
+    {0x1.b2036576afce6p-1, 0x1.526e57720db08p-3},  {0x1.9c2d163a1aa2dp-1, 0x1.bc2860d22477p-3},
+    {0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2},  {0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2}};
 PT_HD float logf_glibc(float x) {
-    const LogfEntry T[16] = {
-        {0x1.661ec79f8f3bep+0, -0x1.57bf7808caadep-2}, {0x1.571ed4aaf883dp+0, -0x1.2bef0a7c06ddbp-2},
-        {0x1.49539f0f010bp+0, -0x1.01eae7f513a67p-2},  {0x1.3c995b0b80385p+0, -0x1.b31d8a68224e9p-3},
-        {0x1.30d190c8864a5p+0, -0x1.6574f0ac07758p-3}, {0x1.25e227b0b8eap+0, -0x1.1aa2bc79c81p-3},
-        {0x1.1bb4a4a1a343fp+0, -0x1.a4e76ce8c0e5ep-4}, {0x1.12358f08ae5bap+0, -0x1.1973c5a611cccp-4},
-        {0x1.0953f419900a7p+0, -0x1.252f438e10c1ep-5}, {0x1p+0, 0x0p+0},
-        {0x1.e608cfd9a47acp-1, 0x1.aa5aa5df25984p-5},  {0x1.ca4b31f026aap-1, 0x1.c5e53aa362eb4p-4},
-        {0x1.b2036576afce6p-1, 0x1.526e57720db08p-3},  {0x1.9c2d163a1aa2dp-1, 0x1.bc2860d22477p-3},
-        {0x1.886e6037841edp-1, 0x1.1058bc8a07ee1p-2},  {0x1.767dcf5534862p-1, 0x1.4043057b6ee09p-2}};
     const double Ln2 = 0x1.62e42fefa39efp-1;
     const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2, A2 = -0x1.ffffef20a4123p-2;
     uint32_t ix = f2u(x);
@@ -91,7 +98,7 @@ PT_HD float logf_glibc(float x) {
     const int i = (int)((tmp >> (23 - 4)) % 16u);
     const int k = (int32_t)tmp >> 23;
     const uint32_t iz = ix - (tmp & (0x1ffu << 23));
-    const double invc = T[i].invc, logc = T[i].logc;
+    const double invc = kLogfT[i].invc, logc = kLogfT[i].logc;
     const double z = (double)u2f(iz);
     const double r = z * invc - 1.0;
     const double y0 = logc + (double)k * Ln2;
@@ -301,6 +308,19 @@ PT_HD bool prim_intersect(const Prim& P, const Ray& ray, Hit& h) {
     }
     if (ok) h.n = normalize(qrot(q, h.n));
     return ok;
+}
+
+// plane-only form of prim_intersect (the scene's plane list): same operations
+PT_HD bool plane_intersect(const Prim& P, const Ray& ray, Hit& h) {
+    const f3 pos = mk3(P.p0.x, P.p0.y, P.p0.z);
+    q4 q; q.x = P.p1.x; q.y = P.p1.y; q.z = P.p1.z; q.w = P.p1.w;
+    const q4 cq = conj(q);
+    Ray lr;
+    lr.o = qrot(cq, ray.o + -1.f * pos);
+    lr.d = qrot(cq, ray.d);
+    if (!isect_plane(lr, mk3(P.p2.x, P.p2.y, P.p2.z), h)) return false;
+    h.n = normalize(qrot(q, h.n));
+    return true;
 }
 
 // ------------------------------------------------- light distributions -----

@@ -6,7 +6,7 @@
 #include <hip/hip_runtime_api.h>
 #endif
 
-#include "pt_trace.h"
+#include "pt_query.h"
 
 namespace pt {
 
@@ -42,6 +42,40 @@ struct TraceParams {
     ReplayCfg cfg;
     uint32_t depth;
     uint32_t spp;
+    uint32_t n_tiles_local;
+    unsigned long long* wg_prof;  // optional per-workgroup {start, end, HW_ID, XCC_ID} (diagnostics)
+};
+
+// ---- wavefront renderer (pt_wave.hip) ----------------------------------
+struct WaveQueue {                // rays of one bounce, compacted
+    F4* ro;                       // {o.xyz, u32 slot}
+    F4* rd;                       // {d.xyz, -}
+};
+struct WaveHits {                 // closest hit per queue entry
+    F4* th;                       // {t, n.xyz}
+    uint32_t* id;                 // prim | interior << 31, 0xffffffff = miss
+};
+// per-slot path end state (pstate = nv | end << 8)
+enum : uint32_t { PE_LIVE = 0u, PE_MISS = 1u, PE_CUT = 2u, PE_TERM = 3u };
+
+struct WaveParams {
+    SceneView S;
+    const AuxSL* aux;
+    uint32_t n_aux;
+    CamView cam;
+    TileMap tm;
+    PixelState st;
+    uint32_t* vscratch;           // 3 * depth * n_slots fold records
+    uint32_t* pstate;             // n_slots
+    WaveQueue q[2];               // ping-pong: bounce b reads q[b & 1], enqueues into q[(b + 1) & 1]
+    WaveHits hits;
+    uint32_t* fb;                 // queue indices left to the exact DFS (this bounce)
+    uint32_t* ctl;                // [0, D]: queue counts per bounce, [D+1, 2D+1]: fetch heads, [2D+2, 3D+2]: exact counts
+    unsigned long long* counters; // rays, nodes, prim tests, plane tests, errors, aux visits, fallbacks
+    uint32_t depth;
+    uint32_t bounce;
+    uint32_t n_tiles_local;
+    uint32_t max_stack;           // exact DFS stack words per lane
 };
 
 struct ResolveParams {
@@ -55,5 +89,8 @@ struct ResolveParams {
 }  // namespace pt
 
 hipError_t pt_launch_init(const pt::InitParams& p, uint32_t n_tiles, hipStream_t s);
-hipError_t pt_launch_trace(const pt::TraceParams& p, uint32_t n_tiles, uint32_t lds_bytes, hipStream_t s);
+// variant: bit 0 = filtered node tests + flat replay, bit 1 = XCD-banded tile order
+hipError_t pt_launch_trace(const pt::TraceParams& p, int variant, uint32_t lds_bytes, hipStream_t s);
+// one sample of every owned pixel through the wavefront pipeline (pt_wave.hip)
+hipError_t pt_launch_wave_sample(pt::WaveParams p, uint32_t isect_grid, hipStream_t s);
 hipError_t pt_launch_resolve(const pt::ResolveParams& p, uint32_t n_tiles, hipStream_t s);

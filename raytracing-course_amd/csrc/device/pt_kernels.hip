@@ -13,48 +13,11 @@
 // Compiled with -ffp-contract=off (see pt_core.h).
 #include <hip/hip_runtime.h>
 
+#include "pt_devutil.h"
 #include "pt_kernels.h"
 #include "pt_trace.h"
 
 namespace pt {
-
-// per-lane word memory in LDS, [word][lane] (consecutive lanes -> consecutive banks)
-struct LdsMem {
-    uint32_t* base;
-    __device__ __forceinline__ void set(uint32_t i, uint32_t v) { base[i * 256u] = v; }
-    __device__ __forceinline__ uint32_t get(uint32_t i) const { return base[i * 256u]; }
-};
-
-struct HbmVStore {
-    uint32_t* base;   // + slot
-    uint32_t stride;  // n_slots
-    __device__ __forceinline__ void put(uint32_t k, uint32_t idm, float s1, float s2) {
-        base[(3u * k) * stride] = idm;
-        base[(3u * k + 1u) * stride] = f2u(s1);
-        base[(3u * k + 2u) * stride] = f2u(s2);
-    }
-    __device__ __forceinline__ void get(uint32_t k, uint32_t& idm, float& s1, float& s2) const {
-        idm = base[(3u * k) * stride];
-        s1 = u2f(base[(3u * k + 1u) * stride]);
-        s2 = u2f(base[(3u * k + 2u) * stride]);
-    }
-};
-
-// owned slot -> global pixel (16x16 tiles of the window dealt round-robin to ranks)
-__device__ __forceinline__ bool slot_pixel(const TileMap& tm, uint32_t tile_local, uint32_t lane, uint32_t& x,
-                                           uint32_t& y) {
-    const uint32_t gt = tile_local * tm.world + tm.rank;
-    const uint32_t tx = gt % tm.tiles_x, ty = gt / tm.tiles_x;
-    const uint32_t wx = tx * 16u + (lane & 15u), wy = ty * 16u + (lane >> 4);
-    x = tm.x0 + wx;
-    y = tm.y0 + wy;
-    return gt < tm.n_tiles && wx < tm.ww && wy < tm.wh;
-}
-
-__device__ __forceinline__ void wave_add_u64(unsigned long long* dst, unsigned long long v) {
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    if ((threadIdx.x & 63u) == 0u && v != 0ull) atomicAdd(dst, v);
-}
 
 __global__ void __launch_bounds__(256) k_init(InitParams P) {
     const uint32_t slot = blockIdx.x * 256u + threadIdx.x;
@@ -69,11 +32,23 @@ __global__ void __launch_bounds__(256) k_init(InitParams P) {
     P.st.sum[2u * P.st.n_slots + slot] = 0.f;
 }
 
+// V bit 0: filtered node tests + flat replay loop (FAST); bit 1: XCD-banded
+// tile order -- workgroup b runs on XCD b % 8, so XCD x is given the x-th
+// contiguous band of tiles and its 4 MB L2 caches that band's working set.
+template <int V>
 __global__ void __launch_bounds__(256) k_trace(TraceParams P) {
     extern __shared__ uint32_t lds_stack[];
-    const uint32_t slot = blockIdx.x * 256u + threadIdx.x;
+    uint32_t tile = blockIdx.x;
+    if (V & 2) {
+        const uint32_t per = (P.n_tiles_local + 7u) / 8u;
+        tile = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+        if (tile >= P.n_tiles_local) return;
+    }
+    uint64_t t_start = 0;
+    if (P.wg_prof && threadIdx.x == 0) t_start = __builtin_amdgcn_s_memrealtime();
+    const uint32_t slot = tile * 256u + threadIdx.x;
     uint32_t x, y;
-    const bool ok = slot_pixel(P.tm, blockIdx.x, threadIdx.x, x, y);
+    const bool ok = slot_pixel(P.tm, tile, threadIdx.x, x, y);
     Counts C;
     C.rays = C.nodes = C.ptests = C.planes = C.aux = C.fallbacks = 0ull;
     C.errs = 0u;
@@ -90,7 +65,7 @@ __global__ void __launch_bounds__(256) k_trace(TraceParams P) {
             const float fx = fxb + rng_uniform(R);
             const float fy = fyb + rng_uniform(R);
             const Ray ray = camera_ray(P.cam, fx, fy);
-            sum = sum + trace_path(P.S, P.cfg, ray, P.depth, R, stk, vs, C);
+            sum = sum + trace_path<(V & 1) != 0>(P.S, P.cfg, ray, P.depth, R, stk, vs, C);
         }
         P.st.rng_x[slot] = R.x;
         P.st.rng_saved[slot] = R.saved;
@@ -106,6 +81,17 @@ __global__ void __launch_bounds__(256) k_trace(TraceParams P) {
     wave_add_u64(P.counters + 4, (unsigned long long)C.errs);
     wave_add_u64(P.counters + 5, C.aux);
     wave_add_u64(P.counters + 6, C.fallbacks);
+    if (P.wg_prof) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            // {start, end (100 MHz), HW_ID, XCC_ID} per workgroup, indexed by tile
+            unsigned long long* w = P.wg_prof + 4ull * tile;
+            w[0] = t_start;
+            w[1] = __builtin_amdgcn_s_memrealtime();
+            w[2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            w[3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+        }
+    }
 }
 
 __global__ void __launch_bounds__(256) k_resolve(ResolveParams P) {
@@ -133,8 +119,14 @@ hipError_t pt_launch_init(const pt::InitParams& p, uint32_t n_tiles, hipStream_t
     hipLaunchKernelGGL(pt::k_init, dim3(n_tiles), dim3(256), 0, s, p);
     return hipGetLastError();
 }
-hipError_t pt_launch_trace(const pt::TraceParams& p, uint32_t n_tiles, uint32_t lds_bytes, hipStream_t s) {
-    hipLaunchKernelGGL(pt::k_trace, dim3(n_tiles), dim3(256), lds_bytes, s, p);
+hipError_t pt_launch_trace(const pt::TraceParams& p, int variant, uint32_t lds_bytes, hipStream_t s) {
+    const uint32_t n = p.n_tiles_local, nx = (n + 7u) / 8u * 8u;
+    switch (variant) {
+        case 0: hipLaunchKernelGGL(pt::k_trace<0>, dim3(n), dim3(256), lds_bytes, s, p); break;
+        case 1: hipLaunchKernelGGL(pt::k_trace<1>, dim3(n), dim3(256), lds_bytes, s, p); break;
+        case 2: hipLaunchKernelGGL(pt::k_trace<2>, dim3(nx), dim3(256), lds_bytes, s, p); break;
+        default: hipLaunchKernelGGL(pt::k_trace<3>, dim3(nx), dim3(256), lds_bytes, s, p); break;
+    }
     return hipGetLastError();
 }
 hipError_t pt_launch_resolve(const pt::ResolveParams& p, uint32_t n_tiles, hipStream_t s) {

@@ -1,0 +1,246 @@
+// pt_query.h -- the closest-hit query of the wavefront renderer as a per-lane
+// state machine (Scene::RayIntersection, src/scene.cpp:46-77, with the
+// reference BVH semantics of src/bvh.cpp:181-225 reproduced by candidate
+// replay; see pt_trace.h for the replay argument).
+//
+// Built for a persistent, refilling intersection kernel: every call of
+// q_step() advances ONE lane by one node visit, so lanes whose rays need many
+// visits (the candidate tail: p99 ~25 leaves) no longer hold the other 63
+// lanes of their wave -- an idle lane simply takes the next ray.
+//
+//   * auxiliary BVH: stackless BVH2 in DFS preorder with skip links
+//     (AuxSL, 32 B): internal = conservative inflated box; leaf = the
+//     reference leaf's own exact (center, half-size), tested with the filtered
+//     exact test node_enter() -- one dependent load per visit, no stack.
+//   * candidates: the PT_QK smallest reference-leaf indices of the pass, kept
+//     sorted in registers by a min/max insertion network (no LDS, no dynamic
+//     register indexing); more than PT_QK -> further passes above the last
+//     processed index (rare).
+//   * replay: one reference node per step, root -> candidate, with the
+//     reference's pruning and right-child bounds.
+// Rays the replay cannot take (non-finite or near-zero direction
+// components) or whose replay hit list overflows are flagged for the exact
+// stack DFS (bvh_exact) in a separate pass.
+#pragma once
+#include "pt_trace.h"
+
+namespace pt {
+
+#ifndef PT_QK
+#define PT_QK 16
+#endif
+
+// stackless auxiliary node (32 B):
+//   internal: a = {lo.x, lo.y, lo.z, hi.x}, b = {hi.y, hi.z, u32 skip, 0xffffffff}
+//   leaf:     a = {c.x, c.y, c.z, s.x},     b = {s.y, s.z, u32 skip (= own index + 1), u32 reference leaf}
+// (c, s) of a leaf are bit-identical copies of the reference node's record.
+struct AuxSL { F4 a, b; };
+#define PT_AUX_INTERNAL 0xffffffffu
+
+enum : uint32_t { Q_AUX = 0u, Q_REPLAY = 1u, Q_DONE = 2u, Q_EXACT = 3u };
+
+struct QHits {                  // replay hit list (reference leaf index, leaf first-min t)
+    uint32_t idx[PT_REPLAY_HITS];
+    float t[PT_REPLAY_HITS];
+};
+
+struct Query {
+    Ray ray;
+    f3 inv, oinv;
+    float P;                    // closest plane t (the BVH bound at the root)
+    uint32_t phase;
+    uint32_t node;              // Q_AUX: aux node; Q_REPLAY: reference node on the current path
+    uint32_t lb;                // every candidate below lb has been processed
+    uint32_t cand, skip, last;
+    float bound;
+    uint32_t overflow;
+    uint32_t c[PT_QK];          // sorted candidates of this pass (0xffffffff = empty)
+    uint32_t nh;
+    QHits H;
+    float bt;                   // best BVH leaf hit so far (first strict minimum)
+    Hit res;                    // result so far (plane, then BVH hits that beat it)
+    int res_id;
+};
+
+struct QCounts {
+    uint32_t nodes, aux, ptests, planes;
+};
+
+// planes (src/scene.cpp:50-57), then the BVH set-up
+PT_HD void q_init(const SceneView& S, const Ray& ray, Query& q, QCounts& C) {
+    q.ray = ray;
+    q.res_id = -1;
+    q.res.t = PT_INF;
+    float closest = PT_INF;
+    for (uint32_t k = 0; k < S.n_planes; ++k) {
+        const uint32_t pi = S.planes[k];
+        Hit h;
+        C.planes++;
+        if (plane_intersect(S.prims[pi], ray, h) && h.t < closest) { closest = h.t; q.res = h; q.res_id = (int)pi; }
+    }
+    q.P = closest;
+    q.bt = PT_INF;
+    q.nh = 0;
+    q.lb = 0;
+    q.overflow = 0;
+    q.node = 0;
+#pragma unroll
+    for (int i = 0; i < PT_QK; ++i) q.c[i] = 0xffffffffu;
+    if (!replay_ok_ray(ray)) { q.phase = Q_EXACT; return; }
+    q.inv = mk3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
+    q.oinv = mk3(ray.o.x * q.inv.x, ray.o.y * q.inv.y, ray.o.z * q.inv.z);
+    q.phase = Q_AUX;
+}
+
+PT_HD void q_insert(Query& q, uint32_t v) {
+#pragma unroll
+    for (int i = 0; i < PT_QK; ++i) {
+        const uint32_t lo = q.c[i] < v ? q.c[i] : v;
+        v = q.c[i] < v ? v : q.c[i];
+        q.c[i] = lo;
+    }
+    if (v != 0xffffffffu) q.overflow = 1u;   // a candidate above the kept PT_QK was dropped
+}
+
+PT_HD uint32_t q_pop(Query& q) {
+    const uint32_t v = q.c[0];
+#pragma unroll
+    for (int i = 0; i + 1 < PT_QK; ++i) q.c[i] = q.c[i + 1];
+    q.c[PT_QK - 1] = 0xffffffffu;
+    return v;
+}
+
+// next candidate >= skip, or end of pass (-> next pass / done)
+PT_HD void q_next_candidate(Query& q) {
+    for (;;) {
+        const uint32_t v = q_pop(q);
+        if (v == 0xffffffffu) break;
+        q.last = v;
+        if (v >= q.skip) {
+            q.cand = v;
+            q.node = 0;
+            q.bound = q.P;
+            q.phase = Q_REPLAY;
+            return;
+        }
+    }
+    if (q.overflow) {
+        // candidates above the last processed one were dropped: another aux pass
+        q.lb = q.skip > q.last + 1u ? q.skip : q.last + 1u;
+        q.overflow = 0;
+        q.node = 0;
+        q.phase = Q_AUX;
+        return;
+    }
+    q.phase = Q_DONE;
+}
+
+// Advance one node visit.  Precondition: phase is Q_AUX or Q_REPLAY.
+PT_HD void q_step(const SceneView& S, const AuxSL* aux, uint32_t n_aux, Query& q, QCounts& C) {
+    if (q.phase == Q_AUX) {
+        const AuxSL an = aux[q.node];
+        C.aux++;
+        const uint32_t skip = f2u(an.b.z), code = f2u(an.b.w);
+        uint32_t next;
+        if (code == PT_AUX_INTERNAL) {
+            next = aux_box(an.a.x, an.a.y, an.a.z, an.a.w, an.b.x, an.b.y, q.inv, q.oinv) ? q.node + 1u : skip;
+        } else {
+            if (code >= q.lb) {
+                Node nd;
+                nd.a = an.a;
+                nd.b = an.b;
+                if (node_enter(nd, q.ray, q.inv, PT_INF)) q_insert(q, code);
+            }
+            next = skip;
+        }
+        q.node = next;
+        if (next >= n_aux) {
+            // aux pass complete: replay the candidates in reference preorder
+            q.skip = q.lb;
+            q_next_candidate(q);
+        }
+        return;
+    }
+    // Q_REPLAY: one node of the root -> cand path
+    const Node nd = S.nodes[q.node];
+    C.nodes++;
+    const uint32_t a = q.node;
+    const uint32_t ref = f2u(nd.b.z), info = f2u(nd.b.w);
+    if (!node_enter(nd, q.ray, q.inv, q.bound)) {
+        q.skip = (info & PT_NODE_INTERIOR) ? (info & 0x7fffffffu) : a + 1u;
+        q_next_candidate(q);
+        return;
+    }
+    if (a == q.cand) {
+        // leaf reached: first-min over its primitives (src/bvh.cpp:205-213)
+        Hit lbh;
+        lbh.t = PT_INF;
+        int lid = -1;
+        for (uint32_t i = ref; i < ref + info; ++i) {
+            Hit h;
+            C.ptests++;
+            if (prim_intersect(S.prims[i], q.ray, h) && h.t < lbh.t) { lbh = h; lid = (int)i; }
+        }
+        if (lid >= 0) {
+            if (q.nh == PT_REPLAY_HITS) { q.phase = Q_EXACT; return; }
+#pragma unroll
+            for (int k = 0; k < PT_REPLAY_HITS; ++k)
+                if ((uint32_t)k == q.nh) { q.H.idx[k] = a; q.H.t[k] = lbh.t; }
+            ++q.nh;
+            // BVH result = first strict minimum; it replaces the plane hit iff strictly closer
+            if (lbh.t < q.bt) {
+                q.bt = lbh.t;
+                if (lbh.t < q.P) { q.res = lbh; q.res_id = lid; }
+            }
+        }
+        q.skip = a + 1u;
+        q_next_candidate(q);
+        return;
+    }
+    if (q.cand < ref) {
+        q.node = a + 1u;                 // left child: same bound
+    } else {
+        // right child: bound = best hit of the left sibling's subtree, if any
+        float m = q.bound;
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < PT_REPLAY_HITS; ++k) {
+            if ((uint32_t)k < q.nh && q.H.idx[k] > a && q.H.idx[k] < ref) {
+                if (!any || q.H.t[k] < m) m = q.H.t[k];
+                any = true;
+            }
+        }
+        q.bound = m;
+        q.node = ref;
+    }
+}
+
+// exact stack DFS for the rays the replay leaves (planes again + bvh_exact:
+// the replay may already have replaced the plane result)
+template <class Stack>
+PT_HD int q_exact(const SceneView& S, const Ray& ray, Stack& stk, Hit& out, QCounts& C) {
+    SceneView E = S;
+    E.aux = nullptr;
+    Counts X{};
+    const ReplayCfg cfg{0u, 0u};
+    const int id = ray_intersection<false>(E, cfg, ray, stk, out, X);
+    C.nodes += (uint32_t)X.nodes;
+    C.ptests += (uint32_t)X.ptests;
+    C.planes += (uint32_t)X.planes;
+    return id;
+}
+
+// whole query on one thread (host tests / reference form of the state machine)
+template <class Stack>
+PT_HD int q_run(const SceneView& S, const AuxSL* aux, uint32_t n_aux, const Ray& ray, Stack& stk, Hit& out,
+                QCounts& C, uint32_t& exact_used) {
+    Query q;
+    q_init(S, ray, q, C);
+    while (q.phase == Q_AUX || q.phase == Q_REPLAY) q_step(S, aux, n_aux, q, C);
+    exact_used = q.phase == Q_EXACT ? 1u : 0u;
+    if (exact_used) return q_exact(S, ray, stk, out, C);
+    out = q.res;
+    return q.res_id;
+}
+
+}  // namespace pt

@@ -165,6 +165,54 @@ PT_HD bool node_slab(const Node& nd, const Ray& ray, float& t, uint32_t& interio
     return slab(ray.o + -1.f * c, ray.d, s, t, interior);
 }
 
+// Filtered exact node test.  Decides exactly what node_slab + the reference's
+// prune rule decide -- hit iff !(t1 > t2) && !(t2 < 0); pruned iff
+// bound < t1 && !(t1 < 0) -- but evaluates the six quotients (+-s - o)/d as
+// (+-s - o) * rinv with rinv = 1/d (IEEE, once per ray) instead of six IEEE
+// divisions.  Both quotient forms are within 1.5 ulp of the real quotient
+// (rinv rel. error <= 2^-24, product rounding <= 2^-24; the IEEE quotient
+// <= 2^-24), min/max selection is monotone in both, so every compared value
+// is within E = |v| 2^-20 + 1e-30 of its exact counterpart.  A decision whose
+// operands are closer than that margin is re-done with the exact division
+// (slab()).  Requires replay_ok_ray(ray) (finite, non-tiny d: |rinv| < 1e30).
+// Returns true iff the node is entered (hit and not pruned).
+PT_HD bool node_enter(const Node& nd, const Ray& ray, f3 rinv, float bound) {
+    const f3 c = mk3(nd.a.x, nd.a.y, nd.a.z);
+    const f3 s = mk3(nd.a.w, nd.b.x, nd.b.y);
+    const f3 o = ray.o + -1.f * c;                 // src/bvh.cpp:92 (same IEEE adds)
+    const f3 nlo = -1.f * s - o, nhi = s - o;      // src/primitives.cpp:71-72 numerators
+    const float ax = nlo.x * rinv.x, bx = nhi.x * rinv.x;
+    const float ay = nlo.y * rinv.y, by = nhi.y * rinv.y;
+    const float az = nlo.z * rinv.z, bz = nhi.z * rinv.z;
+    const float t1 = smax(smax(smin(ax, bx), smin(ay, by)), smin(az, bz));
+    const float t2 = smin(smin(smax(ax, bx), smax(ay, by)), smax(az, bz));
+    const float e1 = fabsf(t1) * 0x1p-20f + 1e-30f, e2 = fabsf(t2) * 0x1p-20f + 1e-30f;
+    const float m12 = 2.f * (e1 + e2);
+    const float d12 = t1 - t2;
+    // certain outcomes (every comparison separated by more than its error margin)
+    bool amb = !(e1 < 1e20f && e2 < 1e20f) || !(fabsf(d12) > m12);
+    bool enter = false;
+    if (!amb) {
+        if (d12 > 0.f) return false;                            // t1 > t2: miss
+        if (!(fabsf(t2) > e2)) amb = true;
+        else if (t2 < 0.f) return false;                        // box behind the ray
+        else if (!(fabsf(t1) > e1)) amb = true;
+        else if (t1 < 0.f) return true;                         // interior: never pruned
+        else {
+            const float eb = 2.f * e1 + fabsf(bound) * 0x1p-22f;
+            if (!(fabsf(bound - t1) > eb)) amb = true;
+            else enter = !(bound < t1);
+        }
+    }
+    if (amb) {
+        float t;
+        uint32_t in;
+        if (!slab(o, ray.d, s, t, in)) return false;
+        return !(bound < t && !in);
+    }
+    return enter;
+}
+
 PT_HD bool replay_ok_ray(const Ray& r) {
     // rays with a (near-)zero or non-finite direction component, or a non-finite
     // origin, take the exact stack DFS (NaN/inf slab semantics)
@@ -174,8 +222,10 @@ PT_HD bool replay_ok_ray(const Ray& r) {
            fabsf(r.o.z) < big;
 }
 
-// returns best hit id (-1 none); sets `fallback` when the exact DFS must be used instead
-template <class Mem>
+// returns best hit id (-1 none); sets `fallback` when the exact DFS must be used instead.
+// FAST: filtered node tests (node_enter) and one flat replay loop over all
+// (candidate, ancestor) steps; otherwise the IEEE-division reference form.
+template <bool FAST, class Mem>
 PT_HD int bvh_replay(const SceneView& S, const ReplayCfg& cfg, const Ray& ray, float P, Mem& L, Hit& best,
                      Counts& C, bool& fallback) {
     fallback = false;
@@ -208,10 +258,14 @@ PT_HD int bvh_replay(const SceneView& S, const ReplayCfg& cfg, const Ray& ray, f
                 if (code & 0x80000000u) {
                     const uint32_t leaf = code & 0x7fffffffu;
                     if (leaf < lb) continue;
-                    float t;
-                    uint32_t in;
                     C.nodes++;
-                    if (!node_slab(S.nodes[leaf], ray, t, in)) continue;
+                    if (FAST) {
+                        if (!node_enter(S.nodes[leaf], ray, inv, PT_INF)) continue;
+                    } else {
+                        float t;
+                        uint32_t in;
+                        if (!node_slab(S.nodes[leaf], ray, t, in)) continue;
+                    }
                     if (n < cfg.cap) {
                         L.set(cfg.as + n, leaf);
                         if (leaf > mx || n == 0) { mx = leaf; mxpos = n; }
@@ -252,23 +306,21 @@ PT_HD int bvh_replay(const SceneView& S, const ReplayCfg& cfg, const Ray& ray, f
         }
         // ---- replay root -> candidate paths in preorder
         uint32_t skip = lb;
-        for (uint32_t k = 0; k < n; ++k) {
-            const uint32_t cand = L.get(cfg.as + k);
-            if (cand < skip) continue;
+        if (FAST) {
+            // one flat loop: each iteration tests one node of the current candidate's root path
+            uint32_t k = 0, cand = 0;
+            while (k < n && (cand = L.get(cfg.as + k)) < skip) ++k;
             uint32_t a = 0;
             float bound = P;
-            for (;;) {
+            while (k < n) {
                 const Node nd = S.nodes[a];
                 C.nodes++;
-                float t;
-                uint32_t in;
-                const bool hit = node_slab(nd, ray, t, in);
                 const uint32_t ref = f2u(nd.b.z), info = f2u(nd.b.w);
-                if (!hit || (bound < t && !in)) {
+                bool next_cand = false;
+                if (!node_enter(nd, ray, inv, bound)) {
                     skip = (info & PT_NODE_INTERIOR) ? (info & 0x7fffffffu) : a + 1u;
-                    break;
-                }
-                if (a == cand) {
+                    next_cand = true;
+                } else if (a == cand) {
                     // leaf reached: first-min over its primitives (src/bvh.cpp:205-213)
                     Hit lbh;
                     lbh.t = PT_INF;
@@ -287,9 +339,8 @@ PT_HD int bvh_replay(const SceneView& S, const ReplayCfg& cfg, const Ray& ray, f
                         if (lbh.t < best.t) { best = lbh; best_id = lid; }
                     }
                     skip = cand + 1u;
-                    break;
-                }
-                if (cand < ref) {
+                    next_cand = true;
+                } else if (cand < ref) {
                     a = a + 1u;                      // left child: same bound
                 } else {
                     // right child: bound = best hit of the left sibling's subtree, if any
@@ -305,6 +356,68 @@ PT_HD int bvh_replay(const SceneView& S, const ReplayCfg& cfg, const Ray& ray, f
                     bound = m;
                     a = ref;
                 }
+                if (next_cand) {
+                    ++k;
+                    while (k < n && (cand = L.get(cfg.as + k)) < skip) ++k;
+                    a = 0;
+                    bound = P;
+                }
+            }
+        } else {
+            for (uint32_t k = 0; k < n; ++k) {
+                const uint32_t cand = L.get(cfg.as + k);
+                if (cand < skip) continue;
+                uint32_t a = 0;
+                float bound = P;
+                for (;;) {
+                    const Node nd = S.nodes[a];
+                    C.nodes++;
+                    float t;
+                    uint32_t in;
+                    const bool hit = node_slab(nd, ray, t, in);
+                    const uint32_t ref = f2u(nd.b.z), info = f2u(nd.b.w);
+                    if (!hit || (bound < t && !in)) {
+                        skip = (info & PT_NODE_INTERIOR) ? (info & 0x7fffffffu) : a + 1u;
+                        break;
+                    }
+                    if (a == cand) {
+                        // leaf reached: first-min over its primitives (src/bvh.cpp:205-213)
+                        Hit lbh;
+                        lbh.t = PT_INF;
+                        int lid = -1;
+                        for (uint32_t i = ref; i < ref + info; ++i) {
+                            Hit h;
+                            C.ptests++;
+                            if (prim_intersect(S.prims[i], ray, h) && h.t < lbh.t) { lbh = h; lid = (int)i; }
+                        }
+                        if (lid >= 0) {
+                            if (nh == PT_REPLAY_HITS) { fallback = true; return -1; }
+#pragma unroll
+                            for (int q = 0; q < PT_REPLAY_HITS; ++q)
+                                if ((uint32_t)q == nh) { h_idx[q] = cand; h_t[q] = lbh.t; }
+                            ++nh;
+                            if (lbh.t < best.t) { best = lbh; best_id = lid; }
+                        }
+                        skip = cand + 1u;
+                        break;
+                    }
+                    if (cand < ref) {
+                        a = a + 1u;                      // left child: same bound
+                    } else {
+                        // right child: bound = best hit of the left sibling's subtree, if any
+                        float m = bound;
+                        bool any = false;
+#pragma unroll
+                        for (int q = 0; q < PT_REPLAY_HITS; ++q) {
+                            if ((uint32_t)q < nh && h_idx[q] > a && h_idx[q] < ref) {
+                                if (!any || h_t[q] < m) m = h_t[q];
+                                any = true;
+                            }
+                        }
+                        bound = m;
+                        a = ref;
+                    }
+                }
             }
         }
         if (!overflow) break;
@@ -315,7 +428,7 @@ PT_HD int bvh_replay(const SceneView& S, const ReplayCfg& cfg, const Ray& ray, f
 }
 
 // src/scene.cpp:46-77: planes first (strict <), then the BVH bounded by the plane t
-template <class Stack>
+template <bool FAST, class Stack>
 PT_HD int ray_intersection(const SceneView& S, const ReplayCfg& cfg, const Ray& ray, Stack& stk, Hit& out,
                            Counts& C) {
     int id = -1;
@@ -329,7 +442,7 @@ PT_HD int ray_intersection(const SceneView& S, const ReplayCfg& cfg, const Ray& 
     Hit bh;
     int bid;
     bool fallback = true;
-    if (S.aux && replay_ok_ray(ray)) bid = bvh_replay(S, cfg, ray, closest, stk, bh, C, fallback);
+    if (S.aux && replay_ok_ray(ray)) bid = bvh_replay<FAST>(S, cfg, ray, closest, stk, bh, C, fallback);
     if (fallback) {
         if (S.aux) C.fallbacks++;
         bid = bvh_exact(S, ray, closest, stk, bh, C);
@@ -341,95 +454,131 @@ PT_HD int ray_intersection(const SceneView& S, const ReplayCfg& cfg, const Ray& 
 // per-vertex fold record modes
 enum : uint32_t { V_TERM = 0u, V_DIFFUSE = 1u, V_COL = 2u, V_IDENT = 3u };
 
+// One path vertex of RayTrace (src/scene.cpp:91-177) after a closest hit:
+// consumes the vertex's random numbers, returns its fold record
+// (idm = prim id | mode << 30, factors s1, s2) and whether the path continues
+// with `ray` set to the child ray.  Shared by the megakernel integrator and
+// the wavefront shade kernel.
+PT_HD bool shade_vertex(const SceneView& S, Rng& R, Ray& ray, const Hit& h, int id, uint32_t& idm, float& s1,
+                        float& s2) {
+    const float eps = 1e-4f;  // Scene::eps, include/scene.h:56
+    const Shade sh = S.shade[id];
+    const uint32_t mat = f2u(sh.s1.w);
+    const f3 p = ray.o + h.t * ray.d;
+    const f3 n = h.n;
+    if (mat == M_DIFFUSE) {
+        const f3 p_outer = p + eps * n;
+        const f3 dir = sample_mix(S, R, p_outer, n);
+        const float cosv = dot(dir, n);
+        if (cosv <= 0.f) { idm = (uint32_t)id | (V_TERM << 30); s1 = s2 = 0.f; return false; }
+        const float pw = pdf_mix(S, p_outer, n, dir);
+        idm = (uint32_t)id | (V_DIFFUSE << 30);
+        s1 = cosv;
+        s2 = 1.f / pw;
+        ray.o = p + eps * dir;
+        ray.d = dir;
+        return true;
+    }
+    if (mat == M_METALLIC) {
+        const f3 rd = reflect(n, normalize(ray.d));
+        idm = (uint32_t)id | (V_COL << 30);
+        s1 = s2 = 1.f;
+        ray.o = p + eps * rd;
+        ray.d = rd;
+        return true;
+    }
+    if (mat == M_DIELECTRIC) {
+        float eta1 = 1.f, eta2 = sh.s0.w;
+        if (h.interior) { const float tt = eta1; eta1 = eta2; eta2 = tt; }
+        const f3 dir = -1.f * normalize(ray.d);
+        const float cosn = dot(n, dir);
+        const float sin2 = (float)((double)(eta1 / eta2) * sqrt((double)smax(0.f, 1.f - cosn * cosn)));
+        bool refl;
+        if (fabs((double)sin2) > 1.0) {
+            refl = true;                                  // total internal reflection
+        } else {
+            const float q = (eta1 - eta2) / (eta1 + eta2);
+            const float r0 = (float)((double)q * (double)q);             // pow(q, 2.)
+            const float rr = (float)((double)r0 + (double)(1.f - r0) * pow5_cr((double)(1.f - cosn)));
+            refl = rng_uniform(R) < rr;
+        }
+        s1 = s2 = 1.f;
+        if (refl) {
+            const f3 rd = reflect(n, normalize(ray.d));
+            idm = (uint32_t)id | (V_IDENT << 30);
+            ray.o = p + eps * rd;
+            ray.d = rd;
+        } else {
+            const float cos2 = (float)sqrt((double)(1.f - sin2 * sin2));
+            const float k = eta1 / eta2;
+            const f3 rd = k * (-1.f * dir) + (k * cosn - cos2) * n;
+            idm = (uint32_t)id | ((h.interior ? V_IDENT : V_COL) << 30);
+            ray.o = p + eps * rd;
+            ray.d = rd;
+        }
+        return true;
+    }
+    idm = (uint32_t)id | (V_TERM << 30);   // unknown material: other = 0
+    s1 = s2 = 0.f;
+    return false;
+}
+
+// backward fold of one vertex record: L = E_k + ((A_k * L) * s1_k) * s2_k
+PT_HD f3 fold_vertex(const SceneView& S, f3 L, uint32_t idm, float s1, float s2) {
+    const uint32_t id = idm & 0x3fffffffu, mode = idm >> 30;
+    const Shade sh = S.shade[id];
+    const f3 E = mk3(sh.s1.x, sh.s1.y, sh.s1.z);
+    f3 other;
+    if (mode == V_TERM) {
+        other = mk3(0.f, 0.f, 0.f);
+    } else {
+        const f3 col = mk3(sh.s0.x, sh.s0.y, sh.s0.z);
+        f3 A;
+        if (mode == V_DIFFUSE) A = col / PT_PI_F;
+        else if (mode == V_COL) A = col;
+        else A = mk3(1.f, 1.f, 1.f);
+        other = ((A * L) * s1) * s2;
+    }
+    return E + other;
+}
+
 // One camera sample: src/scene.cpp:189-203 (inner) + RayTrace :83-178.
 // `vs` provides put(k, idmode, s1, s2) / get(k, idmode, s1, s2) for k < depth.
-template <class Stack, class VStore>
-PT_HD f3 trace_path(const SceneView& S, const ReplayCfg& cfg, Ray ray, uint32_t depth, Rng& R, Stack& stk, VStore& vs,
-                    Counts& C) {
-    const float eps = 1e-4f;  // Scene::eps, include/scene.h:56
+// `isect(ray, hit, counts)` is the closest-hit query (Scene::RayIntersection).
+template <class Isect, class VStore>
+PT_HD f3 trace_path_with(const SceneView& S, Isect&& isect, Ray ray, uint32_t depth, Rng& R, VStore& vs, Counts& C) {
     uint32_t nv = 0;
     f3 leaf = mk3(0.f, 0.f, 0.f);
     for (uint32_t rem = depth;; --rem) {
         if (rem == 0u) { leaf = mk3(0.f, 0.f, 0.f); break; }
         C.rays++;
         Hit h;
-        const int id = ray_intersection(S, cfg, ray, stk, h, C);
+        const int id = isect(ray, h, C);
         if (id == -1) { leaf = S.bg; break; }
-        const Shade sh = S.shade[id];
-        const uint32_t mat = f2u(sh.s1.w);
-        const f3 p = ray.o + h.t * ray.d;
-        const f3 n = h.n;
-        if (mat == M_DIFFUSE) {
-            const f3 p_outer = p + eps * n;
-            const f3 dir = sample_mix(S, R, p_outer, n);
-            const float cosv = dot(dir, n);
-            if (cosv <= 0.f) { vs.put(nv++, (uint32_t)id | (V_TERM << 30), 0.f, 0.f); break; }
-            const float pw = pdf_mix(S, p_outer, n, dir);
-            vs.put(nv++, (uint32_t)id | (V_DIFFUSE << 30), cosv, 1.f / pw);
-            ray.o = p + eps * dir;
-            ray.d = dir;
-        } else if (mat == M_METALLIC) {
-            const f3 rd = reflect(n, normalize(ray.d));
-            vs.put(nv++, (uint32_t)id | (V_COL << 30), 1.f, 1.f);
-            ray.o = p + eps * rd;
-            ray.d = rd;
-        } else if (mat == M_DIELECTRIC) {
-            float eta1 = 1.f, eta2 = sh.s0.w;
-            if (h.interior) { const float tt = eta1; eta1 = eta2; eta2 = tt; }
-            const f3 dir = -1.f * normalize(ray.d);
-            const float cosn = dot(n, dir);
-            const float sin2 = (float)((double)(eta1 / eta2) * sqrt((double)smax(0.f, 1.f - cosn * cosn)));
-            bool refl;
-            if (fabs((double)sin2) > 1.0) {
-                refl = true;                                  // total internal reflection
-            } else {
-                const float q = (eta1 - eta2) / (eta1 + eta2);
-                const float r0 = (float)((double)q * (double)q);             // pow(q, 2.)
-                const float rr = (float)((double)r0 + (double)(1.f - r0) * pow5_cr((double)(1.f - cosn)));
-                refl = rng_uniform(R) < rr;
-            }
-            if (refl) {
-                const f3 rd = reflect(n, normalize(ray.d));
-                vs.put(nv++, (uint32_t)id | (V_IDENT << 30), 1.f, 1.f);
-                ray.o = p + eps * rd;
-                ray.d = rd;
-            } else {
-                const float cos2 = (float)sqrt((double)(1.f - sin2 * sin2));
-                const float k = eta1 / eta2;
-                const f3 rd = k * (-1.f * dir) + (k * cosn - cos2) * n;
-                vs.put(nv++, (uint32_t)id | ((h.interior ? V_IDENT : V_COL) << 30), 1.f, 1.f);
-                ray.o = p + eps * rd;
-                ray.d = rd;
-            }
-        } else {
-            vs.put(nv++, (uint32_t)id | (V_TERM << 30), 0.f, 0.f);   // unknown material: other = 0
-            break;
-        }
+        uint32_t idm;
+        float s1, s2;
+        const bool cont = shade_vertex(S, R, ray, h, id, idm, s1, s2);
+        vs.put(nv++, idm, s1, s2);
+        if (!cont) break;
     }
-    // backward fold: L = E_k + ((A_k * L) * s1_k) * s2_k, deepest vertex first
+    // backward fold, deepest vertex first
     f3 L = leaf;
     while (nv > 0u) {
         --nv;
         uint32_t idm;
         float s1, s2;
         vs.get(nv, idm, s1, s2);
-        const uint32_t id = idm & 0x3fffffffu, mode = idm >> 30;
-        const Shade sh = S.shade[id];
-        const f3 E = mk3(sh.s1.x, sh.s1.y, sh.s1.z);
-        f3 other;
-        if (mode == V_TERM) {
-            other = mk3(0.f, 0.f, 0.f);
-        } else {
-            const f3 col = mk3(sh.s0.x, sh.s0.y, sh.s0.z);
-            f3 A;
-            if (mode == V_DIFFUSE) A = col / PT_PI_F;
-            else if (mode == V_COL) A = col;
-            else A = mk3(1.f, 1.f, 1.f);
-            other = ((A * L) * s1) * s2;
-        }
-        L = E + other;
+        L = fold_vertex(S, L, idm, s1, s2);
     }
     return L;
+}
+
+template <bool FAST, class Stack, class VStore>
+PT_HD f3 trace_path(const SceneView& S, const ReplayCfg& cfg, Ray ray, uint32_t depth, Rng& R, Stack& stk, VStore& vs,
+                    Counts& C) {
+    return trace_path_with(
+        S, [&](const Ray& r, Hit& h, Counts& c) { return ray_intersection<FAST>(S, cfg, r, stk, h, c); }, ray, depth, R,
+        vs, C);
 }
 
 }  // namespace pt

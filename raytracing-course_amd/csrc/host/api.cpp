@@ -7,6 +7,7 @@
 #include <hip/hip_runtime_api.h>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -47,6 +48,7 @@ struct DevScene {
     uint32_t* emitters = nullptr;
     float* thr = nullptr;
     pt::AuxNode* aux = nullptr;
+    pt::AuxSL* auxsl = nullptr;
 };
 
 constexpr uint32_t kCandCap = 24;   // candidate-list words per lane (per replay pass)
@@ -63,7 +65,8 @@ struct pt_scene {
     std::vector<pt::Prim> dprims;
     std::vector<pt::Shade> dshade;
     std::vector<pt::AuxNode> aux;
-    uint32_t tree_depth = 0, max_stack = 0, aux_depth = 0;
+    std::vector<pt::AuxSL> auxsl;
+    uint32_t tree_depth = 0, max_stack = 0, aux_depth = 0, auxsl_depth = 0;
     float thr[256];
     std::map<int, DevScene> dev;
     std::mutex mu;
@@ -79,6 +82,15 @@ struct pt_session {
     unsigned long long* counters = nullptr;
     uint8_t* out = nullptr;
     float* rad = nullptr;
+    unsigned long long* wg_prof = nullptr;
+    // wavefront engine buffers (replay traversal)
+    bool wave = false;
+    uint32_t* pstate = nullptr;
+    pt::F4* qbuf = nullptr;       // 5 * n_slots F4: q0.ro, q0.rd, q1.ro, q1.rd, hits.th
+    uint32_t* hid = nullptr;      // n_slots
+    uint32_t* fb = nullptr;       // n_slots
+    uint32_t* ctl = nullptr;      // 3 * (depth + 1)
+    uint32_t isect_grid = 0;
     hipStream_t stream = nullptr;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
     double kernel_ms = 0.0, resolve_ms = 0.0;
@@ -181,6 +193,7 @@ int ensure_device_scene(pt_scene* s, int dev, DevScene** out) {
     std::vector<float> thr(s->thr, s->thr + 256);
     if ((rc = upload(&d.thr, thr))) return rc;
     if ((rc = upload(&d.aux, s->aux))) return rc;
+    if ((rc = upload(&d.auxsl, s->auxsl))) return rc;
     s->dev[dev] = d;
     *out = &s->dev[dev];
     return PT_OK;
@@ -189,6 +202,7 @@ int ensure_device_scene(pt_scene* s, int dev, DevScene** out) {
 void free_device_scene(DevScene& d) {
     (void)hipFree(d.nodes); (void)hipFree(d.prims); (void)hipFree(d.shade);
     (void)hipFree(d.planes); (void)hipFree(d.emitters); (void)hipFree(d.thr); (void)hipFree(d.aux);
+    (void)hipFree(d.auxsl);
 }
 
 // per-lane LDS words: replay needs [aux stack | candidates], the exact DFS its stack
@@ -325,6 +339,7 @@ int pt_scene_prepare(pt_scene* s) {
         }
         build_device_layout(s);
         pth::build_aux_bvh(s->nodes, s->aux, s->aux_depth);
+        pth::build_aux_stackless(s->aux, s->dnodes, s->auxsl, s->auxsl_depth);
         pth::build_gamma_thresholds(s->thr);
     } catch (const std::exception& e) {
         return fail(PT_E_SCENE, e.what());
@@ -437,6 +452,22 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         hipMalloc(&ss->out, 3 * n) != hipSuccess)
         return cleanup(fail(PT_E_OOM, "device allocation failed"));
     ss->st.n_slots = ss->n_slots;
+    // engine: the wavefront pipeline for the (filtered) replay traversal; the
+    // megakernel for the exact DFS and the division-form replay (PT_ENGINE=mega forces it)
+    ss->wave = o->traversal == PT_TRAVERSAL_REPLAY;
+    if (const char* e = getenv("PT_ENGINE")) ss->wave = ss->wave && strcmp(e, "mega") != 0;
+    if (ss->wave) {
+        if (hipMalloc(&ss->pstate, n * 4) != hipSuccess || hipMalloc(&ss->qbuf, 5 * n * 16) != hipSuccess ||
+            hipMalloc(&ss->hid, n * 4) != hipSuccess || hipMalloc(&ss->fb, n * 4) != hipSuccess ||
+            hipMalloc(&ss->ctl, 4ull * 3 * (ss->depth + 1)) != hipSuccess)
+            return cleanup(fail(PT_E_OOM, "device allocation failed (wavefront buffers)"));
+        hipDeviceProp_t pr;
+        if (hipGetDeviceProperties(&pr, ss->dev) != hipSuccess) return cleanup(fail(PT_E_HIP, "device query failed"));
+        // persistent intersection grid: 8 workgroups (32 waves) per CU, capped by the work
+        ss->isect_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * 8u;
+        if (const char* g = getenv("PT_ISECT_WG_PER_CU")) ss->isect_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * (uint32_t)std::max(1, atoi(g));
+        ss->isect_grid = std::min(ss->isect_grid, std::max(1u, ss->n_tiles_local));
+    }
     if (hipMemsetAsync(ss->counters, 0, 64, ss->stream) != hipSuccess) return cleanup(fail(PT_E_HIP, "memset failed"));
     if (ss->n_tiles_local) {
         pt::InitParams ip;
@@ -456,10 +487,58 @@ int pt_session_layout(const pt_session* ss, uint32_t* n_tiles, uint64_t* packed_
     return PT_OK;
 }
 
+namespace {
+int trace_wave(pt_session* ss, uint32_t spp) {
+    DevScene& ds = ss->sc->dev[ss->dev];
+    const pt_scene* s = ss->sc;
+    pt::WaveParams wp;
+    memset(&wp, 0, sizeof(wp));
+    wp.S.aux = nullptr;
+    wp.S.nodes = ds.nodes;
+    wp.S.prims = ds.prims;
+    wp.S.shade = ds.shade;
+    wp.S.planes = ds.planes;
+    wp.S.emitters = ds.emitters;
+    wp.S.n_planes = (uint32_t)s->planes.size();
+    wp.S.n_emitters = (uint32_t)s->emitters.size();
+    wp.S.bg = pt::mk3(s->hs.bg[0], s->hs.bg[1], s->hs.bg[2]);
+    wp.aux = ds.auxsl;
+    wp.n_aux = (uint32_t)s->auxsl.size();
+    wp.cam = ss->cam;
+    wp.tm = ss->tm;
+    wp.st = ss->st;
+    wp.vscratch = ss->vscratch;
+    wp.pstate = ss->pstate;
+    const size_t n = std::max<size_t>(ss->n_slots, 1);
+    wp.q[0].ro = ss->qbuf;
+    wp.q[0].rd = ss->qbuf + n;
+    wp.q[1].ro = ss->qbuf + 2 * n;
+    wp.q[1].rd = ss->qbuf + 3 * n;
+    wp.hits.th = ss->qbuf + 4 * n;
+    wp.hits.id = ss->hid;
+    wp.fb = ss->fb;
+    wp.ctl = ss->ctl;
+    wp.counters = ss->counters;
+    wp.depth = ss->depth;
+    wp.n_tiles_local = ss->n_tiles_local;
+    wp.max_stack = std::max<uint32_t>(s->max_stack, 1u);
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, ss->stream));
+    for (uint32_t k = 0; k < spp; ++k) HIP_TRY(pt_launch_wave_sample(wp, ss->isect_grid, ss->stream));
+    HIP_TRY(hipEventRecord(e1, ss->stream));
+    ss->pending.emplace_back(e0, e1);
+    ss->samples_done += spp;
+    return PT_OK;
+}
+}  // namespace
+
 int pt_session_trace(pt_session* ss, uint32_t spp) {
     if (!ss) return fail(PT_E_INVALID, "null session");
     if (spp == 0 || ss->n_tiles_local == 0) { ss->samples_done += spp; return PT_OK; }
     HIP_TRY(hipSetDevice(ss->dev));
+    if (ss->wave) return trace_wave(ss, spp);
     DevScene& ds = ss->sc->dev[ss->dev];
     pt::TraceParams tp;
     const pt_scene* s = ss->sc;
@@ -480,14 +559,37 @@ int pt_session_trace(pt_session* ss, uint32_t spp) {
     tp.counters = ss->counters;
     tp.depth = ss->depth;
     tp.spp = spp;
+    tp.n_tiles_local = ss->n_tiles_local;
+    tp.wg_prof = nullptr;
+    // kernel variant: filtered tests unless the division form was asked for;
+    // XCD-banded tile order by default (PT_VARIANT=<0..3> overrides, for A/B runs)
+    int variant = (ss->traversal == PT_TRAVERSAL_REPLAY ? 1 : 0) | 2;
+    if (const char* v = getenv("PT_VARIANT")) variant = atoi(v) & 3;
+    if (ss->traversal == PT_TRAVERSAL_EXACT) variant &= 2;
+    const char* wgp = getenv("PT_WGPROF");
+    if (wgp && *wgp) {
+        if (!ss->wg_prof) HIP_TRY(hipMalloc(&ss->wg_prof, 32ull * std::max(ss->n_tiles_local, 1u)));
+        HIP_TRY(hipMemsetAsync(ss->wg_prof, 0, 32ull * std::max(ss->n_tiles_local, 1u), ss->stream));
+        tp.wg_prof = ss->wg_prof;
+    }
     const uint32_t lds = 256u * 4u * lane_words(s, ss->traversal);
     if (lds > 160u * 1024u) return fail(PT_E_SCENE, "BVH too deep for the LDS traversal stack");
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
     HIP_TRY(hipEventRecord(e0, ss->stream));
-    HIP_TRY(pt_launch_trace(tp, ss->n_tiles_local, lds, ss->stream));
+    HIP_TRY(pt_launch_trace(tp, variant, lds, ss->stream));
     HIP_TRY(hipEventRecord(e1, ss->stream));
+    if (tp.wg_prof) {
+        // diagnostics: append this launch's per-workgroup timeline to $PT_WGPROF
+        std::vector<unsigned long long> h(4ull * ss->n_tiles_local);
+        HIP_TRY(hipMemcpyAsync(h.data(), tp.wg_prof, h.size() * 8, hipMemcpyDeviceToHost, ss->stream));
+        HIP_TRY(hipStreamSynchronize(ss->stream));
+        if (FILE* f = fopen(wgp, "ab")) {
+            fwrite(h.data(), 8, h.size(), f);
+            fclose(f);
+        }
+    }
     ss->pending.emplace_back(e0, e1);
     ss->samples_done += spp;
     return PT_OK;
@@ -560,7 +662,7 @@ int pt_session_stats(pt_session* ss, pt_stats* st) {
     st->resolve_ms = ss->resolve_ms;
     st->node_bytes = sizeof(pt::Node);
     st->prim_bytes = sizeof(pt::Prim);
-    st->aux_bytes = sizeof(pt::AuxNode);
+    st->aux_bytes = ss->wave ? sizeof(pt::AuxSL) : sizeof(pt::AuxNode);
     return PT_OK;
 }
 
@@ -573,7 +675,9 @@ void pt_session_free(pt_session* ss) {
     finish_pending(ss);
     (void)hipFree(ss->st.rng_x); (void)hipFree(ss->st.rng_saved); (void)hipFree(ss->st.rng_flag);
     (void)hipFree(ss->st.sum); (void)hipFree(ss->vscratch); (void)hipFree(ss->counters);
-    (void)hipFree(ss->out); (void)hipFree(ss->rad);
+    (void)hipFree(ss->out); (void)hipFree(ss->rad); (void)hipFree(ss->wg_prof);
+    (void)hipFree(ss->pstate); (void)hipFree(ss->qbuf); (void)hipFree(ss->hid); (void)hipFree(ss->fb);
+    (void)hipFree(ss->ctl);
     if (ss->stream) (void)hipStreamDestroy(ss->stream);
     delete ss;
 }
@@ -616,7 +720,7 @@ void pt_render_opts_default(pt_render_opts* o) {
     memset(o, 0, sizeof(*o));
     o->device = 0;
     o->ngpu = 1;
-    o->traversal = PT_TRAVERSAL_EXACT;
+    o->traversal = PT_TRAVERSAL_REPLAY;
 }
 
 int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radiance, pt_stats* stats) {
@@ -742,7 +846,16 @@ int pt_selftest_ray_intersection(pt_scene* s, int32_t traversal, uint32_t n, con
         r.o = pt::mk3(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
         r.d = pt::mk3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
         pt::Hit h;
-        const int id = pt::ray_intersection(V, cfg, r, stk, h, C);
+        int id;
+        if (traversal == PT_TRAVERSAL_REPLAY) {
+            pt::QCounts Q{0u, 0u, 0u, 0u};
+            uint32_t ex = 0;
+            id = pt::q_run(V, s->auxsl.data(), (uint32_t)s->auxsl.size(), r, stk, h, Q, ex);
+            C.rays++;
+            C.nodes += Q.nodes; C.ptests += Q.ptests; C.planes += Q.planes; C.aux += Q.aux; C.fallbacks += ex;
+        } else {
+            id = pt::ray_intersection<false>(V, cfg, r, stk, h, C);
+        }
         ids[i] = id;
         const bool ok = id != -1;
         hits[5 * i] = ok ? h.t : 0.f;
@@ -781,7 +894,20 @@ int pt_selftest_render_host(pt_scene* s, int32_t traversal, uint32_t x0, uint32_
                 for (uint32_t i = 0; i < S; ++i) {
                     const float fx = (float)x + pt::rng_uniform(R);
                     const float fy = (float)y + pt::rng_uniform(R);
-                    sum = sum + pt::trace_path(V, cfg, pt::camera_ray(cam, fx, fy), s->hs.depth, R, stk, vs, C);
+                    const pt::Ray ray = pt::camera_ray(cam, fx, fy);
+                    if (traversal == PT_TRAVERSAL_REPLAY) {
+                        // the wavefront engine's query (pt_query.h state machine), run to completion
+                        auto q = [&](const pt::Ray& rr, pt::Hit& hh, pt::Counts& cc) {
+                            pt::QCounts Q{0u, 0u, 0u, 0u};
+                            uint32_t ex = 0;
+                            const int id = pt::q_run(V, s->auxsl.data(), (uint32_t)s->auxsl.size(), rr, stk, hh, Q, ex);
+                            cc.fallbacks += ex;
+                            return id;
+                        };
+                        sum = sum + pt::trace_path_with(V, q, ray, s->hs.depth, R, vs, C);
+                    } else {
+                        sum = sum + pt::trace_path<false>(V, cfg, ray, s->hs.depth, R, stk, vs, C);
+                    }
                 }
                 const pt::f3 m = (1.f / (float)S) * sum;
                 radiance[3 * k] = m.x; radiance[3 * k + 1] = m.y; radiance[3 * k + 2] = m.z;

@@ -168,3 +168,80 @@ void build_aux_bvh(const std::vector<HNode>& nodes, std::vector<pt::AuxNode>& ou
 }
 
 }  // namespace pth
+
+namespace pth {
+
+// Stackless preorder form of the auxiliary BVH (pt_query.h AuxSL): every node
+// carries its own box and the index one past its subtree (skip link).
+// Internal boxes are the inflated (conservative) child boxes of the pair
+// tree; leaves carry the reference leaf's exact (center, half-size) record,
+// so the query's leaf test IS the reference slab test.
+void build_aux_stackless(const std::vector<pt::AuxNode>& pairs, const std::vector<pt::Node>& dnodes,
+                         std::vector<pt::AuxSL>& out, uint32_t& max_depth) {
+    out.clear();
+    max_depth = 0;
+    auto child = [&](const pt::AuxNode& n, int k, float lo[3], float hi[3]) {
+        const float* f = reinterpret_cast<const float*>(&n) + 6 * k;
+        for (int a = 0; a < 3; ++a) { lo[a] = f[a]; hi[a] = f[3 + a]; }
+        return reinterpret_cast<const uint32_t*>(&n)[12 + k];
+    };
+    struct Item { uint32_t code; float lo[3], hi[3]; uint32_t depth; };
+    // explicit preorder walk; skip links are patched when a subtree closes
+    std::vector<std::pair<uint32_t, uint32_t>> open;  // (out index of internal node, depth)
+    std::vector<Item> st;
+    {
+        Item r;
+        r.code = 0;  // aux pair node 0 = root (internal unless the tree is a single leaf pair)
+        float l0[3], h0[3], l1[3], h1[3];
+        const uint32_t c1 = child(pairs[0], 1, l1, h1);
+        child(pairs[0], 0, l0, h0);
+        for (int a = 0; a < 3; ++a) {
+            r.lo[a] = c1 == 0xFFFFFFFFu ? l0[a] : std::min(l0[a], l1[a]);
+            r.hi[a] = c1 == 0xFFFFFFFFu ? h0[a] : std::max(h0[a], h1[a]);
+        }
+        r.depth = 0;
+        st.push_back(r);
+    }
+    while (!st.empty()) {
+        const Item it = st.back();
+        st.pop_back();
+        // close every open internal node that is not an ancestor of this item
+        while (!open.empty() && open.back().second >= it.depth) {
+            const uint32_t idx = open.back().first;
+            reinterpret_cast<uint32_t*>(&out[idx])[6] = (uint32_t)out.size();
+            open.pop_back();
+        }
+        max_depth = std::max(max_depth, it.depth + 1);
+        pt::AuxSL n;
+        uint32_t* u = reinterpret_cast<uint32_t*>(&n);
+        float* f = reinterpret_cast<float*>(&n);
+        if (it.code & 0x80000000u) {
+            const uint32_t leaf = it.code & 0x7fffffffu;
+            const pt::Node& r = dnodes[leaf];
+            f[0] = r.a.x; f[1] = r.a.y; f[2] = r.a.z; f[3] = r.a.w; f[4] = r.b.x; f[5] = r.b.y;
+            u[6] = (uint32_t)out.size() + 1u;
+            u[7] = leaf;
+            out.push_back(n);
+            continue;
+        }
+        f[0] = it.lo[0]; f[1] = it.lo[1]; f[2] = it.lo[2]; f[3] = it.hi[0]; f[4] = it.hi[1]; f[5] = it.hi[2];
+        u[6] = 0;
+        u[7] = PT_AUX_INTERNAL;
+        open.emplace_back((uint32_t)out.size(), it.depth);
+        out.push_back(n);
+        const pt::AuxNode& p = pairs[it.code];
+        for (int k = 1; k >= 0; --k) {  // push right first: left child is visited next (index + 1)
+            Item c;
+            c.code = child(p, k, c.lo, c.hi);
+            if (c.code == 0xFFFFFFFFu) continue;
+            c.depth = it.depth + 1;
+            st.push_back(c);
+        }
+    }
+    while (!open.empty()) {
+        reinterpret_cast<uint32_t*>(&out[open.back().first])[6] = (uint32_t)out.size();
+        open.pop_back();
+    }
+}
+
+}  // namespace pth

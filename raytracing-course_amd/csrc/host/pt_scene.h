@@ -6,7 +6,7 @@
 #include <string>
 #include <vector>
 
-#include "../device/pt_core.h"
+#include "../device/pt_query.h"
 
 namespace pth {
 
@@ -48,6 +48,10 @@ void build_reference_bvh(std::vector<HPrim>& prims, uint32_t n, std::vector<HNod
 
 // Auxiliary BVH2 over the reference leaf boxes (aux_bvh.cpp)
 void build_aux_bvh(const std::vector<HNode>& nodes, std::vector<pt::AuxNode>& out, uint32_t& max_depth);
+
+// Stackless preorder form of the auxiliary BVH for the wavefront query (aux_bvh.cpp)
+void build_aux_stackless(const std::vector<pt::AuxNode>& pairs, const std::vector<pt::Node>& dnodes,
+                         std::vector<pt::AuxSL>& out, uint32_t& max_depth);
 
 // Gamma/quantise threshold table (tonemap.cpp)
 void build_gamma_thresholds(float thr[256]);

@@ -24,6 +24,7 @@ PT_OK = 0
 PT_E_INVALID, PT_E_IO, PT_E_SCENE, PT_E_NO_GPU, PT_E_HIP, PT_E_RCCL, PT_E_OOM = -1, -2, -3, -4, -5, -6, -7
 TRAVERSAL_REPLAY = 0
 TRAVERSAL_EXACT = 1
+TRAVERSAL_REPLAY_DIV = 2
 
 # One HIP runtime per process: PyTorch bundles its own libamdhip64 (soname
 # libamdhip64.so.7, but its users link the unversioned name), so loading

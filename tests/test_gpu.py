@@ -20,7 +20,7 @@ def pt():
     return mod
 
 
-TRAVERSALS = {"replay": 0, "exact": 1}
+TRAVERSALS = {"replay": 0, "exact": 1, "replay_div": 2}
 
 
 @pytest.mark.parametrize("trav", sorted(TRAVERSALS))

@@ -110,7 +110,7 @@ def test_scene_errors():
         assert e.value.code == pt.PT_E_SCENE
 
 
-TRAVERSALS = {"replay": 0, "exact": 1}
+TRAVERSALS = {"replay": 0, "exact": 1, "replay_div": 2}
 
 
 @pytest.mark.parametrize("trav", sorted(TRAVERSALS))
