@@ -197,6 +197,7 @@ struct SceneView {
     const uint32_t* emitters;   // prim indices of BOX/ELLIPSOID emitters
     uint32_t n_planes, n_emitters;
     f3 bg;
+    float box_extent;           // max |coordinate| over the reference node boxes (replay certification)
 };
 
 struct Ray { f3 o, d; };

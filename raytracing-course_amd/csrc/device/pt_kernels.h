@@ -76,6 +76,7 @@ struct WaveParams {
     uint32_t bounce;
     uint32_t n_tiles_local;
     uint32_t max_stack;           // exact DFS stack words per lane
+    uint32_t aux_stack;           // wide aux traversal stack words per lane (LDS)
 };
 
 struct ResolveParams {

@@ -29,6 +29,9 @@ namespace pt {
 #ifndef PT_QK
 #define PT_QK 16
 #endif
+#ifndef PT_AUXW
+#define PT_AUXW 4               // auxiliary BVH width (nodes = PT_AUXW AuxSL entries)
+#endif
 
 // stackless auxiliary node (32 B):
 //   internal: a = {lo.x, lo.y, lo.z, hi.x}, b = {hi.y, hi.z, u32 skip, 0xffffffff}
@@ -50,9 +53,12 @@ struct Query {
     float P;                    // closest plane t (the BVH bound at the root)
     uint32_t phase;
     uint32_t node;              // Q_AUX: aux node; Q_REPLAY: reference node on the current path
+    uint32_t sp;                // Q_AUX: pending aux nodes on the per-lane stack
     uint32_t lb;                // every candidate below lb has been processed
     uint32_t cand, skip, last;
     float bound;
+    float dl;                   // certification margin (t units, see q_leaf_certain)
+    uint32_t walk;              // Q_REPLAY: 0 = candidate leaf check, 1 = walking its root path
     uint32_t overflow;
     uint32_t c[PT_QK];          // sorted candidates of this pass (0xffffffff = empty)
     uint32_t nh;
@@ -64,6 +70,9 @@ struct Query {
 
 struct QCounts {
     uint32_t nodes, aux, ptests, planes;
+#ifdef PT_QDIAG
+    uint32_t cands, passes;
+#endif
 };
 
 // planes (src/scene.cpp:50-57), then the BVH set-up
@@ -84,11 +93,15 @@ PT_HD void q_init(const SceneView& S, const Ray& ray, Query& q, QCounts& C) {
     q.lb = 0;
     q.overflow = 0;
     q.node = 0;
+    q.sp = 0;
 #pragma unroll
     for (int i = 0; i < PT_QK; ++i) q.c[i] = 0xffffffffu;
     if (!replay_ok_ray(ray)) { q.phase = Q_EXACT; return; }
     q.inv = mk3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
     q.oinv = mk3(ray.o.x * q.inv.x, ray.o.y * q.inv.y, ray.o.z * q.inv.z);
+    const float om = fmaxf(fmaxf(fabsf(ray.o.x), fabsf(ray.o.y)), fabsf(ray.o.z));
+    const float dm = fminf(fminf(fabsf(ray.d.x), fabsf(ray.d.y)), fabsf(ray.d.z));
+    q.dl = 0x1p-18f * (S.box_extent + om) / dm;
     q.phase = Q_AUX;
 }
 
@@ -118,8 +131,7 @@ PT_HD void q_next_candidate(Query& q) {
         q.last = v;
         if (v >= q.skip) {
             q.cand = v;
-            q.node = 0;
-            q.bound = q.P;
+            q.walk = 0;
             q.phase = Q_REPLAY;
             return;
         }
@@ -129,39 +141,138 @@ PT_HD void q_next_candidate(Query& q) {
         q.lb = q.skip > q.last + 1u ? q.skip : q.last + 1u;
         q.overflow = 0;
         q.node = 0;
+        q.sp = 0;
         q.phase = Q_AUX;
         return;
     }
     q.phase = Q_DONE;
 }
 
-// Advance one node visit.  Precondition: phase is Q_AUX or Q_REPLAY.
-PT_HD void q_step(const SceneView& S, const AuxSL* aux, uint32_t n_aux, Query& q, QCounts& C) {
-    if (q.phase == Q_AUX) {
-        const AuxSL an = aux[q.node];
-        C.aux++;
-        const uint32_t skip = f2u(an.b.z), code = f2u(an.b.w);
-        uint32_t next;
-        if (code == PT_AUX_INTERNAL) {
-            next = aux_box(an.a.x, an.a.y, an.a.z, an.a.w, an.b.x, an.b.y, q.inv, q.oinv) ? q.node + 1u : skip;
-        } else {
-            if (code >= q.lb) {
-                Node nd;
-                nd.a = an.a;
-                nd.b = an.b;
-                if (node_enter(nd, q.ray, q.inv, PT_INF)) q_insert(q, code);
-            }
-            next = skip;
+// leaf reached: first-min over its primitives (src/bvh.cpp:205-213), hit bookkeeping
+PT_HD void q_leaf_hit(const SceneView& S, Query& q, uint32_t a, uint32_t ref, uint32_t cnt, QCounts& C) {
+    Hit lbh;
+    lbh.t = PT_INF;
+    int lid = -1;
+    for (uint32_t i = ref; i < ref + cnt; ++i) {
+        Hit h;
+        C.ptests++;
+        if (prim_intersect(S.prims[i], q.ray, h) && h.t < lbh.t) { lbh = h; lid = (int)i; }
+    }
+    if (lid >= 0) {
+        if (q.nh == PT_REPLAY_HITS) { q.phase = Q_EXACT; return; }
+#pragma unroll
+        for (int k = 0; k < PT_REPLAY_HITS; ++k)
+            if ((uint32_t)k == q.nh) { q.H.idx[k] = a; q.H.t[k] = lbh.t; }
+        ++q.nh;
+        // BVH result = first strict minimum; it replaces the plane hit iff strictly closer
+        if (lbh.t < q.bt) {
+            q.bt = lbh.t;
+            if (lbh.t < q.P) { q.res = lbh; q.res_id = lid; }
         }
-        q.node = next;
-        if (next >= n_aux) {
-            // aux pass complete: replay the candidates in reference preorder
-            q.skip = q.lb;
+    }
+    q.skip = a + 1u;
+    q_next_candidate(q);
+}
+
+// Candidate leaf check before any root-path replay.  Every bound the replay
+// can carry is P or a minimum over earlier hits, so it lies in [lo, hi] =
+// [min, max](P, recorded hits).
+//  * certain accept: the ray crosses the leaf box robustly (slab interval
+//    longer than 2 margins, exit beyond the margin) and lo >= entry + margin.
+//    Every ancestor's box contains the leaf's (the reference builds them as
+//    exact min/max unions); their stored (center, half-size) records and the
+//    float slab evaluation move interval ends by at most the margin
+//    dl = 2^-18 (X + |o|max) / |d|min + 2^-18 |t| (X = scene box extent;
+//    rounding of c/s <= 2^-23 X each, of o and the numerators <= 2^-24 each,
+//    quotients 2^-24 relative, the multiply-by-reciprocal form 2^-20; >= 4x
+//    headroom).  So every ancestor is hit with entry <= leaf entry + margin
+//    <= its bound (or is interior): no ancestor prunes and the leaf is entered.
+//  * certain reject: the leaf's own exact test fails even against hi (its
+//    actual bound is <= hi): it is not entered whatever its ancestors do.
+// Returns 1 = accept, 0 = reject, 2 = undecided (replay the root path).
+PT_HD uint32_t q_leaf_certain(const Query& q, const Node& nd) {
+    float lo = q.P, hi = q.P;
+#pragma unroll
+    for (int k = 0; k < PT_REPLAY_HITS; ++k)
+        if ((uint32_t)k < q.nh) { lo = fminf(lo, q.H.t[k]); hi = fmaxf(hi, q.H.t[k]); }
+    const f3 c = mk3(nd.a.x, nd.a.y, nd.a.z);
+    const f3 s = mk3(nd.a.w, nd.b.x, nd.b.y);
+    const f3 o = q.ray.o + -1.f * c;
+    const f3 nlo = -1.f * s - o, nhi = s - o;
+    const float ax = nlo.x * q.inv.x, bx = nhi.x * q.inv.x;
+    const float ay = nlo.y * q.inv.y, by = nhi.y * q.inv.y;
+    const float az = nlo.z * q.inv.z, bz = nhi.z * q.inv.z;
+    const float t1 = smax(smax(smin(ax, bx), smin(ay, by)), smin(az, bz));
+    const float t2 = smin(smin(smax(ax, bx), smax(ay, by)), smax(az, bz));
+    const float m = q.dl + (fabsf(t1) + fabsf(t2)) * 0x1p-18f;
+    if (t1 + m <= t2 - m && t2 - m >= 0.f && lo >= t1 + m) return 1u;
+    if (!node_enter(nd, q.ray, q.inv, hi)) return 0u;
+    return 2u;
+}
+
+// Advance one node visit.  Precondition: phase is Q_AUX or Q_REPLAY.
+// `stk` = per-lane word memory for the pending aux nodes (set/get).
+template <class Mem>
+PT_HD void q_step(const SceneView& S, const AuxSL* aux, uint32_t n_aux, Query& q, QCounts& C, Mem& stk) {
+    if (q.phase == Q_AUX) {
+        // one wide node: PT_AUXW child entries (independent loads)
+        AuxSL e[PT_AUXW];
+#pragma unroll
+        for (int k = 0; k < PT_AUXW; ++k) e[k] = aux[q.node * PT_AUXW + k];
+        C.aux++;
+        uint32_t next = 0xffffffffu;
+#pragma unroll
+        for (int k = 0; k < PT_AUXW; ++k) {
+            const uint32_t code = f2u(e[k].b.w);
+            if (code == 0xffffffffu) continue;
+            if (code & 0x80000000u) {
+                const uint32_t leaf = code & 0x7fffffffu;
+                if (leaf < q.lb) continue;
+                Node nd;
+                nd.a = e[k].a;
+                nd.b = e[k].b;
+                if (node_enter(nd, q.ray, q.inv, PT_INF)) {
+#ifdef PT_QDIAG
+                    C.cands++;
+#endif
+                    q_insert(q, leaf);
+                }
+            } else if (aux_box(e[k].a.x, e[k].a.y, e[k].a.z, e[k].a.w, e[k].b.x, e[k].b.y, q.inv, q.oinv)) {
+                if (next == 0xffffffffu) next = code;
+                else stk.set(q.sp++, code);
+            }
+        }
+        if (next == 0xffffffffu && q.sp > 0u) next = stk.get(--q.sp);
+        if (next != 0xffffffffu) {
+            q.node = next;
+            return;
+        }
+#ifdef PT_QDIAG
+        C.passes++;
+#endif
+        // aux pass complete: replay the candidates in reference preorder
+        q.skip = q.lb;
+        q_next_candidate(q);
+        return;
+    }
+    if (!q.walk) {
+        // Q_REPLAY, first visit of a candidate: its own leaf record
+        const Node nd = S.nodes[q.cand];
+        C.nodes++;
+        const uint32_t v = q_leaf_certain(q, nd);
+        if (v == 1u) {
+            q_leaf_hit(S, q, q.cand, f2u(nd.b.z), f2u(nd.b.w), C);
+        } else if (v == 0u) {
+            q.skip = q.cand + 1u;
             q_next_candidate(q);
+        } else {
+            q.walk = 1u;
+            q.node = 0u;
+            q.bound = q.P;
         }
         return;
     }
-    // Q_REPLAY: one node of the root -> cand path
+    // Q_REPLAY, undecided candidate: one node of the root -> cand path
     const Node nd = S.nodes[q.node];
     C.nodes++;
     const uint32_t a = q.node;
@@ -172,29 +283,7 @@ PT_HD void q_step(const SceneView& S, const AuxSL* aux, uint32_t n_aux, Query& q
         return;
     }
     if (a == q.cand) {
-        // leaf reached: first-min over its primitives (src/bvh.cpp:205-213)
-        Hit lbh;
-        lbh.t = PT_INF;
-        int lid = -1;
-        for (uint32_t i = ref; i < ref + info; ++i) {
-            Hit h;
-            C.ptests++;
-            if (prim_intersect(S.prims[i], q.ray, h) && h.t < lbh.t) { lbh = h; lid = (int)i; }
-        }
-        if (lid >= 0) {
-            if (q.nh == PT_REPLAY_HITS) { q.phase = Q_EXACT; return; }
-#pragma unroll
-            for (int k = 0; k < PT_REPLAY_HITS; ++k)
-                if ((uint32_t)k == q.nh) { q.H.idx[k] = a; q.H.t[k] = lbh.t; }
-            ++q.nh;
-            // BVH result = first strict minimum; it replaces the plane hit iff strictly closer
-            if (lbh.t < q.bt) {
-                q.bt = lbh.t;
-                if (lbh.t < q.P) { q.res = lbh; q.res_id = lid; }
-            }
-        }
-        q.skip = a + 1u;
-        q_next_candidate(q);
+        q_leaf_hit(S, q, a, ref, info, C);
         return;
     }
     if (q.cand < ref) {
@@ -236,7 +325,7 @@ PT_HD int q_run(const SceneView& S, const AuxSL* aux, uint32_t n_aux, const Ray&
                 QCounts& C, uint32_t& exact_used) {
     Query q;
     q_init(S, ray, q, C);
-    while (q.phase == Q_AUX || q.phase == Q_REPLAY) q_step(S, aux, n_aux, q, C);
+    while (q.phase == Q_AUX || q.phase == Q_REPLAY) q_step(S, aux, n_aux, q, C, stk);
     exact_used = q.phase == Q_EXACT ? 1u : 0u;
     if (exact_used) return q_exact(S, ray, stk, out, C);
     out = q.res;

@@ -67,6 +67,8 @@ __device__ __forceinline__ void write_hit(const WaveParams& P, uint32_t qi, int 
 #define PT_REFILL_MIN 16u
 
 __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
+    extern __shared__ uint32_t lds_stack[];
+    LdsMem stk{lds_stack + threadIdx.x};
     const uint32_t b = P.bounce;
     const uint32_t count = P.ctl[b];
     uint32_t* head = P.ctl + P.depth + 1u + b;
@@ -115,7 +117,7 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
         }
         if (__ballot(active) == 0ull) break;
         if (active) {
-            if (q.phase == Q_AUX || q.phase == Q_REPLAY) q_step(P.S, P.aux, P.n_aux, q, C);
+            if (q.phase == Q_AUX || q.phase == Q_REPLAY) q_step(P.S, P.aux, P.n_aux, q, C, stk);
             if (q.phase == Q_DONE) {
                 write_hit(P, qi, q.res_id, q.res);
                 active = false;
@@ -241,7 +243,7 @@ hipError_t pt_launch_wave_sample(pt::WaveParams p, uint32_t isect_grid, hipStrea
     const uint32_t exact_lds = 64u * 4u * (p.max_stack ? p.max_stack : 1u);
     for (uint32_t b = 0; b < D; ++b) {
         p.bounce = b;
-        hipLaunchKernelGGL(pt::k_wisect, dim3(isect_grid), dim3(256), 0, s, p);
+        hipLaunchKernelGGL(pt::k_wisect, dim3(isect_grid), dim3(256), 1024u * p.aux_stack, s, p);
         hipLaunchKernelGGL(pt::k_wexact, dim3(64), dim3(64), exact_lds, s, p);
         hipLaunchKernelGGL(pt::k_wshade, dim3(nt), dim3(256), 0, s, p);
     }

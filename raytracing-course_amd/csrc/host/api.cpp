@@ -6,11 +6,13 @@
 
 #include <hip/hip_runtime_api.h>
 #include <math.h>
+#include <cmath>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <fstream>
 #include <map>
@@ -67,6 +69,8 @@ struct pt_scene {
     std::vector<pt::AuxNode> aux;
     std::vector<pt::AuxSL> auxsl;
     uint32_t tree_depth = 0, max_stack = 0, aux_depth = 0, auxsl_depth = 0;
+    float box_extent = 0.f;     // max |coordinate| of the reference node boxes
+    uint32_t auxw_stack = 0;    // per-lane stack words of the wide aux traversal
     float thr[256];
     std::map<int, DevScene> dev;
     std::mutex mu;
@@ -229,6 +233,7 @@ pt::SceneView host_view(const pt_scene* s, int traversal) {
     v.n_planes = (uint32_t)s->planes.size();
     v.n_emitters = (uint32_t)s->emitters.size();
     v.bg = pt::mk3(s->hs.bg[0], s->hs.bg[1], s->hs.bg[2]);
+    v.box_extent = s->box_extent;
     return v;
 }
 
@@ -338,8 +343,12 @@ int pt_scene_prepare(pt_scene* s) {
             if (p.type == pt::T_BOX || p.type == pt::T_ELLIPSOID) s->emitters.push_back(i);
         }
         build_device_layout(s);
+        s->box_extent = 0.f;
+        for (const auto& n : s->nodes)
+            for (int a = 0; a < 3; ++a) s->box_extent = std::max({s->box_extent, fabsf(n.mn[a]), fabsf(n.mx[a])});
+        if (!std::isfinite(s->box_extent)) s->box_extent = INFINITY;   // certification then never succeeds
         pth::build_aux_bvh(s->nodes, s->aux, s->aux_depth);
-        pth::build_aux_stackless(s->aux, s->dnodes, s->auxsl, s->auxsl_depth);
+        pth::build_aux_wide(s->aux, s->dnodes, PT_AUXW, s->auxsl, s->auxsl_depth, s->auxw_stack);
         pth::build_gamma_thresholds(s->thr);
     } catch (const std::exception& e) {
         return fail(PT_E_SCENE, e.what());
@@ -362,8 +371,8 @@ int pt_scene_get_info(const pt_scene* s, pt_scene_info* info) {
     info->n_nodes = (uint32_t)s->nodes.size();
     info->tree_depth = s->tree_depth;
     info->max_stack = s->max_stack;
-    info->n_aux_nodes = (uint32_t)s->aux.size();
-    info->aux_depth = s->aux_depth;
+    info->n_aux_nodes = (uint32_t)(s->auxsl.size() / PT_AUXW);   // wide auxiliary BVH (wavefront query)
+    info->aux_depth = s->auxsl_depth;
     info->n_warnings = (uint32_t)s->hs.warnings.size();
     return PT_OK;
 }
@@ -502,6 +511,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.S.n_planes = (uint32_t)s->planes.size();
     wp.S.n_emitters = (uint32_t)s->emitters.size();
     wp.S.bg = pt::mk3(s->hs.bg[0], s->hs.bg[1], s->hs.bg[2]);
+    wp.S.box_extent = s->box_extent;
     wp.aux = ds.auxsl;
     wp.n_aux = (uint32_t)s->auxsl.size();
     wp.cam = ss->cam;
@@ -522,6 +532,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.depth = ss->depth;
     wp.n_tiles_local = ss->n_tiles_local;
     wp.max_stack = std::max<uint32_t>(s->max_stack, 1u);
+    wp.aux_stack = std::max<uint32_t>(s->auxw_stack, 1u);
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
@@ -552,6 +563,7 @@ int pt_session_trace(pt_session* ss, uint32_t spp) {
     tp.S.n_planes = (uint32_t)s->planes.size();
     tp.S.n_emitters = (uint32_t)s->emitters.size();
     tp.S.bg = pt::mk3(s->hs.bg[0], s->hs.bg[1], s->hs.bg[2]);
+    tp.S.box_extent = s->box_extent;
     tp.cam = ss->cam;
     tp.tm = ss->tm;
     tp.st = ss->st;
@@ -882,8 +894,12 @@ int pt_selftest_render_host(pt_scene* s, int32_t traversal, uint32_t x0, uint32_
     const uint32_t nt = std::max(1u, std::thread::hardware_concurrency());
     std::vector<std::thread> th;
     std::vector<uint32_t> errs(nt, 0);
+    // diagnostics: PT_QSTATS=<file> dumps per-query {aux visits, node tests, prim tests, exact} (u32 x4)
+    const char* qpath = getenv("PT_QSTATS");
+    std::vector<std::vector<std::array<uint32_t, 4>>> qlogs(nt);
     for (uint32_t t = 0; t < nt; ++t) {
         th.emplace_back([&, t]() {
+            std::vector<std::array<uint32_t, 4>>* qlog = qpath ? &qlogs[t] : nullptr;
             HostStack stk;
             HostVStore vs;
             pt::Counts C{};
@@ -902,6 +918,11 @@ int pt_selftest_render_host(pt_scene* s, int32_t traversal, uint32_t x0, uint32_
                             uint32_t ex = 0;
                             const int id = pt::q_run(V, s->auxsl.data(), (uint32_t)s->auxsl.size(), rr, stk, hh, Q, ex);
                             cc.fallbacks += ex;
+#ifdef PT_QDIAG
+                            if (qlog) qlog->push_back({Q.aux, Q.nodes, Q.ptests | (ex << 31), Q.cands | (Q.passes << 16)});
+#else
+                            if (qlog) qlog->push_back({Q.aux, Q.nodes, Q.ptests | (ex << 31), 0u});
+#endif
                             return id;
                         };
                         sum = sum + pt::trace_path_with(V, q, ray, s->hs.depth, R, vs, C);
@@ -916,6 +937,11 @@ int pt_selftest_render_host(pt_scene* s, int32_t traversal, uint32_t x0, uint32_
         });
     }
     for (auto& x : th) x.join();
+    if (qpath)
+        if (FILE* f = fopen(qpath, "wb")) {
+            for (auto& v : qlogs) fwrite(v.data(), 16, v.size(), f);
+            fclose(f);
+        }
     for (uint32_t e : errs)
         if (e) return fail(PT_E_INVALID, "hit list overflow");
     return PT_OK;

@@ -245,3 +245,81 @@ void build_aux_stackless(const std::vector<pt::AuxNode>& pairs, const std::vecto
 }
 
 }  // namespace pth
+
+namespace pth {
+
+// Wide (W-ary) form of the auxiliary BVH for the wavefront query: the binary
+// pair tree collapsed greedily (the child with the largest box area is
+// replaced by its two children until W children or only leaves remain).
+// Node n = entries [n*W, n*W + W) in the AuxSL layout; entry code:
+// internal child node index, 0x80000000 | reference leaf (box = the leaf's
+// exact center/half-size record), or 0xffffffff (empty).
+void build_aux_wide(const std::vector<pt::AuxNode>& pairs, const std::vector<pt::Node>& dnodes, uint32_t W,
+                    std::vector<pt::AuxSL>& out, uint32_t& max_depth, uint32_t& max_stack) {
+    struct Ch { uint32_t code; float lo[3], hi[3]; };
+    auto child = [&](const pt::AuxNode& n, int k) {
+        Ch c;
+        const float* f = reinterpret_cast<const float*>(&n) + 6 * k;
+        for (int a = 0; a < 3; ++a) { c.lo[a] = f[a]; c.hi[a] = f[3 + a]; }
+        c.code = reinterpret_cast<const uint32_t*>(&n)[12 + k];
+        return c;
+    };
+    auto area = [](const Ch& c) {
+        const float dx = c.hi[0] - c.lo[0], dy = c.hi[1] - c.lo[1], dz = c.hi[2] - c.lo[2];
+        return dx * dy + dx * dz + dy * dz;
+    };
+    out.clear();
+    max_depth = 0;
+    // BFS over wide nodes: (pair-tree internal code, wide node index, depth)
+    std::vector<std::pair<uint32_t, uint32_t>> todo;  // pair node code -> wide node index
+    std::vector<uint32_t> depth_of;
+    out.resize(W);
+    depth_of.push_back(1);
+    todo.emplace_back(0u, 0u);
+    for (size_t qi = 0; qi < todo.size(); ++qi) {
+        const uint32_t pc = todo[qi].first, wn = todo[qi].second;
+        std::vector<Ch> ch;
+        ch.push_back(child(pairs[pc], 0));
+        const Ch c1 = child(pairs[pc], 1);
+        if (c1.code != 0xFFFFFFFFu) ch.push_back(c1);
+        for (;;) {
+            if (ch.size() >= W) break;
+            int best = -1;
+            float ba = -1.f;
+            for (int k = 0; k < (int)ch.size(); ++k)
+                if (!(ch[k].code & 0x80000000u) && area(ch[k]) > ba) { ba = area(ch[k]); best = k; }
+            if (best < 0) break;
+            const pt::AuxNode& p = pairs[ch[best].code];
+            const Ch a = child(p, 0), b = child(p, 1);
+            ch[best] = a;
+            if (b.code != 0xFFFFFFFFu) ch.push_back(b);
+        }
+        max_depth = std::max(max_depth, depth_of[wn]);
+        for (uint32_t k = 0; k < W; ++k) {
+            pt::AuxSL e;
+            memset(&e, 0, sizeof(e));
+            uint32_t* u = reinterpret_cast<uint32_t*>(&e);
+            float* f = reinterpret_cast<float*>(&e);
+            if (k >= ch.size()) {
+                u[7] = 0xFFFFFFFFu;
+            } else if (ch[k].code & 0x80000000u) {
+                const pt::Node& r = dnodes[ch[k].code & 0x7fffffffu];
+                f[0] = r.a.x; f[1] = r.a.y; f[2] = r.a.z; f[3] = r.a.w; f[4] = r.b.x; f[5] = r.b.y;
+                u[7] = ch[k].code;
+            } else {
+                f[0] = ch[k].lo[0]; f[1] = ch[k].lo[1]; f[2] = ch[k].lo[2];
+                f[3] = ch[k].hi[0]; f[4] = ch[k].hi[1]; f[5] = ch[k].hi[2];
+                const uint32_t nn = (uint32_t)(out.size() / W);
+                out.resize(out.size() + W);
+                depth_of.push_back(depth_of[wn] + 1);
+                todo.emplace_back(ch[k].code, nn);
+                u[7] = nn;
+            }
+            out[(size_t)wn * W + k] = e;
+        }
+    }
+    // stack bound: a visit pushes at most W-1 entries beyond the one it continues with
+    max_stack = (W - 1) * max_depth + 1;
+}
+
+}  // namespace pth

@@ -53,6 +53,10 @@ void build_aux_bvh(const std::vector<HNode>& nodes, std::vector<pt::AuxNode>& ou
 void build_aux_stackless(const std::vector<pt::AuxNode>& pairs, const std::vector<pt::Node>& dnodes,
                          std::vector<pt::AuxSL>& out, uint32_t& max_depth);
 
+// W-ary form of the auxiliary BVH (aux_bvh.cpp)
+void build_aux_wide(const std::vector<pt::AuxNode>& pairs, const std::vector<pt::Node>& dnodes, uint32_t W,
+                    std::vector<pt::AuxSL>& out, uint32_t& max_depth, uint32_t& max_stack);
+
 // Gamma/quantise threshold table (tonemap.cpp)
 void build_gamma_thresholds(float thr[256]);
 

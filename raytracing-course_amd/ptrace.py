@@ -144,7 +144,7 @@ class Scene:
         return cls(h)
 
     def close(self):
-        if self._h:
+        if getattr(self, "_h", None) and _lib is not None:
             _lib.pt_scene_free(self._h)
             self._h = None
 
@@ -256,7 +256,7 @@ class Session:
         return _lib.pt_session_stream(self._h)
 
     def close(self):
-        if getattr(self, "_h", None):
+        if getattr(self, "_h", None) and _lib is not None:
             _lib.pt_session_free(self._h)
             self._h = None
 
