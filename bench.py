@@ -249,6 +249,7 @@ def main():
             "node_visits_per_ray": float(tsum[2]) / max(total_rays, 1),
             "aux_visits_per_ray": float(tsum[6]) / max(total_rays, 1),
             "fallback_rate": float(tsum[7]) / max(total_rays, 1),
+            "fallbacks": int(tsum[7]),
             "exactness_errors": int(tsum[5]),
             "wall": {"load_s": t_prep - t_load, "prepare_bvh_s": t_sess - t_prep, "session_upload_s": t_ready - t_sess},
             "framebuffer_gathered": img is not None and img.shape == (H, W, 3),

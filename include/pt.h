@@ -111,6 +111,7 @@ typedef struct pt_stats {
     uint64_t node_bytes;     /* bytes of one node record / primitive record / aux node */
     uint64_t prim_bytes;
     uint64_t aux_bytes;
+    uint64_t fallbacks_ray;  /* of `fallbacks`: rays with non-finite origin/direction (exact DFS by design) */
 } pt_stats;
 
 /* Scene::Render minus the stream write: renders W*H*3 u8 (row-major, top row

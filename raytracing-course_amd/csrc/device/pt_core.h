@@ -198,6 +198,8 @@ struct SceneView {
     uint32_t n_planes, n_emitters;
     f3 bg;
     float box_extent;           // max |coordinate| over the reference node boxes (replay certification)
+    const uint32_t* anc_info;   // per reference node: offset | length << 26 of its ancestor list (leaves)
+    const uint32_t* anc;        // ancestor lists: root .. parent, ascending preorder indices
 };
 
 struct Ray { f3 o, d; };
@@ -302,6 +304,29 @@ PT_HD bool prim_intersect(const Prim& P, const Ray& ray, Hit& h) {
         ok = isect_triangle(lr, a, mk3(P.p3.x, P.p3.y, P.p3.z), mk3(P.p3.w, P.p4.x, P.p4.y), h);
     } else if (type == T_PLANE) {
         ok = isect_plane(lr, a, h);
+    } else if (type == T_BOX) {
+        ok = isect_box(lr, a, h);
+    } else {
+        ok = isect_ellipsoid(lr, a, h);
+    }
+    if (ok) h.n = normalize(qrot(q, h.n));
+    return ok;
+}
+
+// prim_intersect for BVH primitives (std::partition keeps planes out of the
+// BVH, src/scene.cpp:16-21): same operations without the plane branch
+PT_HD bool bvh_prim_intersect(const Prim& P, const Ray& ray, Hit& h) {
+    const f3 pos = mk3(P.p0.x, P.p0.y, P.p0.z);
+    const uint32_t type = f2u(P.p0.w);
+    q4 q; q.x = P.p1.x; q.y = P.p1.y; q.z = P.p1.z; q.w = P.p1.w;
+    const q4 cq = conj(q);
+    Ray lr;
+    lr.o = qrot(cq, ray.o + -1.f * pos);
+    lr.d = qrot(cq, ray.d);
+    const f3 a = mk3(P.p2.x, P.p2.y, P.p2.z);
+    bool ok;
+    if (type == T_TRIANGLE) {
+        ok = isect_triangle(lr, a, mk3(P.p3.x, P.p3.y, P.p3.z), mk3(P.p3.w, P.p4.x, P.p4.y), h);
     } else if (type == T_BOX) {
         ok = isect_box(lr, a, h);
     } else {

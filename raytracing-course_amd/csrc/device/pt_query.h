@@ -58,7 +58,12 @@ struct Query {
     uint32_t cand, skip, last;
     float bound;
     float dl;                   // certification margin (t units, see q_leaf_certain)
-    uint32_t walk;              // Q_REPLAY: 0 = candidate leaf check, 1 = walking its root path
+    uint32_t walk;              // Q_REPLAY: 0 = candidate leaf check, else 1 + position in its ancestor list
+    uint32_t known;             // walk: the segment bound is known (below the LCA with the last hit)
+    uint32_t astar;             // walk: deepest ancestor at or above that LCA seen so far
+    uint32_t robust;            // leaf check: the ray crosses the leaf box robustly (t1c, mc valid)
+    float t1c, mc;              // leaf check: approximate entry and certification margin
+    uint32_t par;               // near-zero direction component: exact node tests, robust aux boxes
     uint32_t overflow;
     uint32_t c[PT_QK];          // sorted candidates of this pass (0xffffffff = empty)
     uint32_t nh;
@@ -71,7 +76,7 @@ struct Query {
 struct QCounts {
     uint32_t nodes, aux, ptests, planes;
 #ifdef PT_QDIAG
-    uint32_t cands, passes;
+    uint32_t cands, passes, steps;
 #endif
 };
 
@@ -96,12 +101,19 @@ PT_HD void q_init(const SceneView& S, const Ray& ray, Query& q, QCounts& C) {
     q.sp = 0;
 #pragma unroll
     for (int i = 0; i < PT_QK; ++i) q.c[i] = 0xffffffffu;
-    if (!replay_ok_ray(ray)) { q.phase = Q_EXACT; return; }
+    // non-finite rays: exact stack DFS (their NaN/inf slab semantics are not replayed)
+    const float big = 3e38f;
+    if (!(fabsf(ray.o.x) < big && fabsf(ray.o.y) < big && fabsf(ray.o.z) < big && fabsf(ray.d.x) < big &&
+          fabsf(ray.d.y) < big && fabsf(ray.d.z) < big)) {
+        q.phase = Q_EXACT;
+        return;
+    }
+    q.par = replay_ok_ray(ray) ? 0u : 1u;
     q.inv = mk3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
     q.oinv = mk3(ray.o.x * q.inv.x, ray.o.y * q.inv.y, ray.o.z * q.inv.z);
     const float om = fmaxf(fmaxf(fabsf(ray.o.x), fabsf(ray.o.y)), fabsf(ray.o.z));
     const float dm = fminf(fminf(fabsf(ray.d.x), fabsf(ray.d.y)), fabsf(ray.d.z));
-    q.dl = 0x1p-18f * (S.box_extent + om) / dm;
+    q.dl = q.par ? INFINITY : 0x1p-18f * (S.box_extent + om) / dm;
     q.phase = Q_AUX;
 }
 
@@ -149,17 +161,18 @@ PT_HD void q_next_candidate(Query& q) {
 }
 
 // leaf reached: first-min over its primitives (src/bvh.cpp:205-213), hit bookkeeping
-PT_HD void q_leaf_hit(const SceneView& S, Query& q, uint32_t a, uint32_t ref, uint32_t cnt, QCounts& C) {
+// returns false when the replay hit list is full (the ray then takes the exact DFS)
+PT_HD bool q_leaf_hit(const SceneView& S, Query& q, uint32_t a, uint32_t ref, uint32_t cnt, QCounts& C) {
     Hit lbh;
     lbh.t = PT_INF;
     int lid = -1;
     for (uint32_t i = ref; i < ref + cnt; ++i) {
         Hit h;
         C.ptests++;
-        if (prim_intersect(S.prims[i], q.ray, h) && h.t < lbh.t) { lbh = h; lid = (int)i; }
+        if (bvh_prim_intersect(S.prims[i], q.ray, h) && h.t < lbh.t) { lbh = h; lid = (int)i; }
     }
     if (lid >= 0) {
-        if (q.nh == PT_REPLAY_HITS) { q.phase = Q_EXACT; return; }
+        if (q.nh == PT_REPLAY_HITS) return false;
 #pragma unroll
         for (int k = 0; k < PT_REPLAY_HITS; ++k)
             if ((uint32_t)k == q.nh) { q.H.idx[k] = a; q.H.t[k] = lbh.t; }
@@ -170,8 +183,22 @@ PT_HD void q_leaf_hit(const SceneView& S, Query& q, uint32_t a, uint32_t ref, ui
             if (lbh.t < q.P) { q.res = lbh; q.res_id = lid; }
         }
     }
-    q.skip = a + 1u;
-    q_next_candidate(q);
+    return true;
+}
+
+// min of the recorded hits strictly inside (a, r) (the left subtree of a when
+// r is a's right child); at least one exists when called with a = a*
+PT_HD float q_bound_between(const Query& q, uint32_t a, uint32_t r) {
+    float m = q.P;
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < PT_REPLAY_HITS; ++k) {
+        if ((uint32_t)k < q.nh && q.H.idx[k] > a && q.H.idx[k] < r) {
+            if (!any || q.H.t[k] < m) m = q.H.t[k];
+            any = true;
+        }
+    }
+    return m;
 }
 
 // Candidate leaf check before any root-path replay.  Every bound the replay
@@ -190,7 +217,7 @@ PT_HD void q_leaf_hit(const SceneView& S, Query& q, uint32_t a, uint32_t ref, ui
 //  * certain reject: the leaf's own exact test fails even against hi (its
 //    actual bound is <= hi): it is not entered whatever its ancestors do.
 // Returns 1 = accept, 0 = reject, 2 = undecided (replay the root path).
-PT_HD uint32_t q_leaf_certain(const Query& q, const Node& nd) {
+PT_HD uint32_t q_leaf_certain(Query& q, const Node& nd) {
     float lo = q.P, hi = q.P;
 #pragma unroll
     for (int k = 0; k < PT_REPLAY_HITS; ++k)
@@ -205,8 +232,11 @@ PT_HD uint32_t q_leaf_certain(const Query& q, const Node& nd) {
     const float t1 = smax(smax(smin(ax, bx), smin(ay, by)), smin(az, bz));
     const float t2 = smin(smin(smax(ax, bx), smax(ay, by)), smax(az, bz));
     const float m = q.dl + (fabsf(t1) + fabsf(t2)) * 0x1p-18f;
-    if (t1 + m <= t2 - m && t2 - m >= 0.f && lo >= t1 + m) return 1u;
-    if (!node_enter(nd, q.ray, q.inv, hi)) return 0u;
+    q.t1c = t1;
+    q.mc = m;
+    q.robust = (!q.par && t1 + m <= t2 - m && t2 - m >= 0.f) ? 1u : 0u;
+    if (q.robust && lo >= t1 + m) return 1u;
+    if (!node_enter(nd, q.ray, q.inv, hi, q.par != 0u)) return 0u;
     return 2u;
 }
 
@@ -214,6 +244,9 @@ PT_HD uint32_t q_leaf_certain(const Query& q, const Node& nd) {
 // `stk` = per-lane word memory for the pending aux nodes (set/get).
 template <class Mem>
 PT_HD void q_step(const SceneView& S, const AuxSL* aux, uint32_t n_aux, Query& q, QCounts& C, Mem& stk) {
+#ifdef PT_QDIAG
+    C.steps++;
+#endif
     if (q.phase == Q_AUX) {
         // one wide node: PT_AUXW child entries (independent loads)
         AuxSL e[PT_AUXW];
@@ -231,13 +264,15 @@ PT_HD void q_step(const SceneView& S, const AuxSL* aux, uint32_t n_aux, Query& q
                 Node nd;
                 nd.a = e[k].a;
                 nd.b = e[k].b;
-                if (node_enter(nd, q.ray, q.inv, PT_INF)) {
+                if (node_enter(nd, q.ray, q.inv, PT_INF, q.par != 0u)) {
 #ifdef PT_QDIAG
                     C.cands++;
 #endif
                     q_insert(q, leaf);
                 }
-            } else if (aux_box(e[k].a.x, e[k].a.y, e[k].a.z, e[k].a.w, e[k].b.x, e[k].b.y, q.inv, q.oinv)) {
+            } else if (q.par ? aux_box_par(e[k].a.x, e[k].a.y, e[k].a.z, e[k].a.w, e[k].b.x, e[k].b.y, q.ray, q.inv,
+                                           q.oinv)
+                             : aux_box(e[k].a.x, e[k].a.y, e[k].a.z, e[k].a.w, e[k].b.x, e[k].b.y, q.inv, q.oinv)) {
                 if (next == 0xffffffffu) next = code;
                 else stk.set(q.sp++, code);
             }
@@ -255,53 +290,68 @@ PT_HD void q_step(const SceneView& S, const AuxSL* aux, uint32_t n_aux, Query& q
         q_next_candidate(q);
         return;
     }
+    uint32_t verdict;   // 0 reject, 1 accept, 2 undecided
     if (!q.walk) {
         // Q_REPLAY, first visit of a candidate: its own leaf record
         const Node nd = S.nodes[q.cand];
         C.nodes++;
-        const uint32_t v = q_leaf_certain(q, nd);
-        if (v == 1u) {
-            q_leaf_hit(S, q, q.cand, f2u(nd.b.z), f2u(nd.b.w), C);
-        } else if (v == 0u) {
-            q.skip = q.cand + 1u;
-            q_next_candidate(q);
-        } else {
+        verdict = q_leaf_certain(q, nd);
+        if (verdict == 2u) {
             q.walk = 1u;
-            q.node = 0u;
+            q.known = q.nh == 0u ? 1u : 0u;   // no earlier hit: the bound is P on the whole path
             q.bound = q.P;
+            q.astar = 0u;
+            return;
         }
-        return;
-    }
-    // Q_REPLAY, undecided candidate: one node of the root -> cand path
-    const Node nd = S.nodes[q.node];
-    C.nodes++;
-    const uint32_t a = q.node;
-    const uint32_t ref = f2u(nd.b.z), info = f2u(nd.b.w);
-    if (!node_enter(nd, q.ray, q.inv, q.bound)) {
-        q.skip = (info & PT_NODE_INTERIOR) ? (info & 0x7fffffffu) : a + 1u;
-        q_next_candidate(q);
-        return;
-    }
-    if (a == q.cand) {
-        q_leaf_hit(S, q, a, ref, info, C);
-        return;
-    }
-    if (q.cand < ref) {
-        q.node = a + 1u;                 // left child: same bound
     } else {
-        // right child: bound = best hit of the left sibling's subtree, if any
-        float m = q.bound;
-        bool any = false;
+        // Q_REPLAY, undecided candidate: its ancestor list, 4 entries per step.
+        // Ancestors at or above a* = LCA(last recorded hit h, cand) were entered on
+        // h's path (same node, same bound: both depend only on earlier hits) -- they
+        // are the list entries <= h.  Below a* no left subtree holds a hit, so the
+        // bound is constant: B = min{hits in (a*, right child of a*)}.  Each
+        // remaining ancestor, then the leaf itself, is tested with B.
+        const uint32_t info = S.anc_info[q.cand];
+        const uint32_t off = info & 0x03ffffffu, len = info >> 26;
+        const uint32_t pos = q.walk - 1u;
+        uint32_t hlast = 0u;   // last recorded hit (unrolled select: no dynamic register indexing)
 #pragma unroll
-        for (int k = 0; k < PT_REPLAY_HITS; ++k) {
-            if ((uint32_t)k < q.nh && q.H.idx[k] > a && q.H.idx[k] < ref) {
-                if (!any || q.H.t[k] < m) m = q.H.t[k];
-                any = true;
+        for (int k = 0; k < PT_REPLAY_HITS; ++k)
+            if ((uint32_t)k + 1u == q.nh) hlast = q.H.idx[k];
+        verdict = 2u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t at = pos + (uint32_t)j;
+            if (verdict != 2u || at >= len) continue;
+            const uint32_t e = S.anc[off + at];
+            if (!q.known) {
+                if (e <= hlast) { q.astar = e; continue; }
+                q.bound = q_bound_between(q, q.astar, e);
+                q.known = 1u;
+                if (q.robust && q.bound >= q.t1c + q.mc) { verdict = 1u; continue; }   // whole segment certain
             }
+            C.nodes++;
+            if (!node_enter(S.nodes[e], q.ray, q.inv, q.bound, q.par != 0u)) verdict = 0u;
         }
-        q.bound = m;
-        q.node = ref;
+        if (verdict == 2u) {
+            if (pos + 4u < len) {
+                q.walk += 4u;
+                return;
+            }
+            // every ancestor entered: the leaf itself, with its bound
+            if (!q.known) q.bound = q_bound_between(q, q.astar, q.cand);
+            if (q.robust && q.bound >= q.t1c + q.mc) verdict = 1u;
+            else verdict = node_enter(S.nodes[q.cand], q.ray, q.inv, q.bound, q.par != 0u) ? 1u : 0u;
+        }
     }
+    if (verdict == 1u) {
+        const Node nd = S.nodes[q.cand];
+        if (!q_leaf_hit(S, q, q.cand, f2u(nd.b.z), f2u(nd.b.w), C)) {
+            q.phase = Q_EXACT;
+            return;
+        }
+    }
+    q.skip = q.cand + 1u;
+    q_next_candidate(q);
 }
 
 // exact stack DFS for the rays the replay leaves (planes again + bvh_exact:

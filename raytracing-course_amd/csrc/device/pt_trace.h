@@ -176,7 +176,8 @@ PT_HD bool node_slab(const Node& nd, const Ray& ray, float& t, uint32_t& interio
 // operands are closer than that margin is re-done with the exact division
 // (slab()).  Requires replay_ok_ray(ray) (finite, non-tiny d: |rinv| < 1e30).
 // Returns true iff the node is entered (hit and not pruned).
-PT_HD bool node_enter(const Node& nd, const Ray& ray, f3 rinv, float bound) {
+// exact = true: always the IEEE-division form (rays with near-zero direction components).
+PT_HD bool node_enter(const Node& nd, const Ray& ray, f3 rinv, float bound, bool exact = false) {
     const f3 c = mk3(nd.a.x, nd.a.y, nd.a.z);
     const f3 s = mk3(nd.a.w, nd.b.x, nd.b.y);
     const f3 o = ray.o + -1.f * c;                 // src/bvh.cpp:92 (same IEEE adds)
@@ -190,7 +191,7 @@ PT_HD bool node_enter(const Node& nd, const Ray& ray, f3 rinv, float bound) {
     const float m12 = 2.f * (e1 + e2);
     const float d12 = t1 - t2;
     // certain outcomes (every comparison separated by more than its error margin)
-    bool amb = !(e1 < 1e20f && e2 < 1e20f) || !(fabsf(d12) > m12);
+    bool amb = exact || !(e1 < 1e20f && e2 < 1e20f) || !(fabsf(d12) > m12);
     bool enter = false;
     if (!amb) {
         if (d12 > 0.f) return false;                            // t1 > t2: miss
@@ -211,6 +212,30 @@ PT_HD bool node_enter(const Node& nd, const Ray& ray, f3 rinv, float bound) {
         return !(bound < t && !in);
     }
     return enter;
+}
+
+// conservative inflated-box test for rays with near-zero direction components
+// (|d_k| <= 1e-30): such an axis bounds no t, the origin must lie in the slab;
+// other axes as aux_box.  Covers every box the exact (inf/NaN) slab test can
+// enter: with o_k outside the slab by more than the inflation margin the exact
+// quotients are both huge of one sign (t beyond any bound, or exit < 0).
+PT_HD bool aux_box_par(float lx, float ly, float lz, float hx, float hy, float hz, const Ray& r, f3 inv, f3 oinv) {
+    const float lo[3] = {lx, ly, lz}, hi[3] = {hx, hy, hz};
+    const float o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
+    const float iv[3] = {inv.x, inv.y, inv.z}, oi[3] = {oinv.x, oinv.y, oinv.z};
+    float tn = -INFINITY, tf = INFINITY;
+    bool inside = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (!(fabsf(d[k]) > 1e-30f)) {
+            inside = inside && lo[k] <= o[k] && o[k] <= hi[k];
+        } else {
+            const float a = fmaf(lo[k], iv[k], -oi[k]), b = fmaf(hi[k], iv[k], -oi[k]);
+            tn = fmaxf(tn, fminf(a, b));
+            tf = fminf(tf, fmaxf(a, b));
+        }
+    }
+    return inside && tn <= tf && tf >= 0.f;
 }
 
 PT_HD bool replay_ok_ray(const Ray& r) {

@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
     uint32_t qi = 0u;
     Query q;
     QCounts C{0u, 0u, 0u, 0u};
-    uint32_t rays = 0u, fallbacks = 0u;
+    uint32_t rays = 0u, fallbacks = 0u, init_exact = 0u;
     for (;;) {
         const unsigned long long idle = __ballot(!active);
         uint32_t nidle = (uint32_t)__popcll(idle);
@@ -112,6 +112,7 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
                 ray.d = mk3(d.x, d.y, d.z);
                 rays++;
                 q_init(P.S, ray, q, C);
+                if (q.phase == Q_EXACT) init_exact++;
                 active = true;
             }
         }
@@ -135,6 +136,7 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
     wave_add_u64(P.counters + 3, C.planes);
     wave_add_u64(P.counters + 5, C.aux);
     wave_add_u64(P.counters + 6, fallbacks);
+    wave_add_u64(P.counters + 7, init_exact);
 }
 
 // exact stack DFS for the handed-back rays; 64-lane workgroups, stack in LDS

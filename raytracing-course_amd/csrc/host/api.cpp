@@ -51,6 +51,8 @@ struct DevScene {
     float* thr = nullptr;
     pt::AuxNode* aux = nullptr;
     pt::AuxSL* auxsl = nullptr;
+    uint32_t* anc_info = nullptr;
+    uint32_t* anc = nullptr;
 };
 
 constexpr uint32_t kCandCap = 24;   // candidate-list words per lane (per replay pass)
@@ -70,6 +72,7 @@ struct pt_scene {
     std::vector<pt::AuxSL> auxsl;
     uint32_t tree_depth = 0, max_stack = 0, aux_depth = 0, auxsl_depth = 0;
     float box_extent = 0.f;     // max |coordinate| of the reference node boxes
+    std::vector<uint32_t> anc_info, anc;   // per-leaf ancestor lists (replay walk)
     uint32_t auxw_stack = 0;    // per-lane stack words of the wide aux traversal
     float thr[256];
     std::map<int, DevScene> dev;
@@ -161,6 +164,23 @@ void build_device_layout(pt_scene* s) {
     }
     s->tree_depth = maxdep + 1;
     s->max_stack = need.empty() ? 0 : need[0];
+    // ancestor lists of the leaves (root .. parent), for the replay walk (pt_query.h)
+    std::vector<uint32_t> parent(s->nodes.size(), 0xFFFFFFFFu);
+    for (size_t i = 0; i < s->nodes.size(); ++i)
+        if (s->nodes[i].left != 0xFFFFFFFFu) { parent[s->nodes[i].left] = (uint32_t)i; parent[s->nodes[i].right] = (uint32_t)i; }
+    s->anc_info.assign(s->nodes.size(), 0u);
+    s->anc.clear();
+    std::vector<uint32_t> path;
+    for (size_t i = 0; i < s->nodes.size(); ++i) {
+        if (s->nodes[i].left != 0xFFFFFFFFu) continue;
+        path.clear();
+        for (uint32_t a = parent[i]; a != 0xFFFFFFFFu; a = parent[a]) path.push_back(a);
+        if (path.size() > 63 || s->anc.size() + path.size() >= (1u << 26))
+            throw std::runtime_error("BVH too deep for the ancestor lists");
+        s->anc_info[i] = (uint32_t)s->anc.size() | ((uint32_t)path.size() << 26);
+        s->anc.insert(s->anc.end(), path.rbegin(), path.rend());
+    }
+    if (s->anc.empty()) s->anc.push_back(0u);
     if (s->nodes.size() >= (1u << 24)) throw std::runtime_error("BVH larger than 2^24 nodes");
 }
 
@@ -198,6 +218,7 @@ int ensure_device_scene(pt_scene* s, int dev, DevScene** out) {
     if ((rc = upload(&d.thr, thr))) return rc;
     if ((rc = upload(&d.aux, s->aux))) return rc;
     if ((rc = upload(&d.auxsl, s->auxsl))) return rc;
+    if ((rc = upload(&d.anc_info, s->anc_info)) || (rc = upload(&d.anc, s->anc))) return rc;
     s->dev[dev] = d;
     *out = &s->dev[dev];
     return PT_OK;
@@ -206,7 +227,7 @@ int ensure_device_scene(pt_scene* s, int dev, DevScene** out) {
 void free_device_scene(DevScene& d) {
     (void)hipFree(d.nodes); (void)hipFree(d.prims); (void)hipFree(d.shade);
     (void)hipFree(d.planes); (void)hipFree(d.emitters); (void)hipFree(d.thr); (void)hipFree(d.aux);
-    (void)hipFree(d.auxsl);
+    (void)hipFree(d.auxsl); (void)hipFree(d.anc_info); (void)hipFree(d.anc);
 }
 
 // per-lane LDS words: replay needs [aux stack | candidates], the exact DFS its stack
@@ -234,6 +255,8 @@ pt::SceneView host_view(const pt_scene* s, int traversal) {
     v.n_emitters = (uint32_t)s->emitters.size();
     v.bg = pt::mk3(s->hs.bg[0], s->hs.bg[1], s->hs.bg[2]);
     v.box_extent = s->box_extent;
+    v.anc_info = s->anc_info.data();
+    v.anc = s->anc.data();
     return v;
 }
 
@@ -472,8 +495,8 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
             return cleanup(fail(PT_E_OOM, "device allocation failed (wavefront buffers)"));
         hipDeviceProp_t pr;
         if (hipGetDeviceProperties(&pr, ss->dev) != hipSuccess) return cleanup(fail(PT_E_HIP, "device query failed"));
-        // persistent intersection grid: 8 workgroups (32 waves) per CU, capped by the work
-        ss->isect_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * 8u;
+        // persistent intersection grid: 4 workgroups (16 waves) per CU, capped by the work
+        ss->isect_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * 4u;
         if (const char* g = getenv("PT_ISECT_WG_PER_CU")) ss->isect_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * (uint32_t)std::max(1, atoi(g));
         ss->isect_grid = std::min(ss->isect_grid, std::max(1u, ss->n_tiles_local));
     }
@@ -512,6 +535,8 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.S.n_emitters = (uint32_t)s->emitters.size();
     wp.S.bg = pt::mk3(s->hs.bg[0], s->hs.bg[1], s->hs.bg[2]);
     wp.S.box_extent = s->box_extent;
+    wp.S.anc_info = ds.anc_info;
+    wp.S.anc = ds.anc;
     wp.aux = ds.auxsl;
     wp.n_aux = (uint32_t)s->auxsl.size();
     wp.cam = ss->cam;
@@ -564,6 +589,8 @@ int pt_session_trace(pt_session* ss, uint32_t spp) {
     tp.S.n_emitters = (uint32_t)s->emitters.size();
     tp.S.bg = pt::mk3(s->hs.bg[0], s->hs.bg[1], s->hs.bg[2]);
     tp.S.box_extent = s->box_extent;
+    tp.S.anc_info = ds.anc_info;
+    tp.S.anc = ds.anc;
     tp.cam = ss->cam;
     tp.tm = ss->tm;
     tp.st = ss->st;
@@ -662,6 +689,7 @@ int pt_session_stats(pt_session* ss, pt_stats* st) {
     st->errors = c[4];
     st->aux_visits = c[5];
     st->fallbacks = c[6];
+    st->fallbacks_ray = c[7];
     uint64_t px = 0;
     for (uint32_t t = 0; t < ss->n_tiles_local; ++t) {
         const uint32_t gt = t * ss->tm.world + ss->tm.rank;
@@ -804,7 +832,8 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
         if ((rc = pt_session_stats(x, &st))) return cleanup(rc);
         agg.rays += st.rays; agg.node_visits += st.node_visits; agg.prim_tests += st.prim_tests;
         agg.plane_tests += st.plane_tests; agg.samples += st.samples; agg.errors += st.errors;
-        agg.aux_visits += st.aux_visits; agg.fallbacks += st.fallbacks; agg.aux_bytes = st.aux_bytes;
+        agg.aux_visits += st.aux_visits; agg.fallbacks += st.fallbacks;
+        agg.fallbacks_ray += st.fallbacks_ray; agg.aux_bytes = st.aux_bytes;
         agg.kernel_ms = std::max(agg.kernel_ms, st.kernel_ms);
         agg.resolve_ms = std::max(agg.resolve_ms, st.resolve_ms);
         agg.node_bytes = st.node_bytes; agg.prim_bytes = st.prim_bytes;
@@ -914,12 +943,12 @@ int pt_selftest_render_host(pt_scene* s, int32_t traversal, uint32_t x0, uint32_
                     if (traversal == PT_TRAVERSAL_REPLAY) {
                         // the wavefront engine's query (pt_query.h state machine), run to completion
                         auto q = [&](const pt::Ray& rr, pt::Hit& hh, pt::Counts& cc) {
-                            pt::QCounts Q{0u, 0u, 0u, 0u};
+                            pt::QCounts Q{};
                             uint32_t ex = 0;
                             const int id = pt::q_run(V, s->auxsl.data(), (uint32_t)s->auxsl.size(), rr, stk, hh, Q, ex);
                             cc.fallbacks += ex;
 #ifdef PT_QDIAG
-                            if (qlog) qlog->push_back({Q.aux, Q.nodes, Q.ptests | (ex << 31), Q.cands | (Q.passes << 16)});
+                            if (qlog) qlog->push_back({Q.aux, Q.steps, Q.ptests | (ex << 31), Q.cands | (Q.passes << 16)});
 #else
                             if (qlog) qlog->push_back({Q.aux, Q.nodes, Q.ptests | (ex << 31), 0u});
 #endif
