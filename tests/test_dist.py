@@ -1,0 +1,92 @@
+"""Multi-rank path on CPU: world-size-2 gloo runs of bench.py's tile deal and
+framebuffer gather (the N>1 data path; on the GPU box the same code runs
+over RCCL).  Tiles are 16x16, tile t belongs to rank t % world
+(include/pt.h sessions, bench.py gather_tiles)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import _util as U
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _expected(W, H):
+    y, x = np.mgrid[0:H, 0:W]
+    img = np.stack([(x * 7 + y) % 251, (y * 3 + x // 16) % 253, (x ^ y) % 255], axis=-1)
+    return img.astype(np.uint8)
+
+
+def _packed_for_rank(img, rank, world):
+    """what a rank's session resolves into: its tiles in local order, 256 px each, row-major"""
+    H, W, _ = img.shape
+    tx, ty = (W + 15) // 16, (H + 15) // 16
+    out = []
+    for gt in range(rank, tx * ty, world):
+        t = np.zeros((16, 16, 3), np.uint8)
+        x0, y0 = (gt % tx) * 16, (gt // tx) * 16
+        blk = img[y0:y0 + 16, x0:x0 + 16]
+        t[:blk.shape[0], :blk.shape[1]] = blk
+        out.append(t.reshape(-1))
+    return np.concatenate(out) if out else np.zeros(0, np.uint8)
+
+
+def _worker(rank, world, port, W, H, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    img = _expected(W, H)
+    packed = torch.from_numpy(_packed_for_rank(img, rank, world))
+    got = bench.gather_tiles(dist, packed, rank, world, W, H, torch.device("cpu"))
+    # the max-over-ranks timing reduction bench.py uses
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        q.put((got.tobytes(), float(t[0])))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("W,H", [(64, 48), (50, 37), (16, 16), (7, 3)])
+def test_gloo_gather_two_ranks(W, H):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, W, H, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got, tmax = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert np.frombuffer(got, np.uint8).reshape(H, W, 3).tolist() == _expected(W, H).tolist()
+    assert tmax == 2.0
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_unpack_tiles_abi_matches_deal(world):
+    """pt_unpack_tiles (C ABI) inverts the round-robin tile deal for every rank"""
+    pt = U.ptrace()
+    W, H = 83, 45
+    img = _expected(W, H)
+    out = np.zeros_like(img)
+    for r in range(world):
+        pt.unpack_tiles(_packed_for_rank(img, r, world), W, H, r, world, out=out)
+    assert np.array_equal(out, img)
