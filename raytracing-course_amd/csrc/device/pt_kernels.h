@@ -47,16 +47,20 @@ struct TraceParams {
 };
 
 // ---- wavefront renderer (pt_wave.hip) ----------------------------------
-struct WaveQueue {                // rays of one bounce, compacted
+struct RayQ {                     // rays waiting for a closest-hit query
     F4* ro;                       // {o.xyz, u32 slot}
     F4* rd;                       // {d.xyz, -}
 };
-struct WaveHits {                 // closest hit per queue entry
-    F4* th;                       // {t, n.xyz}
-    uint32_t* id;                 // prim | interior << 31, 0xffffffff = miss
+struct DoneQ {                    // finished queries, input of the shade kernel
+    F4* ro;                       // {o.xyz, u32 slot}
+    F4* rd;                       // {d.xyz, -}
+    uint32_t* id;                 // closest prim (the shade kernel recomputes t, n, side from it), 0xffffffff = miss
 };
-// per-slot path end state (pstate = nv | end << 8)
+// per-slot path state (pstate = nv | end << 8)
 enum : uint32_t { PE_LIVE = 0u, PE_MISS = 1u, PE_CUT = 2u, PE_TERM = 3u };
+
+// round counters: set p = ctl + 8p
+enum : uint32_t { C_FRESH = 0u, C_CARRY = 1u, C_HEAD = 2u, C_DONE = 3u, C_EXACT = 4u };
 
 struct WaveParams {
     SceneView S;
@@ -67,16 +71,22 @@ struct WaveParams {
     PixelState st;
     uint32_t* vscratch;           // 3 * depth * n_slots fold records
     uint32_t* pstate;             // n_slots
-    WaveQueue q[2];               // ping-pong: bounce b reads q[b & 1], enqueues into q[(b + 1) & 1]
-    WaveHits hits;
-    uint32_t* fb;                 // queue indices left to the exact DFS (this bounce)
-    uint32_t* ctl;                // [0, D]: queue counts per bounce, [D+1, 2D+1]: fetch heads, [2D+2, 3D+2]: exact counts
-    unsigned long long* counters; // rays, nodes, prim tests, plane tests, errors, aux visits, fallbacks
+    uint32_t* nsamp;              // samples completed per slot (this session)
+    RayQ fq[2];                   // fresh rays: round with parity p reads fq[p], appends to fq[1-p]
+    uint32_t* cq[2];              // suspended queries (carry_words each): read cq[p], append to cq[1-p]
+    uint32_t carry_cap, carry_words;
+    DoneQ done;
+    RayQ ex;                      // rays handed to the exact DFS this round
+    uint32_t* ctl;                // 2 x 8 round counters
+    unsigned long long* counters; // rays, nodes, prim tests, plane tests, errors, aux visits, fallbacks, ray fallbacks
     uint32_t depth;
-    uint32_t bounce;
+    uint32_t parity;
+    uint32_t target;              // samples per pixel to reach in this pass
     uint32_t n_tiles_local;
     uint32_t max_stack;           // exact DFS stack words per lane
     uint32_t aux_stack;           // wide aux traversal stack words per lane (LDS)
+    uint32_t straggler_steps;     // steps a query may run after its wave ran out of work, before suspending
+    unsigned long long* wg_prof;  // optional (diagnostics): per isect workgroup {start, end, HW_ID, XCC_ID, steps}
 };
 
 struct ResolveParams {
@@ -92,6 +102,8 @@ struct ResolveParams {
 hipError_t pt_launch_init(const pt::InitParams& p, uint32_t n_tiles, hipStream_t s);
 // variant: bit 0 = filtered node tests + flat replay, bit 1 = XCD-banded tile order
 hipError_t pt_launch_trace(const pt::TraceParams& p, int variant, uint32_t lds_bytes, hipStream_t s);
-// one sample of every owned pixel through the wavefront pipeline (pt_wave.hip)
-hipError_t pt_launch_wave_sample(pt::WaveParams p, uint32_t isect_grid, hipStream_t s);
+// wavefront pipeline (pt_wave.hip): start a pass (first camera ray of every
+// owned pixel), then rounds of {closest-hit, exact, shade}
+hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s);
+hipError_t pt_launch_wave_round(pt::WaveParams p, uint32_t isect_grid, uint32_t shade_grid, hipStream_t s);
 hipError_t pt_launch_resolve(const pt::ResolveParams& p, uint32_t n_tiles, hipStream_t s);

@@ -41,6 +41,8 @@ struct AuxSL { F4 a, b; };
 #define PT_AUX_INTERNAL 0xffffffffu
 
 enum : uint32_t { Q_AUX = 0u, Q_REPLAY = 1u, Q_DONE = 2u, Q_EXACT = 3u };
+// replay step kinds: each issues one round of independent loads
+enum : uint32_t { R_CAND = 0u, R_LEAF = 1u, R_WALK_E = 2u, R_WALK_N = 3u };
 
 struct QHits {                  // replay hit list (reference leaf index, leaf first-min t)
     uint32_t idx[PT_REPLAY_HITS];
@@ -49,29 +51,36 @@ struct QHits {                  // replay hit list (reference leaf index, leaf f
 
 struct Query {
     Ray ray;
-    f3 inv, oinv;
+    f3 inv;                     // 1/d (IEEE, once per ray)
     float P;                    // closest plane t (the BVH bound at the root)
-    uint32_t phase;
-    uint32_t node;              // Q_AUX: aux node; Q_REPLAY: reference node on the current path
-    uint32_t sp;                // Q_AUX: pending aux nodes on the per-lane stack
+    // small state packed into one register
+    uint32_t phase : 2;         // Q_*
+    uint32_t walk : 2;          // Q_REPLAY step kind: R_CAND, R_LEAF, R_WALK_E, R_WALK_N
+    uint32_t par : 1;           // near-zero direction component: exact node tests, robust aux boxes
+    uint32_t robust : 1;        // leaf check: the ray crosses the leaf box robustly (t1c, mc valid)
+    uint32_t known : 1;         // walk: the segment bound is known (below the LCA with the last hit)
+    uint32_t overflow : 1;      // aux pass dropped candidates above the kept PT_QK
+    uint32_t nh : 3;            // recorded replay hits (<= PT_REPLAY_HITS)
+    uint32_t sp : 7;            // Q_AUX: pending aux nodes on the per-lane stack
+    uint32_t pos : 7;           // walk: position reached in the ancestor list
+    uint32_t len : 7;           // walk: ancestor list length
+    uint32_t node;              // Q_AUX: aux node
     uint32_t lb;                // every candidate below lb has been processed
     uint32_t cand, skip, last;
     float bound;
     float dl;                   // certification margin (t units, see q_leaf_certain)
-    uint32_t walk;              // Q_REPLAY: 0 = candidate leaf check, else 1 + position in its ancestor list
-    uint32_t known;             // walk: the segment bound is known (below the LCA with the last hit)
+    uint32_t lref, lcnt;        // the candidate leaf's primitive range
+    uint32_t off;               // walk: ancestor list offset
+    uint32_t e[4];              // walk: the entries under test (0xffffffff = none)
     uint32_t astar;             // walk: deepest ancestor at or above that LCA seen so far
-    uint32_t robust;            // leaf check: the ray crosses the leaf box robustly (t1c, mc valid)
     float t1c, mc;              // leaf check: approximate entry and certification margin
-    uint32_t par;               // near-zero direction component: exact node tests, robust aux boxes
-    uint32_t overflow;
     uint32_t c[PT_QK];          // sorted candidates of this pass (0xffffffff = empty)
-    uint32_t nh;
     QHits H;
     float bt;                   // best BVH leaf hit so far (first strict minimum)
-    Hit res;                    // result so far (plane, then BVH hits that beat it)
-    int res_id;
+    float res_t;                // result so far (plane, then BVH hits that beat it): t and prim;
+    int res_id;                 // the normal is recomputed from the prim by the consumer
 };
+static_assert(PT_REPLAY_HITS < 8, "nh is a 3-bit field");
 
 struct QCounts {
     uint32_t nodes, aux, ptests, planes;
@@ -84,13 +93,13 @@ struct QCounts {
 PT_HD void q_init(const SceneView& S, const Ray& ray, Query& q, QCounts& C) {
     q.ray = ray;
     q.res_id = -1;
-    q.res.t = PT_INF;
+    q.res_t = PT_INF;
     float closest = PT_INF;
     for (uint32_t k = 0; k < S.n_planes; ++k) {
         const uint32_t pi = S.planes[k];
         Hit h;
         C.planes++;
-        if (plane_intersect(S.prims[pi], ray, h) && h.t < closest) { closest = h.t; q.res = h; q.res_id = (int)pi; }
+        if (plane_intersect(S.prims[pi], ray, h) && h.t < closest) { closest = h.t; q.res_t = h.t; q.res_id = (int)pi; }
     }
     q.P = closest;
     q.bt = PT_INF;
@@ -110,7 +119,6 @@ PT_HD void q_init(const SceneView& S, const Ray& ray, Query& q, QCounts& C) {
     }
     q.par = replay_ok_ray(ray) ? 0u : 1u;
     q.inv = mk3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
-    q.oinv = mk3(ray.o.x * q.inv.x, ray.o.y * q.inv.y, ray.o.z * q.inv.z);
     const float om = fmaxf(fmaxf(fabsf(ray.o.x), fabsf(ray.o.y)), fabsf(ray.o.z));
     const float dm = fminf(fminf(fabsf(ray.d.x), fabsf(ray.d.y)), fabsf(ray.d.z));
     q.dl = q.par ? INFINITY : 0x1p-18f * (S.box_extent + om) / dm;
@@ -143,7 +151,7 @@ PT_HD void q_next_candidate(Query& q) {
         q.last = v;
         if (v >= q.skip) {
             q.cand = v;
-            q.walk = 0;
+            q.walk = R_CAND;
             q.phase = Q_REPLAY;
             return;
         }
@@ -180,7 +188,7 @@ PT_HD bool q_leaf_hit(const SceneView& S, Query& q, uint32_t a, uint32_t ref, ui
         // BVH result = first strict minimum; it replaces the plane hit iff strictly closer
         if (lbh.t < q.bt) {
             q.bt = lbh.t;
-            if (lbh.t < q.P) { q.res = lbh; q.res_id = lid; }
+            if (lbh.t < q.P) { q.res_t = lbh.t; q.res_id = lid; }
         }
     }
     return true;
@@ -253,6 +261,7 @@ PT_HD void q_step(const SceneView& S, const AuxSL* aux, uint32_t n_aux, Query& q
 #pragma unroll
         for (int k = 0; k < PT_AUXW; ++k) e[k] = aux[q.node * PT_AUXW + k];
         C.aux++;
+        const f3 oinv = mk3(q.ray.o.x * q.inv.x, q.ray.o.y * q.inv.y, q.ray.o.z * q.inv.z);
         uint32_t next = 0xffffffffu;
 #pragma unroll
         for (int k = 0; k < PT_AUXW; ++k) {
@@ -271,8 +280,8 @@ PT_HD void q_step(const SceneView& S, const AuxSL* aux, uint32_t n_aux, Query& q
                     q_insert(q, leaf);
                 }
             } else if (q.par ? aux_box_par(e[k].a.x, e[k].a.y, e[k].a.z, e[k].a.w, e[k].b.x, e[k].b.y, q.ray, q.inv,
-                                           q.oinv)
-                             : aux_box(e[k].a.x, e[k].a.y, e[k].a.z, e[k].a.w, e[k].b.x, e[k].b.y, q.inv, q.oinv)) {
+                                           oinv)
+                             : aux_box(e[k].a.x, e[k].a.y, e[k].a.z, e[k].a.w, e[k].b.x, e[k].b.y, q.inv, oinv)) {
                 if (next == 0xffffffffu) next = code;
                 else stk.set(q.sp++, code);
             }
@@ -290,66 +299,96 @@ PT_HD void q_step(const SceneView& S, const AuxSL* aux, uint32_t n_aux, Query& q
         q_next_candidate(q);
         return;
     }
-    uint32_t verdict;   // 0 reject, 1 accept, 2 undecided
-    if (!q.walk) {
-        // Q_REPLAY, first visit of a candidate: its own leaf record
+    // Q_REPLAY.  One round of independent loads per step (the wave waits for
+    // its slowest lane's chain, so no step may chain two memory round trips).
+    bool reject = false;
+    if (q.walk == R_CAND) {
+        // the candidate's own leaf record (+ where its ancestor list is)
         const Node nd = S.nodes[q.cand];
+        const uint32_t info = S.anc_info[q.cand];
         C.nodes++;
-        verdict = q_leaf_certain(q, nd);
-        if (verdict == 2u) {
-            q.walk = 1u;
+        q.lref = f2u(nd.b.z);
+        q.lcnt = f2u(nd.b.w);
+        const uint32_t v = q_leaf_certain(q, nd);
+        if (v == 1u) {
+            q.walk = R_LEAF;
+            return;
+        }
+        if (v == 0u) {
+            reject = true;
+        } else {
+            // undecided: test the root path below a* = LCA(last recorded hit, cand).
+            // Ancestors at or above a* were entered on that hit's path (same
+            // node, same bound: both depend only on earlier hits) -- they are the
+            // list entries <= the hit.  Below a* no left subtree holds a hit, so
+            // the bound is constant: B = min{hits in (a*, right child of a*)}.
+            // Each remaining ancestor, then the leaf itself (entry len), is
+            // tested with B.
+            q.off = info & 0x03ffffffu;
+            q.len = info >> 26;
+            q.pos = 0u;
             q.known = q.nh == 0u ? 1u : 0u;   // no earlier hit: the bound is P on the whole path
             q.bound = q.P;
             q.astar = 0u;
+            q.walk = R_WALK_E;
             return;
         }
-    } else {
-        // Q_REPLAY, undecided candidate: its ancestor list, 4 entries per step.
-        // Ancestors at or above a* = LCA(last recorded hit h, cand) were entered on
-        // h's path (same node, same bound: both depend only on earlier hits) -- they
-        // are the list entries <= h.  Below a* no left subtree holds a hit, so the
-        // bound is constant: B = min{hits in (a*, right child of a*)}.  Each
-        // remaining ancestor, then the leaf itself, is tested with B.
-        const uint32_t info = S.anc_info[q.cand];
-        const uint32_t off = info & 0x03ffffffu, len = info >> 26;
-        const uint32_t pos = q.walk - 1u;
+    } else if (q.walk == R_LEAF) {
+        // leaf entered: its primitives (src/bvh.cpp:205-213)
+        if (!q_leaf_hit(S, q, q.cand, q.lref, q.lcnt, C)) {
+            q.phase = Q_EXACT;
+            return;
+        }
+    } else if (q.walk == R_WALK_E) {
+        // next 4 path entries (position len is the leaf itself)
         uint32_t hlast = 0u;   // last recorded hit (unrolled select: no dynamic register indexing)
 #pragma unroll
         for (int k = 0; k < PT_REPLAY_HITS; ++k)
             if ((uint32_t)k + 1u == q.nh) hlast = q.H.idx[k];
-        verdict = 2u;
+        bool any = false, accept = false;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t at = pos + (uint32_t)j;
-            if (verdict != 2u || at >= len) continue;
-            const uint32_t e = S.anc[off + at];
-            if (!q.known) {
-                if (e <= hlast) { q.astar = e; continue; }
-                q.bound = q_bound_between(q, q.astar, e);
-                q.known = 1u;
-                if (q.robust && q.bound >= q.t1c + q.mc) { verdict = 1u; continue; }   // whole segment certain
+            const uint32_t at = q.pos + (uint32_t)j;
+            uint32_t e = at < q.len ? S.anc[q.off + at] : (at == q.len ? q.cand : 0xffffffffu);
+            if (e != 0xffffffffu && !accept && !q.known) {
+                if (e <= hlast) {
+                    q.astar = e;          // entered on the last hit's path
+                    e = 0xffffffffu;
+                } else {
+                    q.bound = q_bound_between(q, q.astar, e);
+                    q.known = 1u;
+                    if (q.robust && q.bound >= q.t1c + q.mc) accept = true;   // whole segment certain
+                }
             }
+            if (accept) e = 0xffffffffu;
+            q.e[j] = e;
+            any = any || e != 0xffffffffu;
+        }
+        if (accept) {
+            q.walk = R_LEAF;
+            return;
+        }
+        if (any) {
+            q.walk = R_WALK_N;
+        } else {
+            q.pos += 4u;              // all at or above a*
+        }
+        return;
+    } else {
+        // R_WALK_N: the records of the pending entries, tested with B
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (q.e[j] == 0xffffffffu || reject) continue;
             C.nodes++;
-            if (!node_enter(S.nodes[e], q.ray, q.inv, q.bound, q.par != 0u)) verdict = 0u;
+            if (!node_enter(S.nodes[q.e[j]], q.ray, q.inv, q.bound, q.par != 0u)) reject = true;
         }
-        if (verdict == 2u) {
-            if (pos + 4u < len) {
-                q.walk += 4u;
-                return;
-            }
-            // every ancestor entered: the leaf itself, with its bound
-            if (!q.known) q.bound = q_bound_between(q, q.astar, q.cand);
-            if (q.robust && q.bound >= q.t1c + q.mc) verdict = 1u;
-            else verdict = node_enter(S.nodes[q.cand], q.ray, q.inv, q.bound, q.par != 0u) ? 1u : 0u;
-        }
-    }
-    if (verdict == 1u) {
-        const Node nd = S.nodes[q.cand];
-        if (!q_leaf_hit(S, q, q.cand, f2u(nd.b.z), f2u(nd.b.w), C)) {
-            q.phase = Q_EXACT;
+        if (!reject) {
+            q.pos += 4u;
+            q.walk = q.pos > q.len ? R_LEAF : R_WALK_E;   // past the leaf: entered
             return;
         }
     }
+    (void)reject;
     q.skip = q.cand + 1u;
     q_next_candidate(q);
 }
@@ -378,7 +417,11 @@ PT_HD int q_run(const SceneView& S, const AuxSL* aux, uint32_t n_aux, const Ray&
     while (q.phase == Q_AUX || q.phase == Q_REPLAY) q_step(S, aux, n_aux, q, C, stk);
     exact_used = q.phase == Q_EXACT ? 1u : 0u;
     if (exact_used) return q_exact(S, ray, stk, out, C);
-    out = q.res;
+    if (q.res_id >= 0) {
+        // the consumer's form: the hit recomputed from its primitive (identical operations)
+        const bool ok = prim_intersect(S.prims[q.res_id], ray, out);
+        if (!ok || f2u(out.t) != f2u(q.res_t)) C.planes |= 0x80000000u;   // must never happen (tests check)
+    }
     return q.res_id;
 }
 

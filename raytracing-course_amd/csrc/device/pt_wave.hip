@@ -1,25 +1,29 @@
 // pt_wave.hip -- wavefront form of the hw5 render loop on gfx950.
 //
-// One camera sample of every owned pixel = a short pipeline of launches on
-// one stream (no host round trips; counts stay on the device):
+// A pass advances every owned pixel by `target` samples (src/scene.cpp:
+// 189-203) through rounds of three launches on one stream:
 //
-//   k_wcamera        per pixel: the sample's 2 jitter draws, the camera ray
-//                    (src/scene.cpp:189-199), appended to queue 0
-//   for b < RAY_DEPTH:
-//     k_wisect       persistent, per-lane refilling closest-hit query
-//                    (pt_query.h): lanes pull rays in wave batches, one node
-//                    visit per loop trip, so the candidate tail of a few rays
-//                    never idles the rest of the wave
-//     k_wexact       the rare rays the replay hands back (exact stack DFS)
-//     k_wshade       per ray: the vertex's material logic and random draws
-//                    (shade_vertex), its fold record, and the child ray
-//                    appended to queue b+1 (wave-aggregated append)
-//   k_wfold          per pixel: backward fold of the vertex records
-//                    (bit-identical to the reference recursion) into the sum
+//   k_wcamera   (pass start) the first sample's 2 jitter draws and camera
+//               ray (src/scene.cpp:180-199) of every pixel -> fresh queue
+//   round r (parity p):
+//     k_wisect  persistent, per-lane refilling closest-hit query
+//               (pt_query.h): lanes pull fresh rays and suspended queries in
+//               wave batches and advance one node step per loop trip.  Once
+//               its wave has no more work to pull, a query may run
+//               `straggler_steps` more steps; then it is suspended (state +
+//               LDS stack to the carry queue) and resumes next round, so no
+//               round waits for the slowest ray of the frame
+//     k_wexact  the rare rays handed to the exact stack DFS
+//     k_wshade  per finished query: the vertex (shade_vertex: material logic
+//               and random draws) and its fold record, then either the child
+//               ray, or -- path over -- the backward fold into the pixel sum
+//               and the next sample's camera ray
 //
-// Each pixel's random stream is consumed in exactly the reference order: a
-// pixel has at most one ray in flight and its draws happen in camera, then
-// shade b = 0, 1, ... order.  Compiled with -ffp-contract=off (pt_core.h).
+// Every pixel has at most one ray in flight and consumes its random stream
+// in the reference order (jitter, then vertex by vertex), so results are
+// bit-identical however the rounds interleave pixels.  The host loops rounds
+// until the fresh and carry queues are empty.  Compiled with
+// -ffp-contract=off (pt_core.h).
 #include <hip/hip_runtime.h>
 
 #include "pt_devutil.h"
@@ -28,91 +32,134 @@
 
 namespace pt {
 
+__device__ __forceinline__ Rng load_rng(const PixelState& st, uint32_t slot) {
+    Rng R;
+    R.x = st.rng_x[slot];
+    R.saved = st.rng_saved[slot];
+    R.saved_ok = st.rng_flag[slot];
+    return R;
+}
+__device__ __forceinline__ void store_rng(const PixelState& st, uint32_t slot, const Rng& R) {
+    st.rng_x[slot] = R.x;
+    st.rng_saved[slot] = R.saved;
+    st.rng_flag[slot] = R.saved_ok;
+}
+
+// the pixel of an owned slot (slot = local tile * 256 + lane)
+__device__ __forceinline__ void slot_xy(const TileMap& tm, uint32_t slot, uint32_t& x, uint32_t& y) {
+    slot_pixel(tm, slot >> 8, slot & 255u, x, y);
+}
+
+// src/scene.cpp:193-196: one sample's jitter draws and camera ray
+__device__ __forceinline__ Ray camera_sample(const CamView& cam, Rng& R, uint32_t x, uint32_t y) {
+    const float fx = (float)x + rng_uniform(R);
+    const float fy = (float)y + rng_uniform(R);
+    return camera_ray(cam, fx, fy);
+}
+
 __global__ void __launch_bounds__(256) k_wcamera(WaveParams P) {
     const uint32_t slot = blockIdx.x * 256u + threadIdx.x;
     uint32_t x, y;
     const bool ok = slot_pixel(P.tm, blockIdx.x, threadIdx.x, x, y);
+    bool want = false;
     Ray ray;
     if (ok) {
-        Rng R;
-        R.x = P.st.rng_x[slot];
-        R.saved = P.st.rng_saved[slot];
-        R.saved_ok = P.st.rng_flag[slot];
-        const float fx = (float)x + rng_uniform(R);
-        const float fy = (float)y + rng_uniform(R);
-        ray = camera_ray(P.cam, fx, fy);
-        P.st.rng_x[slot] = R.x;
-        P.st.rng_flag[slot] = R.saved_ok;
-        P.st.rng_saved[slot] = R.saved;
-        P.pstate[slot] = P.depth ? (PE_LIVE << 8) : (PE_CUT << 8);
+        Rng R = load_rng(P.st, slot);
+        uint32_t done = P.nsamp[slot];
+        if (P.depth == 0u) {
+            // RayTrace(.., 0) = 0: only the jitter draws and sum += 0 per sample
+            f3 sum = mk3(P.st.sum[slot], P.st.sum[P.st.n_slots + slot], P.st.sum[2u * P.st.n_slots + slot]);
+            for (; done < P.target; ++done) {
+                (void)camera_sample(P.cam, R, x, y);
+                sum = sum + mk3(0.f, 0.f, 0.f);
+            }
+            P.st.sum[slot] = sum.x;
+            P.st.sum[P.st.n_slots + slot] = sum.y;
+            P.st.sum[2u * P.st.n_slots + slot] = sum.z;
+            P.nsamp[slot] = done;
+        } else if (done < P.target) {
+            ray = camera_sample(P.cam, R, x, y);
+            P.pstate[slot] = PE_LIVE << 8;
+            want = true;
+        }
+        store_rng(P.st, slot, R);
     }
-    const bool want = ok && P.depth > 0u;
-    const uint32_t qi = wave_append(P.ctl + 0, want);
+    uint32_t* ctl = P.ctl + 8u * P.parity;
+    const uint32_t qi = wave_append(ctl + C_FRESH, want);
     if (want) {
-        P.q[0].ro[qi] = F4{ray.o.x, ray.o.y, ray.o.z, u2f(slot)};
-        P.q[0].rd[qi] = F4{ray.d.x, ray.d.y, ray.d.z, 0.f};
+        P.fq[P.parity].ro[qi] = F4{ray.o.x, ray.o.y, ray.o.z, u2f(slot)};
+        P.fq[P.parity].rd[qi] = F4{ray.d.x, ray.d.y, ray.d.z, 0.f};
     }
 }
 
-__device__ __forceinline__ void write_hit(const WaveParams& P, uint32_t qi, int id, const Hit& h) {
-    if (id < 0) {
-        P.hits.id[qi] = 0xffffffffu;
-        return;
-    }
-    P.hits.th[qi] = F4{h.t, h.n.x, h.n.y, h.n.z};
-    P.hits.id[qi] = (uint32_t)id | (h.interior ? 0x80000000u : 0u);
-}
-
+#define PT_SUSPENDED 0xfffffffeu   // done.id of a query suspended to the next round
 #define PT_BATCH 64u
 #define PT_REFILL_MIN 16u
 
 __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
     extern __shared__ uint32_t lds_stack[];
     LdsMem stk{lds_stack + threadIdx.x};
-    const uint32_t b = P.bounce;
-    const uint32_t count = P.ctl[b];
-    uint32_t* head = P.ctl + P.depth + 1u + b;
-    const WaveQueue Q = P.q[b & 1u];
-    // wave-uniform batch of queue indices
+    const uint32_t p = P.parity;
+    const uint32_t* in = P.ctl + 8u * p;
+    uint32_t* out = P.ctl + 8u * (1u - p);
+    const uint32_t n_fresh = in[C_FRESH], n_total = n_fresh + in[C_CARRY];
+    const RayQ FQ = P.fq[p];
+    const uint32_t* CQ = P.cq[p];
+    uint32_t* CQout = P.cq[1u - p];
+    // wave-uniform batch of work indices: [0, n_fresh) fresh rays, then suspended queries
     uint32_t bbase = 0u, bleft = 0u;
     bool exhausted = false;
     bool active = false;
-    uint32_t qi = 0u;
+    uint32_t slot = 0u, post = 0u, wi = 0u;
     Query q;
     QCounts C{0u, 0u, 0u, 0u};
     uint32_t rays = 0u, fallbacks = 0u, init_exact = 0u;
+    uint64_t t_start = 0, iters = 0;
+    if (P.wg_prof && threadIdx.x == 0) t_start = __builtin_amdgcn_s_memrealtime();
     for (;;) {
+        iters++;
         const unsigned long long idle = __ballot(!active);
         uint32_t nidle = (uint32_t)__popcll(idle);
         if (!exhausted && (nidle >= PT_REFILL_MIN || nidle == 64u)) {
             uint32_t rank = lanes_below(idle);
-            bool fresh = false;
+            bool got = false;
             while (nidle > 0u) {
                 if (bleft == 0u) {
                     uint32_t v = 0u;
-                    if (lane_id() == 0u) v = atomicAdd(head, PT_BATCH);
+                    if (lane_id() == 0u) v = atomicAdd(out + C_HEAD, PT_BATCH);
                     v = __builtin_amdgcn_readfirstlane(v);
-                    if (v >= count) { exhausted = true; break; }
+                    if (v >= n_total) { exhausted = true; break; }
                     bbase = v;
-                    bleft = count - v < PT_BATCH ? count - v : PT_BATCH;
+                    bleft = n_total - v < PT_BATCH ? n_total - v : PT_BATCH;
                 }
                 const uint32_t take = nidle < bleft ? nidle : bleft;
-                if (!active && !fresh) {
-                    if (rank < take) { qi = bbase + rank; fresh = true; }
+                if (!active && !got) {
+                    if (rank < take) { wi = bbase + rank; got = true; }
                     else rank -= take;
                 }
                 bbase += take;
                 bleft -= take;
                 nidle -= take;
             }
-            if (fresh) {
-                const F4 o = Q.ro[qi], d = Q.rd[qi];
-                Ray ray;
-                ray.o = mk3(o.x, o.y, o.z);
-                ray.d = mk3(d.x, d.y, d.z);
-                rays++;
-                q_init(P.S, ray, q, C);
-                if (q.phase == Q_EXACT) init_exact++;
+            if (got) {
+                post = 0u;
+                if (wi < n_fresh) {
+                    const F4 o = FQ.ro[wi], d = FQ.rd[wi];
+                    Ray ray;
+                    ray.o = mk3(o.x, o.y, o.z);
+                    ray.d = mk3(d.x, d.y, d.z);
+                    slot = f2u(o.w);
+                    rays++;
+                    q_init(P.S, ray, q, C);
+                    if (q.phase == Q_EXACT) init_exact++;
+                } else {
+                    // resume a suspended query: state, slot, then its aux stack into LDS
+                    const uint32_t* w = CQ + (size_t)(wi - n_fresh) * P.carry_words;
+                    q = *reinterpret_cast<const Query*>(w);
+                    const uint32_t* tail = w + sizeof(Query) / 4u;
+                    slot = tail[0];
+                    for (uint32_t k = 0; k < q.sp; ++k) stk.set(k, tail[1u + k]);
+                }
                 active = true;
             }
         }
@@ -120,13 +167,32 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
         if (active) {
             if (q.phase == Q_AUX || q.phase == Q_REPLAY) q_step(P.S, P.aux, P.n_aux, q, C, stk);
             if (q.phase == Q_DONE) {
-                write_hit(P, qi, q.res_id, q.res);
+                // results stay at the work index: no compaction, no atomics
+                const uint32_t k = wi;
+                P.done.ro[k] = F4{q.ray.o.x, q.ray.o.y, q.ray.o.z, u2f(slot)};
+                P.done.rd[k] = F4{q.ray.d.x, q.ray.d.y, q.ray.d.z, 0.f};
+                P.done.id[k] = q.res_id < 0 ? 0xffffffffu : (uint32_t)q.res_id;
                 active = false;
             } else if (q.phase == Q_EXACT) {
-                const uint32_t k = atomicAdd(P.ctl + 2u * (P.depth + 1u) + b, 1u);
-                P.fb[k] = qi;
+                const uint32_t k = atomicAdd(out + C_EXACT, 1u);   // rare
+                P.ex.ro[k] = F4{q.ray.o.x, q.ray.o.y, q.ray.o.z, u2f(slot)};
+                P.ex.rd[k] = F4{q.ray.d.x, q.ray.d.y, q.ray.d.z, u2f(wi)};
                 fallbacks++;
                 active = false;
+            } else if (exhausted && ++post >= P.straggler_steps) {
+                // this wave has nothing left to pull: suspend instead of holding up the round
+                const uint32_t k = atomicAdd(out + C_CARRY, 1u);
+                if (k < P.carry_cap) {
+                    uint32_t* w = CQout + (size_t)k * P.carry_words;
+                    *reinterpret_cast<Query*>(w) = q;
+                    uint32_t* tail = w + sizeof(Query) / 4u;
+                    tail[0] = slot;
+                    for (uint32_t j = 0; j < q.sp; ++j) tail[1u + j] = stk.get(j);
+                    P.done.id[wi] = PT_SUSPENDED;
+                    active = false;
+                } else {
+                    atomicSub(out + C_CARRY, 1u);   // carry queue full: keep running
+                }
             }
         }
     }
@@ -137,25 +203,37 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
     wave_add_u64(P.counters + 5, C.aux);
     wave_add_u64(P.counters + 6, fallbacks);
     wave_add_u64(P.counters + 7, init_exact);
+    if (P.wg_prof) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long* w = P.wg_prof + 5ull * blockIdx.x;
+            w[0] = t_start;
+            w[1] = __builtin_amdgcn_s_memrealtime();
+            w[2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            w[3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+            w[4] = iters;
+        }
+    }
 }
 
 // exact stack DFS for the handed-back rays; 64-lane workgroups, stack in LDS
 __global__ void __launch_bounds__(64) k_wexact(WaveParams P) {
     extern __shared__ uint32_t lds_stack[];
-    const uint32_t b = P.bounce;
-    const uint32_t n = P.ctl[2u * (P.depth + 1u) + b];
-    const WaveQueue Q = P.q[b & 1u];
+    uint32_t* out = P.ctl + 8u * (1u - P.parity);
+    const uint32_t n = out[C_EXACT];
     LdsMemN<64u> stk{lds_stack + threadIdx.x};
     QCounts C{0u, 0u, 0u, 0u};
     for (uint32_t k = blockIdx.x * 64u + threadIdx.x; k < n; k += gridDim.x * 64u) {
-        const uint32_t qi = P.fb[k];
-        const F4 o = Q.ro[qi], d = Q.rd[qi];
+        const F4 o = P.ex.ro[k], d = P.ex.rd[k];
         Ray ray;
         ray.o = mk3(o.x, o.y, o.z);
         ray.d = mk3(d.x, d.y, d.z);
         Hit h;
         const int id = q_exact(P.S, ray, stk, h, C);
-        write_hit(P, qi, id, h);
+        const uint32_t j = f2u(d.w);   // the ray's work index
+        P.done.ro[j] = o;
+        P.done.rd[j] = F4{d.x, d.y, d.z, 0.f};
+        P.done.id[j] = id < 0 ? 0xffffffffu : (uint32_t)id;
     }
     wave_add_u64(P.counters + 1, C.nodes);
     wave_add_u64(P.counters + 2, C.ptests);
@@ -163,93 +241,96 @@ __global__ void __launch_bounds__(64) k_wexact(WaveParams P) {
 }
 
 __global__ void __launch_bounds__(256) k_wshade(WaveParams P) {
-    const uint32_t b = P.bounce;
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    const bool in = i < P.ctl[b];
-    bool cont = false;
-    Ray ray;
-    uint32_t slot = 0u;
-    if (in) {
-        const WaveQueue Q = P.q[b & 1u];
-        const F4 o = Q.ro[i], d = Q.rd[i];
-        slot = f2u(o.w);
-        ray.o = mk3(o.x, o.y, o.z);
-        ray.d = mk3(d.x, d.y, d.z);
-        const uint32_t hid = P.hits.id[i];
-        const uint32_t nv = P.pstate[slot] & 0xffu;
-        if (hid == 0xffffffffu) {
-            P.pstate[slot] = nv | (PE_MISS << 8);
-        } else {
-            const F4 th = P.hits.th[i];
-            Hit h;
-            h.t = th.x;
-            h.n = mk3(th.y, th.z, th.w);
-            h.interior = hid >> 31;
-            const int id = (int)(hid & 0x7fffffffu);
-            Rng R;
-            R.x = P.st.rng_x[slot];
-            R.saved = P.st.rng_saved[slot];
-            R.saved_ok = P.st.rng_flag[slot];
-            uint32_t idm;
-            float s1, s2;
-            cont = shade_vertex(P.S, R, ray, h, id, idm, s1, s2);
-            P.st.rng_x[slot] = R.x;
-            P.st.rng_saved[slot] = R.saved;
-            P.st.rng_flag[slot] = R.saved_ok;
-            HbmVStore vs{P.vscratch + slot, P.st.n_slots};
-            vs.put(nv, idm, s1, s2);
+    const uint32_t* in = P.ctl + 8u * P.parity;
+    uint32_t* out = P.ctl + 8u * (1u - P.parity);
+    const uint32_t n = in[C_FRESH] + in[C_CARRY];   // work indices of this round
+    const RayQ N = P.fq[1u - P.parity];
+    const uint32_t stride = gridDim.x * 256u;
+    // grid-stride with a uniform trip count so the wave-aggregated append sees every lane
+    for (uint32_t base = blockIdx.x * 256u; base < n; base += stride) {
+        const uint32_t i = base + threadIdx.x;
+        bool emit = false;
+        Ray ray;
+        uint32_t slot = 0u;
+        const uint32_t hid = i < n ? P.done.id[i] : PT_SUSPENDED;
+        if (hid != PT_SUSPENDED) {
+            const F4 o = P.done.ro[i], d = P.done.rd[i];
+            slot = f2u(o.w);
+            ray.o = mk3(o.x, o.y, o.z);
+            ray.d = mk3(d.x, d.y, d.z);
+            uint32_t nv = P.pstate[slot] & 0xffu;
             uint32_t end = PE_LIVE;
-            if (!cont) end = PE_TERM;
-            else if (b + 1u >= P.depth) { end = PE_CUT; cont = false; }   // RayTrace(.., 0) = 0
-            P.pstate[slot] = (nv + 1u) | (end << 8);
+            Rng R = load_rng(P.st, slot);
+            if (hid == 0xffffffffu) {
+                end = PE_MISS;
+            } else {
+                // the closest hit's t, normal and side: recomputed from its primitive
+                // (the query's own test, same operations -> same bits)
+                Hit h;
+                (void)prim_intersect(P.S.prims[hid], ray, h);
+                uint32_t idm;
+                float s1, s2;
+                const bool cont = shade_vertex(P.S, R, ray, h, (int)hid, idm, s1, s2);
+                HbmVStore vs{P.vscratch + slot, P.st.n_slots};
+                vs.put(nv, idm, s1, s2);
+                ++nv;
+                if (!cont) end = PE_TERM;
+                else if (nv >= P.depth) end = PE_CUT;   // RayTrace(.., 0) = 0
+                else emit = true;
+            }
+            if (end != PE_LIVE) {
+                // path over: backward fold (deepest vertex first), src/scene.cpp:198 sum += ...
+                f3 L = end == PE_MISS ? P.S.bg : mk3(0.f, 0.f, 0.f);
+                HbmVStore vs{P.vscratch + slot, P.st.n_slots};
+                for (uint32_t k = nv; k > 0u; --k) {
+                    uint32_t idm;
+                    float s1, s2;
+                    vs.get(k - 1u, idm, s1, s2);
+                    L = fold_vertex(P.S, L, idm, s1, s2);
+                }
+                P.st.sum[slot] = P.st.sum[slot] + L.x;
+                P.st.sum[P.st.n_slots + slot] = P.st.sum[P.st.n_slots + slot] + L.y;
+                P.st.sum[2u * P.st.n_slots + slot] = P.st.sum[2u * P.st.n_slots + slot] + L.z;
+                const uint32_t done = P.nsamp[slot] + 1u;
+                P.nsamp[slot] = done;
+                nv = 0u;
+                if (done < P.target) {
+                    // the pixel's next sample: jitter draws + camera ray
+                    uint32_t x, y;
+                    slot_xy(P.tm, slot, x, y);
+                    ray = camera_sample(P.cam, R, x, y);
+                    emit = true;
+                }
+            }
+            P.pstate[slot] = nv;
+            store_rng(P.st, slot, R);
+        }
+        const uint32_t qn = wave_append(out + C_FRESH, emit);
+        if (emit) {
+            N.ro[qn] = F4{ray.o.x, ray.o.y, ray.o.z, u2f(slot)};
+            N.rd[qn] = F4{ray.d.x, ray.d.y, ray.d.z, 0.f};
         }
     }
-    const uint32_t qn = wave_append(P.ctl + b + 1u, cont);
-    if (cont) {
-        const WaveQueue N = P.q[(b + 1u) & 1u];
-        N.ro[qn] = F4{ray.o.x, ray.o.y, ray.o.z, u2f(slot)};
-        N.rd[qn] = F4{ray.d.x, ray.d.y, ray.d.z, 0.f};
-    }
-}
-
-__global__ void __launch_bounds__(256) k_wfold(WaveParams P) {
-    const uint32_t slot = blockIdx.x * 256u + threadIdx.x;
-    uint32_t x, y;
-    if (!slot_pixel(P.tm, blockIdx.x, threadIdx.x, x, y)) return;
-    const uint32_t ps = P.pstate[slot];
-    uint32_t nv = ps & 0xffu;
-    f3 L = (ps >> 8) == PE_MISS ? P.S.bg : mk3(0.f, 0.f, 0.f);
-    HbmVStore vs{P.vscratch + slot, P.st.n_slots};
-    while (nv > 0u) {
-        --nv;
-        uint32_t idm;
-        float s1, s2;
-        vs.get(nv, idm, s1, s2);
-        L = fold_vertex(P.S, L, idm, s1, s2);
-    }
-    // src/scene.cpp:198: sum += RayTrace(...)
-    P.st.sum[slot] = P.st.sum[slot] + L.x;
-    P.st.sum[P.st.n_slots + slot] = P.st.sum[P.st.n_slots + slot] + L.y;
-    P.st.sum[2u * P.st.n_slots + slot] = P.st.sum[2u * P.st.n_slots + slot] + L.z;
 }
 
 }  // namespace pt
 
 extern "C++" {
-hipError_t pt_launch_wave_sample(pt::WaveParams p, uint32_t isect_grid, hipStream_t s) {
-    const uint32_t nt = p.n_tiles_local;
-    const uint32_t D = p.depth;
-    hipError_t e = hipMemsetAsync(p.ctl, 0, 4u * (3u * (D + 1u)), s);
+hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(p.ctl, 0, 4u * 16u, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(pt::k_wcamera, dim3(nt), dim3(256), 0, s, p);
+    p.parity = 0u;
+    hipLaunchKernelGGL(pt::k_wcamera, dim3(p.n_tiles_local), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_wave_round(pt::WaveParams p, uint32_t isect_grid, uint32_t shade_grid, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(p.ctl + 8u * (1u - p.parity), 0, 4u * 8u, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(pt::k_wisect, dim3(isect_grid), dim3(256), 1024u * p.aux_stack, s, p);
     const uint32_t exact_lds = 64u * 4u * (p.max_stack ? p.max_stack : 1u);
-    for (uint32_t b = 0; b < D; ++b) {
-        p.bounce = b;
-        hipLaunchKernelGGL(pt::k_wisect, dim3(isect_grid), dim3(256), 1024u * p.aux_stack, s, p);
-        hipLaunchKernelGGL(pt::k_wexact, dim3(64), dim3(64), exact_lds, s, p);
-        hipLaunchKernelGGL(pt::k_wshade, dim3(nt), dim3(256), 0, s, p);
-    }
-    hipLaunchKernelGGL(pt::k_wfold, dim3(nt), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(pt::k_wexact, dim3(64), dim3(64), exact_lds, s, p);
+    hipLaunchKernelGGL(pt::k_wshade, dim3(shade_grid), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 }

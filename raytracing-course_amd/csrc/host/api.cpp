@@ -93,11 +93,14 @@ struct pt_session {
     // wavefront engine buffers (replay traversal)
     bool wave = false;
     uint32_t* pstate = nullptr;
-    pt::F4* qbuf = nullptr;       // 5 * n_slots F4: q0.ro, q0.rd, q1.ro, q1.rd, hits.th
-    uint32_t* hid = nullptr;      // n_slots
-    uint32_t* fb = nullptr;       // n_slots
-    uint32_t* ctl = nullptr;      // 3 * (depth + 1)
-    uint32_t isect_grid = 0;
+    uint32_t* nsamp = nullptr;    // samples completed per slot
+    pt::F4* qbuf = nullptr;       // 8 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd
+    uint32_t* hid = nullptr;      // n_slots (done.id)
+    uint32_t* carry = nullptr;    // 2 * carry_cap * carry_words
+    uint32_t carry_cap = 0, carry_words = 0, straggler_steps = 64;
+    uint32_t* ctl = nullptr;      // 2 x 8 round counters
+    uint32_t* ctl_host = nullptr; // pinned copy of one counter set
+    uint32_t isect_grid = 0, shade_grid = 0, rounds = 0;
     hipStream_t stream = nullptr;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
     double kernel_ms = 0.0, resolve_ms = 0.0;
@@ -489,12 +492,22 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
     ss->wave = o->traversal == PT_TRAVERSAL_REPLAY;
     if (const char* e = getenv("PT_ENGINE")) ss->wave = ss->wave && strcmp(e, "mega") != 0;
     if (ss->wave) {
-        if (hipMalloc(&ss->pstate, n * 4) != hipSuccess || hipMalloc(&ss->qbuf, 5 * n * 16) != hipSuccess ||
-            hipMalloc(&ss->hid, n * 4) != hipSuccess || hipMalloc(&ss->fb, n * 4) != hipSuccess ||
-            hipMalloc(&ss->ctl, 4ull * 3 * (ss->depth + 1)) != hipSuccess)
+        // suspended-query records: Query | slot | aux stack, rounded to 16 B
+        ss->carry_words = ((uint32_t)(sizeof(pt::Query) / 4) + 1u + std::max<uint32_t>(s->auxw_stack, 1u) + 3u) & ~3u;
+        ss->carry_cap = (uint32_t)std::max<size_t>(4096, n / 16);
+        if (const char* g = getenv("PT_STRAGGLER")) ss->straggler_steps = (uint32_t)std::max(1, atoi(g));
+        if (hipMalloc(&ss->pstate, n * 4) != hipSuccess || hipMalloc(&ss->qbuf, 8 * n * 16) != hipSuccess ||
+            hipMalloc(&ss->hid, n * 4) != hipSuccess || hipMalloc(&ss->nsamp, n * 4) != hipSuccess ||
+            hipMalloc(&ss->carry, 2ull * ss->carry_cap * ss->carry_words * 4) != hipSuccess ||
+            hipMalloc(&ss->ctl, 64) != hipSuccess || hipHostMalloc(&ss->ctl_host, 64) != hipSuccess)
             return cleanup(fail(PT_E_OOM, "device allocation failed (wavefront buffers)"));
+        if (hipMemsetAsync(ss->nsamp, 0, n * 4, ss->stream) != hipSuccess ||
+            hipMemsetAsync(ss->pstate, 0, n * 4, ss->stream) != hipSuccess)
+            return cleanup(fail(PT_E_HIP, "memset failed"));
         hipDeviceProp_t pr;
         if (hipGetDeviceProperties(&pr, ss->dev) != hipSuccess) return cleanup(fail(PT_E_HIP, "device query failed"));
+        ss->shade_grid = std::min<uint32_t>((uint32_t)std::max(1, pr.multiProcessorCount) * 8u,
+                                            std::max(1u, ss->n_tiles_local));
         // persistent intersection grid: 4 workgroups (16 waves) per CU, capped by the work
         ss->isect_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * 4u;
         if (const char* g = getenv("PT_ISECT_WG_PER_CU")) ss->isect_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * (uint32_t)std::max(1, atoi(g));
@@ -544,25 +557,61 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.st = ss->st;
     wp.vscratch = ss->vscratch;
     wp.pstate = ss->pstate;
+    wp.nsamp = ss->nsamp;
     const size_t n = std::max<size_t>(ss->n_slots, 1);
-    wp.q[0].ro = ss->qbuf;
-    wp.q[0].rd = ss->qbuf + n;
-    wp.q[1].ro = ss->qbuf + 2 * n;
-    wp.q[1].rd = ss->qbuf + 3 * n;
-    wp.hits.th = ss->qbuf + 4 * n;
-    wp.hits.id = ss->hid;
-    wp.fb = ss->fb;
+    wp.fq[0] = pt::RayQ{ss->qbuf, ss->qbuf + n};
+    wp.fq[1] = pt::RayQ{ss->qbuf + 2 * n, ss->qbuf + 3 * n};
+    wp.done = pt::DoneQ{ss->qbuf + 4 * n, ss->qbuf + 5 * n, ss->hid};
+    wp.ex = pt::RayQ{ss->qbuf + 6 * n, ss->qbuf + 7 * n};
+    wp.cq[0] = ss->carry;
+    wp.cq[1] = ss->carry + (size_t)ss->carry_cap * ss->carry_words;
+    wp.carry_cap = ss->carry_cap;
+    wp.carry_words = ss->carry_words;
     wp.ctl = ss->ctl;
     wp.counters = ss->counters;
     wp.depth = ss->depth;
+    wp.target = (uint32_t)(ss->samples_done + spp);
     wp.n_tiles_local = ss->n_tiles_local;
     wp.max_stack = std::max<uint32_t>(s->max_stack, 1u);
     wp.aux_stack = std::max<uint32_t>(s->auxw_stack, 1u);
+    wp.straggler_steps = ss->straggler_steps;
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
     HIP_TRY(hipEventRecord(e0, ss->stream));
-    for (uint32_t k = 0; k < spp; ++k) HIP_TRY(pt_launch_wave_sample(wp, ss->isect_grid, ss->stream));
+    HIP_TRY(pt_launch_wave_start(wp, ss->stream));
+    // rounds until no fresh ray and no suspended query is left; counts are
+    // checked every few rounds (empty rounds are cheap, syncs are not free)
+    uint32_t p = 0, batch = 4;
+    for (uint32_t guard = 0;; ++guard) {
+        for (uint32_t r = 0; r < batch; ++r) {
+            wp.parity = p;
+            const char* wgp = getenv("PT_WGPROF");
+            if (wgp && *wgp) {
+                // diagnostics: per-round isect workgroup timelines appended to $PT_WGPROF
+                if (!ss->wg_prof) HIP_TRY(hipMalloc(&ss->wg_prof, 40ull * ss->isect_grid));
+                HIP_TRY(hipMemsetAsync(ss->wg_prof, 0, 40ull * ss->isect_grid, ss->stream));
+                wp.wg_prof = ss->wg_prof;
+            }
+            HIP_TRY(pt_launch_wave_round(wp, ss->isect_grid, ss->shade_grid, ss->stream));
+            if (wp.wg_prof) {
+                std::vector<unsigned long long> h(5ull * ss->isect_grid);
+                HIP_TRY(hipMemcpyAsync(h.data(), wp.wg_prof, h.size() * 8, hipMemcpyDeviceToHost, ss->stream));
+                HIP_TRY(hipStreamSynchronize(ss->stream));
+                if (FILE* f = fopen(wgp, "ab")) {
+                    fwrite(h.data(), 8, h.size(), f);
+                    fclose(f);
+                }
+            }
+            ss->rounds++;
+            p ^= 1u;
+        }
+        HIP_TRY(hipMemcpyAsync(ss->ctl_host, ss->ctl + 8u * p, 8, hipMemcpyDeviceToHost, ss->stream));
+        HIP_TRY(hipStreamSynchronize(ss->stream));
+        if (ss->ctl_host[pt::C_FRESH] == 0u && ss->ctl_host[pt::C_CARRY] == 0u) break;
+        if (guard > 100000u) return fail(PT_E_HIP, "wavefront rounds did not drain");
+        batch = ss->ctl_host[pt::C_FRESH] + ss->ctl_host[pt::C_CARRY] > 4096u ? 4u : 2u;
+    }
     HIP_TRY(hipEventRecord(e1, ss->stream));
     ss->pending.emplace_back(e0, e1);
     ss->samples_done += spp;
@@ -716,8 +765,9 @@ void pt_session_free(pt_session* ss) {
     (void)hipFree(ss->st.rng_x); (void)hipFree(ss->st.rng_saved); (void)hipFree(ss->st.rng_flag);
     (void)hipFree(ss->st.sum); (void)hipFree(ss->vscratch); (void)hipFree(ss->counters);
     (void)hipFree(ss->out); (void)hipFree(ss->rad); (void)hipFree(ss->wg_prof);
-    (void)hipFree(ss->pstate); (void)hipFree(ss->qbuf); (void)hipFree(ss->hid); (void)hipFree(ss->fb);
-    (void)hipFree(ss->ctl);
+    (void)hipFree(ss->pstate); (void)hipFree(ss->qbuf); (void)hipFree(ss->hid); (void)hipFree(ss->nsamp);
+    (void)hipFree(ss->carry); (void)hipFree(ss->ctl);
+    if (ss->ctl_host) (void)hipHostFree(ss->ctl_host);
     if (ss->stream) (void)hipStreamDestroy(ss->stream);
     delete ss;
 }
@@ -892,6 +942,7 @@ int pt_selftest_ray_intersection(pt_scene* s, int32_t traversal, uint32_t n, con
             pt::QCounts Q{0u, 0u, 0u, 0u};
             uint32_t ex = 0;
             id = pt::q_run(V, s->auxsl.data(), (uint32_t)s->auxsl.size(), r, stk, h, Q, ex);
+            if (Q.planes & 0x80000000u) return fail(PT_E_INVALID, "recomputed closest hit differs from the query's");
             C.rays++;
             C.nodes += Q.nodes; C.ptests += Q.ptests; C.planes += Q.planes; C.aux += Q.aux; C.fallbacks += ex;
         } else {
@@ -947,6 +998,7 @@ int pt_selftest_render_host(pt_scene* s, int32_t traversal, uint32_t x0, uint32_
                             uint32_t ex = 0;
                             const int id = pt::q_run(V, s->auxsl.data(), (uint32_t)s->auxsl.size(), rr, stk, hh, Q, ex);
                             cc.fallbacks += ex;
+                            if (Q.planes & 0x80000000u) cc.errs |= 4u;   // recomputed hit differs (checked below)
 #ifdef PT_QDIAG
                             if (qlog) qlog->push_back({Q.aux, Q.steps, Q.ptests | (ex << 31), Q.cands | (Q.passes << 16)});
 #else
