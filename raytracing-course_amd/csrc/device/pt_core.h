@@ -199,7 +199,11 @@ struct SceneView {
     f3 bg;
     float box_extent;           // max |coordinate| over the reference node boxes (replay certification)
     const uint32_t* anc_info;   // per reference node: offset | length << 26 of its ancestor list (leaves)
-    const uint32_t* anc;        // ancestor lists: root .. parent, ascending preorder indices
+    const uint32_t* anc;        // ancestor lists: root .. parent, the leaf, padding to 4 (ascending)
+    // the query's single fetch space: every array above that the wavefront query
+    // reads lives in one 16-B-aligned blob, addressed by 32-bit byte offsets
+    const F4* blob;
+    uint32_t o_nodes, o_aux, o_ainfo, o_anc, o_qprim, o_prim;
 };
 
 struct Ray { f3 o, d; };

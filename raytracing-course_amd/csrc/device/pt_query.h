@@ -1,26 +1,31 @@
 // pt_query.h -- the closest-hit query of the wavefront renderer as a per-lane
 // state machine (Scene::RayIntersection, src/scene.cpp:46-77, with the
 // reference BVH semantics of src/bvh.cpp:181-225 reproduced by candidate
-// replay; see pt_trace.h for the replay argument).
+// replay; the argument is in DESIGN.md §2 and at each step below).
 //
-// Built for a persistent, refilling intersection kernel: every call of
-// q_step() advances ONE lane by one node visit, so lanes whose rays need many
-// visits (the candidate tail: p99 ~25 leaves) no longer hold the other 63
-// lanes of their wave -- an idle lane simply takes the next ray.
+// Built for a persistent, refilling intersection kernel: every q_step()
+// advances ONE lane by one step, so the rays with long candidate lists do not
+// hold the other lanes of their wave -- an idle lane takes the next ray.
 //
-//   * auxiliary BVH: stackless BVH2 in DFS preorder with skip links
-//     (AuxSL, 32 B): internal = conservative inflated box; leaf = the
-//     reference leaf's own exact (center, half-size), tested with the filtered
-//     exact test node_enter() -- one dependent load per visit, no stack.
-//   * candidates: the PT_QK smallest reference-leaf indices of the pass, kept
-//     sorted in registers by a min/max insertion network (no LDS, no dynamic
-//     register indexing); more than PT_QK -> further passes above the last
-//     processed index (rare).
-//   * replay: one reference node per step, root -> candidate, with the
-//     reference's pruning and right-child bounds.
-// Rays the replay cannot take (non-finite or near-zero direction
-// components) or whose replay hit list overflows are flagged for the exact
-// stack DFS (bvh_exact) in a separate pass.
+// Memory discipline (the kernel is bound by the latency of dependent
+// L2/Infinity-Cache loads): a step is  addresses -> ONE batch of eight
+// independent 16-B loads -> compute.  Every phase expresses its reads as up to
+// eight 16-B pieces of one "blob" (all query arrays, 16-B aligned, 32-bit byte
+// offsets), so lanes in different phases share one round trip per step
+// instead of serialising one per phase and one per guarded load.
+//
+//   * auxiliary BVH: 4-wide, nodes of 4 x 32-B entries (one step); internal
+//     entries are conservative inflated boxes, leaf entries carry the
+//     reference leaf's exact (center, half-size), tested with node_enter();
+//     pending nodes on a per-lane LDS stack.
+//   * candidates: the PT_QK smallest reference-leaf indices of the pass,
+//     sorted in registers (min/max insertion network); more -> further passes
+//     above the last processed index.
+//   * replay per candidate: its leaf record (certain accept / certain reject),
+//     else its ancestor list below the LCA with the last hit, 4 entries then
+//     their 4 records per step; entered leaves test one primitive per step.
+// Rays with non-finite components or a fifth replay hit take the exact stack
+// DFS (bvh_exact) in a separate pass.
 #pragma once
 #include "pt_trace.h"
 
@@ -43,6 +48,34 @@ struct AuxSL { F4 a, b; };
 enum : uint32_t { Q_AUX = 0u, Q_REPLAY = 1u, Q_DONE = 2u, Q_EXACT = 3u };
 // replay step kinds: each issues one round of independent loads
 enum : uint32_t { R_CAND = 0u, R_LEAF = 1u, R_WALK_E = 2u, R_WALK_N = 3u };
+
+// compact primitive records of the query (48 B, blob section o_qprim, same index
+// as the full 80-B records):
+//   plain triangle (pos = +0, rotation = (0,0,0,1) exactly): {a.xyz, T_TRIANGLE}, {b.xyz, c.x}, {c.y, c.z, -, -}
+//   box / ellipsoid:                                        {size.xyz, type}, {pos.xyz, rot.x}, {rot.yzw, -}
+//   anything else:                                           {-, -, -, type | PT_QP_FULL} -> full record
+#define PT_QP_FULL 0x100u
+
+// the full Prim a compact record stands for (bit-identical fields, so
+// bvh_prim_intersect performs exactly the reference operations)
+PT_HD Prim qprim_expand(const F4& r0, const F4& r1, const F4& r2) {
+    Prim P;
+    const uint32_t type = f2u(r0.w);
+    if (type == T_TRIANGLE) {
+        P.p0 = F4{0.f, 0.f, 0.f, r0.w};
+        P.p1 = F4{0.f, 0.f, 0.f, 1.f};
+        P.p2 = F4{r0.x, r0.y, r0.z, 0.f};
+        P.p3 = r1;
+        P.p4 = F4{r2.x, r2.y, 0.f, 0.f};
+    } else {
+        P.p0 = F4{r1.x, r1.y, r1.z, r0.w};
+        P.p1 = F4{r1.w, r2.x, r2.y, r2.z};
+        P.p2 = F4{r0.x, r0.y, r0.z, 0.f};
+        P.p3 = F4{0.f, 0.f, 0.f, 0.f};
+        P.p4 = F4{0.f, 0.f, 0.f, 0.f};
+    }
+    return P;
+}
 
 struct QHits {                  // replay hit list (reference leaf index, leaf first-min t)
     uint32_t idx[PT_REPLAY_HITS];
@@ -70,6 +103,9 @@ struct Query {
     float bound;
     float dl;                   // certification margin (t units, see q_leaf_certain)
     uint32_t lref, lcnt;        // the candidate leaf's primitive range
+    uint32_t li;                // R_LEAF: primitives tested so far (bit 31: next fetch = full record)
+    float lt;                   // R_LEAF: leaf first-min t so far
+    int lid;                    // R_LEAF: its primitive (-1 none)
     uint32_t off;               // walk: ancestor list offset
     uint32_t e[4];              // walk: the entries under test (0xffffffff = none)
     uint32_t astar;             // walk: deepest ancestor at or above that LCA seen so far
@@ -168,30 +204,29 @@ PT_HD void q_next_candidate(Query& q) {
     q.phase = Q_DONE;
 }
 
-// leaf reached: first-min over its primitives (src/bvh.cpp:205-213), hit bookkeeping
-// returns false when the replay hit list is full (the ray then takes the exact DFS)
-PT_HD bool q_leaf_hit(const SceneView& S, Query& q, uint32_t a, uint32_t ref, uint32_t cnt, QCounts& C) {
-    Hit lbh;
-    lbh.t = PT_INF;
-    int lid = -1;
-    for (uint32_t i = ref; i < ref + cnt; ++i) {
-        Hit h;
-        C.ptests++;
-        if (bvh_prim_intersect(S.prims[i], q.ray, h) && h.t < lbh.t) { lbh = h; lid = (int)i; }
-    }
-    if (lid >= 0) {
+// leaf finished: record its first-min hit (src/bvh.cpp:205-213 + the replay
+// hit list); returns false when the hit list is full (exact DFS instead)
+PT_HD bool q_leaf_done(Query& q) {
+    if (q.lid >= 0) {
         if (q.nh == PT_REPLAY_HITS) return false;
 #pragma unroll
         for (int k = 0; k < PT_REPLAY_HITS; ++k)
-            if ((uint32_t)k == q.nh) { q.H.idx[k] = a; q.H.t[k] = lbh.t; }
+            if ((uint32_t)k == q.nh) { q.H.idx[k] = q.cand; q.H.t[k] = q.lt; }
         ++q.nh;
         // BVH result = first strict minimum; it replaces the plane hit iff strictly closer
-        if (lbh.t < q.bt) {
-            q.bt = lbh.t;
-            if (lbh.t < q.P) { q.res_t = lbh.t; q.res_id = lid; }
+        if (q.lt < q.bt) {
+            q.bt = q.lt;
+            if (q.lt < q.P) { q.res_t = q.lt; q.res_id = q.lid; }
         }
     }
     return true;
+}
+
+PT_HD void q_enter_leaf(Query& q) {
+    q.walk = R_LEAF;
+    q.li = 0u;
+    q.lt = PT_INF;
+    q.lid = -1;
 }
 
 // min of the recorded hits strictly inside (a, r) (the left subtree of a when
@@ -248,40 +283,77 @@ PT_HD uint32_t q_leaf_certain(Query& q, const Node& nd) {
     return 2u;
 }
 
-// Advance one node visit.  Precondition: phase is Q_AUX or Q_REPLAY.
-// `stk` = per-lane word memory for the pending aux nodes (set/get).
-template <class Mem>
-PT_HD void q_step(const SceneView& S, const AuxSL* aux, uint32_t n_aux, Query& q, QCounts& C, Mem& stk) {
-#ifdef PT_QDIAG
-    C.steps++;
-#endif
+// ---- step = addresses -> one batch of 8 x 16-B loads -> compute -------------
+
+// byte offsets (into S.blob) of the 8 pieces this lane's next step reads
+PT_HD void q_addr(const SceneView& S, const Query& q, uint32_t off[8]) {
     if (q.phase == Q_AUX) {
-        // one wide node: PT_AUXW child entries (independent loads)
-        AuxSL e[PT_AUXW];
+        const uint32_t b = S.o_aux + q.node * (uint32_t)(PT_AUXW * sizeof(AuxSL));
 #pragma unroll
-        for (int k = 0; k < PT_AUXW; ++k) e[k] = aux[q.node * PT_AUXW + k];
+        for (int k = 0; k < 8; ++k) off[k] = b + 16u * (uint32_t)k;
+        return;
+    }
+    uint32_t b0, b1, b2;
+    if (q.walk == R_CAND) {
+        b0 = S.o_nodes + 32u * q.cand;
+        b1 = b0 + 16u;
+        b2 = S.o_ainfo + 16u * (q.cand >> 2);     // the 16 B holding anc_info[cand]
+    } else if (q.walk == R_LEAF) {
+        const uint32_t i = q.lref + (q.li & 0x7fffffffu);
+        if (q.li & 0x80000000u) {
+            b0 = S.o_prim + 80u * i;              // full record: 5 pieces
+#pragma unroll
+            for (int k = 0; k < 8; ++k) off[k] = b0 + 16u * (uint32_t)(k < 5 ? k : 4);
+            return;
+        }
+        b0 = S.o_qprim + 48u * i;
+        b1 = b0 + 16u;
+        b2 = b0 + 32u;
+    } else if (q.walk == R_WALK_E) {
+        b0 = S.o_anc + 4u * (q.off + q.pos);      // 4 entries (lists padded to 16 B)
+        b1 = b0;
+        b2 = b0;
+    } else {
+        // R_WALK_N: the records of the 4 pending entries (none -> node 0)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t e = q.e[j] == 0xffffffffu ? 0u : q.e[j];
+            off[2 * j] = S.o_nodes + 32u * e;
+            off[2 * j + 1] = off[2 * j] + 16u;
+        }
+        return;
+    }
+    off[0] = b0; off[1] = b1; off[2] = b2;
+#pragma unroll
+    for (int k = 3; k < 8; ++k) off[k] = b0;
+}
+
+template <class Mem>
+PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r[8]) {
+    if (q.phase == Q_AUX) {
+        // one wide node: PT_AUXW child entries
         C.aux++;
         const f3 oinv = mk3(q.ray.o.x * q.inv.x, q.ray.o.y * q.inv.y, q.ray.o.z * q.inv.z);
         uint32_t next = 0xffffffffu;
 #pragma unroll
         for (int k = 0; k < PT_AUXW; ++k) {
-            const uint32_t code = f2u(e[k].b.w);
+            const F4 ea = r[2 * k], eb = r[2 * k + 1];
+            const uint32_t code = f2u(eb.w);
             if (code == 0xffffffffu) continue;
             if (code & 0x80000000u) {
                 const uint32_t leaf = code & 0x7fffffffu;
                 if (leaf < q.lb) continue;
                 Node nd;
-                nd.a = e[k].a;
-                nd.b = e[k].b;
+                nd.a = ea;
+                nd.b = eb;
                 if (node_enter(nd, q.ray, q.inv, PT_INF, q.par != 0u)) {
 #ifdef PT_QDIAG
                     C.cands++;
 #endif
                     q_insert(q, leaf);
                 }
-            } else if (q.par ? aux_box_par(e[k].a.x, e[k].a.y, e[k].a.z, e[k].a.w, e[k].b.x, e[k].b.y, q.ray, q.inv,
-                                           oinv)
-                             : aux_box(e[k].a.x, e[k].a.y, e[k].a.z, e[k].a.w, e[k].b.x, e[k].b.y, q.inv, oinv)) {
+            } else if (q.par ? aux_box_par(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, q.ray, q.inv, oinv)
+                             : aux_box(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, q.inv, oinv)) {
                 if (next == 0xffffffffu) next = code;
                 else stk.set(q.sp++, code);
             }
@@ -299,19 +371,20 @@ PT_HD void q_step(const SceneView& S, const AuxSL* aux, uint32_t n_aux, Query& q
         q_next_candidate(q);
         return;
     }
-    // Q_REPLAY.  One round of independent loads per step (the wave waits for
-    // its slowest lane's chain, so no step may chain two memory round trips).
     bool reject = false;
     if (q.walk == R_CAND) {
         // the candidate's own leaf record (+ where its ancestor list is)
-        const Node nd = S.nodes[q.cand];
-        const uint32_t info = S.anc_info[q.cand];
+        Node nd;
+        nd.a = r[0];
+        nd.b = r[1];
+        const uint32_t k4 = q.cand & 3u;
+        const uint32_t info = f2u(k4 == 0u ? r[2].x : k4 == 1u ? r[2].y : k4 == 2u ? r[2].z : r[2].w);
         C.nodes++;
         q.lref = f2u(nd.b.z);
         q.lcnt = f2u(nd.b.w);
         const uint32_t v = q_leaf_certain(q, nd);
         if (v == 1u) {
-            q.walk = R_LEAF;
+            q_enter_leaf(q);
             return;
         }
         if (v == 0u) {
@@ -322,8 +395,8 @@ PT_HD void q_step(const SceneView& S, const AuxSL* aux, uint32_t n_aux, Query& q
             // node, same bound: both depend only on earlier hits) -- they are the
             // list entries <= the hit.  Below a* no left subtree holds a hit, so
             // the bound is constant: B = min{hits in (a*, right child of a*)}.
-            // Each remaining ancestor, then the leaf itself (entry len), is
-            // tested with B.
+            // Each remaining ancestor, then the leaf itself (the list's last
+            // entry), is tested with B.
             q.off = info & 0x03ffffffu;
             q.len = info >> 26;
             q.pos = 0u;
@@ -334,22 +407,36 @@ PT_HD void q_step(const SceneView& S, const AuxSL* aux, uint32_t n_aux, Query& q
             return;
         }
     } else if (q.walk == R_LEAF) {
-        // leaf entered: its primitives (src/bvh.cpp:205-213)
-        if (!q_leaf_hit(S, q, q.cand, q.lref, q.lcnt, C)) {
+        // one primitive of the entered leaf (src/bvh.cpp:205-213: first strict min)
+        Prim pr;
+        if (q.li & 0x80000000u) {
+            pr.p0 = r[0]; pr.p1 = r[1]; pr.p2 = r[2]; pr.p3 = r[3]; pr.p4 = r[4];
+            q.li &= 0x7fffffffu;
+        } else if (f2u(r[0].w) & PT_QP_FULL) {
+            q.li |= 0x80000000u;              // not representable compactly: full record next step
+            return;
+        } else {
+            pr = qprim_expand(r[0], r[1], r[2]);
+        }
+        Hit h;
+        C.ptests++;
+        if (bvh_prim_intersect(pr, q.ray, h) && h.t < q.lt) { q.lt = h.t; q.lid = (int)(q.lref + q.li); }
+        if (++q.li < q.lcnt) return;
+        if (!q_leaf_done(q)) {
             q.phase = Q_EXACT;
             return;
         }
     } else if (q.walk == R_WALK_E) {
-        // next 4 path entries (position len is the leaf itself)
+        // next 4 list entries (ancestors, then the leaf; 0xffffffff = padding)
         uint32_t hlast = 0u;   // last recorded hit (unrolled select: no dynamic register indexing)
 #pragma unroll
         for (int k = 0; k < PT_REPLAY_HITS; ++k)
             if ((uint32_t)k + 1u == q.nh) hlast = q.H.idx[k];
         bool any = false, accept = false;
+        const uint32_t ent[4] = {f2u(r[0].x), f2u(r[0].y), f2u(r[0].z), f2u(r[0].w)};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t at = q.pos + (uint32_t)j;
-            uint32_t e = at < q.len ? S.anc[q.off + at] : (at == q.len ? q.cand : 0xffffffffu);
+            uint32_t e = q.pos + (uint32_t)j < q.len ? ent[j] : 0xffffffffu;
             if (e != 0xffffffffu && !accept && !q.known) {
                 if (e <= hlast) {
                     q.astar = e;          // entered on the last hit's path
@@ -365,32 +452,49 @@ PT_HD void q_step(const SceneView& S, const AuxSL* aux, uint32_t n_aux, Query& q
             any = any || e != 0xffffffffu;
         }
         if (accept) {
-            q.walk = R_LEAF;
+            q_enter_leaf(q);
             return;
         }
-        if (any) {
-            q.walk = R_WALK_N;
-        } else {
-            q.pos += 4u;              // all at or above a*
-        }
+        if (any) q.walk = R_WALK_N;
+        else q.pos += 4u;                // all at or above a*
         return;
     } else {
         // R_WALK_N: the records of the pending entries, tested with B
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            if (q.e[j] == 0xffffffffu || reject) continue;
+            if (q.e[j] == 0xffffffffu) continue;
+            Node nd;
+            nd.a = r[2 * j];
+            nd.b = r[2 * j + 1];
             C.nodes++;
-            if (!node_enter(S.nodes[q.e[j]], q.ray, q.inv, q.bound, q.par != 0u)) reject = true;
+            if (!node_enter(nd, q.ray, q.inv, q.bound, q.par != 0u)) reject = true;
         }
         if (!reject) {
             q.pos += 4u;
-            q.walk = q.pos > q.len ? R_LEAF : R_WALK_E;   // past the leaf: entered
+            if (q.pos >= q.len) q_enter_leaf(q);   // the leaf (last entry) was entered too
+            else q.walk = R_WALK_E;
             return;
         }
     }
     (void)reject;
     q.skip = q.cand + 1u;
     q_next_candidate(q);
+}
+
+PT_HD F4 blob_piece(const SceneView& S, uint32_t off) {
+    return *reinterpret_cast<const F4*>(reinterpret_cast<const unsigned char*>(S.blob) + off);
+}
+
+// Advance one step.  Precondition: phase is Q_AUX or Q_REPLAY.
+// `stk` = per-lane word memory for the pending aux nodes (set/get).
+template <class Mem>
+PT_HD void q_step(const SceneView& S, Query& q, QCounts& C, Mem& stk) {
+    uint32_t off[8];
+    q_addr(S, q, off);
+    F4 r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r[k] = blob_piece(S, off[k]);
+    q_exec(S, q, C, stk, r);
 }
 
 // exact stack DFS for the rays the replay leaves (planes again + bvh_exact:
@@ -410,11 +514,10 @@ PT_HD int q_exact(const SceneView& S, const Ray& ray, Stack& stk, Hit& out, QCou
 
 // whole query on one thread (host tests / reference form of the state machine)
 template <class Stack>
-PT_HD int q_run(const SceneView& S, const AuxSL* aux, uint32_t n_aux, const Ray& ray, Stack& stk, Hit& out,
-                QCounts& C, uint32_t& exact_used) {
+PT_HD int q_run(const SceneView& S, const Ray& ray, Stack& stk, Hit& out, QCounts& C, uint32_t& exact_used) {
     Query q;
     q_init(S, ray, q, C);
-    while (q.phase == Q_AUX || q.phase == Q_REPLAY) q_step(S, aux, n_aux, q, C, stk);
+    while (q.phase == Q_AUX || q.phase == Q_REPLAY) q_step(S, q, C, stk);
     exact_used = q.phase == Q_EXACT ? 1u : 0u;
     if (exact_used) return q_exact(S, ray, stk, out, C);
     if (q.res_id >= 0) {

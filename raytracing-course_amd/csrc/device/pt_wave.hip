@@ -115,9 +115,15 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
     QCounts C{0u, 0u, 0u, 0u};
     uint32_t rays = 0u, fallbacks = 0u, init_exact = 0u;
     uint64_t t_start = 0, iters = 0;
+#ifdef PT_WPROF
+    uint64_t cyc_refill = 0, cyc_step = 0, nact = 0, naux = 0;
+#endif
     if (P.wg_prof && threadIdx.x == 0) t_start = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         iters++;
+#ifdef PT_WPROF
+        const uint64_t c0 = __builtin_amdgcn_s_memtime();
+#endif
         const unsigned long long idle = __ballot(!active);
         uint32_t nidle = (uint32_t)__popcll(idle);
         if (!exhausted && (nidle >= PT_REFILL_MIN || nidle == 64u)) {
@@ -164,8 +170,16 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
             }
         }
         if (__ballot(active) == 0ull) break;
+#ifdef PT_WPROF
+        const uint64_t c1 = __builtin_amdgcn_s_memtime();
+        cyc_refill += c1 - c0;
+        const uint32_t ph = active ? (q.phase == Q_AUX ? 0u : 1u + q.walk) : 5u;
+        const unsigned long long pm = __ballot(ph == 0u) ;
+        nact += (uint64_t)__popcll(__ballot(active));
+        naux += (uint64_t)__popcll(pm);
+#endif
         if (active) {
-            if (q.phase == Q_AUX || q.phase == Q_REPLAY) q_step(P.S, P.aux, P.n_aux, q, C, stk);
+            if (q.phase == Q_AUX || q.phase == Q_REPLAY) q_step(P.S, q, C, stk);
             if (q.phase == Q_DONE) {
                 // results stay at the work index: no compaction, no atomics
                 const uint32_t k = wi;
@@ -195,6 +209,9 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
                 }
             }
         }
+#ifdef PT_WPROF
+        cyc_step += __builtin_amdgcn_s_memtime() - c1;
+#endif
     }
     wave_add_u64(P.counters + 0, rays);
     wave_add_u64(P.counters + 1, C.nodes);
@@ -206,12 +223,18 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
     if (P.wg_prof) {
         __syncthreads();
         if (threadIdx.x == 0) {
-            unsigned long long* w = P.wg_prof + 5ull * blockIdx.x;
+            unsigned long long* w = P.wg_prof + 9ull * blockIdx.x;
             w[0] = t_start;
             w[1] = __builtin_amdgcn_s_memrealtime();
             w[2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
             w[3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
             w[4] = iters;
+#ifdef PT_WPROF
+            w[5] = cyc_refill;
+            w[6] = cyc_step;
+            w[7] = nact;
+            w[8] = naux;
+#endif
         }
     }
 }

@@ -53,6 +53,7 @@ struct DevScene {
     pt::AuxSL* auxsl = nullptr;
     uint32_t* anc_info = nullptr;
     uint32_t* anc = nullptr;
+    pt::F4* blob = nullptr;
 };
 
 constexpr uint32_t kCandCap = 24;   // candidate-list words per lane (per replay pass)
@@ -73,6 +74,8 @@ struct pt_scene {
     uint32_t tree_depth = 0, max_stack = 0, aux_depth = 0, auxsl_depth = 0;
     float box_extent = 0.f;     // max |coordinate| of the reference node boxes
     std::vector<uint32_t> anc_info, anc;   // per-leaf ancestor lists (replay walk)
+    std::vector<pt::F4> blob;   // the wavefront query's fetch space (pt_core.h SceneView::blob)
+    uint32_t o_nodes = 0, o_aux = 0, o_ainfo = 0, o_anc = 0, o_qprim = 0, o_prim = 0;
     uint32_t auxw_stack = 0;    // per-lane stack words of the wide aux traversal
     float thr[256];
     std::map<int, DevScene> dev;
@@ -176,15 +179,61 @@ void build_device_layout(pt_scene* s) {
     std::vector<uint32_t> path;
     for (size_t i = 0; i < s->nodes.size(); ++i) {
         if (s->nodes[i].left != 0xFFFFFFFFu) continue;
+        // root .. parent, then the leaf itself, padded to 4 entries (16-B pieces)
         path.clear();
         for (uint32_t a = parent[i]; a != 0xFFFFFFFFu; a = parent[a]) path.push_back(a);
-        if (path.size() > 63 || s->anc.size() + path.size() >= (1u << 26))
+        if (path.size() + 1 > 63 || s->anc.size() + path.size() + 4 >= (1u << 26))
             throw std::runtime_error("BVH too deep for the ancestor lists");
-        s->anc_info[i] = (uint32_t)s->anc.size() | ((uint32_t)path.size() << 26);
+        s->anc_info[i] = (uint32_t)s->anc.size() | ((uint32_t)(path.size() + 1) << 26);
         s->anc.insert(s->anc.end(), path.rbegin(), path.rend());
+        s->anc.push_back((uint32_t)i);
+        while (s->anc.size() & 3u) s->anc.push_back(0xFFFFFFFFu);
     }
-    if (s->anc.empty()) s->anc.push_back(0u);
+    if (s->anc.empty()) s->anc.assign(4, 0xFFFFFFFFu);
     if (s->nodes.size() >= (1u << 24)) throw std::runtime_error("BVH larger than 2^24 nodes");
+}
+
+// one 16-B-aligned blob holding every array the wavefront query reads
+// (SceneView::blob; 32-bit byte offsets).  The compact primitive records
+// (pt_query.h qprim_expand) are built here.
+void build_query_blob(pt_scene* s) {
+    std::vector<pt::F4>& b = s->blob;
+    b.clear();
+    auto append = [&b](const void* p, size_t bytes) {
+        const uint32_t o = (uint32_t)(b.size() * 16);
+        const size_t n = (bytes + 15) / 16;
+        b.resize(b.size() + n, pt::F4{0.f, 0.f, 0.f, 0.f});
+        if (bytes) memcpy(&b[o / 16], p, bytes);
+        return o;
+    };
+    s->o_nodes = append(s->dnodes.data(), s->dnodes.size() * sizeof(pt::Node));
+    s->o_aux = append(s->auxsl.data(), s->auxsl.size() * sizeof(pt::AuxSL));
+    s->o_ainfo = append(s->anc_info.data(), s->anc_info.size() * 4);
+    s->o_anc = append(s->anc.data(), s->anc.size() * 4);
+    std::vector<pt::F4> qp(3 * s->dprims.size());
+    for (size_t i = 0; i < s->dprims.size(); ++i) {
+        const pt::Prim& P = s->dprims[i];
+        const uint32_t type = pt::f2u(P.p0.w);
+        const bool pos0 = pt::f2u(P.p0.x) == 0u && pt::f2u(P.p0.y) == 0u && pt::f2u(P.p0.z) == 0u;
+        const bool rot1 = pt::f2u(P.p1.x) == 0u && pt::f2u(P.p1.y) == 0u && pt::f2u(P.p1.z) == 0u &&
+                          pt::f2u(P.p1.w) == 0x3f800000u;
+        pt::F4* r = &qp[3 * i];
+        if (type == pt::T_TRIANGLE && pos0 && rot1) {
+            r[0] = pt::F4{P.p2.x, P.p2.y, P.p2.z, P.p0.w};
+            r[1] = P.p3;
+            r[2] = pt::F4{P.p4.x, P.p4.y, 0.f, 0.f};
+        } else if (type == pt::T_BOX || type == pt::T_ELLIPSOID) {
+            r[0] = pt::F4{P.p2.x, P.p2.y, P.p2.z, P.p0.w};
+            r[1] = pt::F4{P.p0.x, P.p0.y, P.p0.z, P.p1.x};
+            r[2] = pt::F4{P.p1.y, P.p1.z, P.p1.w, 0.f};
+        } else {
+            r[0] = pt::F4{0.f, 0.f, 0.f, pt::u2f(type | PT_QP_FULL)};
+            r[1] = r[2] = pt::F4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+    s->o_qprim = append(qp.data(), qp.size() * sizeof(pt::F4));
+    s->o_prim = append(s->dprims.data(), s->dprims.size() * sizeof(pt::Prim));
+    if (b.size() * 16 >= 0xFFFFFFF0ull) throw std::runtime_error("scene too large for 32-bit query offsets");
 }
 
 // ------------------------------------------------------------- devices ---
@@ -222,6 +271,7 @@ int ensure_device_scene(pt_scene* s, int dev, DevScene** out) {
     if ((rc = upload(&d.aux, s->aux))) return rc;
     if ((rc = upload(&d.auxsl, s->auxsl))) return rc;
     if ((rc = upload(&d.anc_info, s->anc_info)) || (rc = upload(&d.anc, s->anc))) return rc;
+    if ((rc = upload(&d.blob, s->blob))) return rc;
     s->dev[dev] = d;
     *out = &s->dev[dev];
     return PT_OK;
@@ -230,7 +280,7 @@ int ensure_device_scene(pt_scene* s, int dev, DevScene** out) {
 void free_device_scene(DevScene& d) {
     (void)hipFree(d.nodes); (void)hipFree(d.prims); (void)hipFree(d.shade);
     (void)hipFree(d.planes); (void)hipFree(d.emitters); (void)hipFree(d.thr); (void)hipFree(d.aux);
-    (void)hipFree(d.auxsl); (void)hipFree(d.anc_info); (void)hipFree(d.anc);
+    (void)hipFree(d.auxsl); (void)hipFree(d.anc_info); (void)hipFree(d.anc); (void)hipFree(d.blob);
 }
 
 // per-lane LDS words: replay needs [aux stack | candidates], the exact DFS its stack
@@ -244,6 +294,12 @@ uint32_t lane_words(const pt_scene* s, int traversal) {
     const pt::ReplayCfg c = replay_cfg(s);
     const uint32_t dfs = std::max<uint32_t>(s->max_stack, 1u);
     return traversal == PT_TRAVERSAL_EXACT ? dfs : std::max(dfs, c.as + c.cap);
+}
+
+void set_blob(pt::SceneView& v, const pt_scene* s, const pt::F4* blob) {
+    v.blob = blob;
+    v.o_nodes = s->o_nodes; v.o_aux = s->o_aux; v.o_ainfo = s->o_ainfo;
+    v.o_anc = s->o_anc; v.o_qprim = s->o_qprim; v.o_prim = s->o_prim;
 }
 
 pt::SceneView host_view(const pt_scene* s, int traversal) {
@@ -260,6 +316,7 @@ pt::SceneView host_view(const pt_scene* s, int traversal) {
     v.box_extent = s->box_extent;
     v.anc_info = s->anc_info.data();
     v.anc = s->anc.data();
+    set_blob(v, s, s->blob.data());
     return v;
 }
 
@@ -375,6 +432,7 @@ int pt_scene_prepare(pt_scene* s) {
         if (!std::isfinite(s->box_extent)) s->box_extent = INFINITY;   // certification then never succeeds
         pth::build_aux_bvh(s->nodes, s->aux, s->aux_depth);
         pth::build_aux_wide(s->aux, s->dnodes, PT_AUXW, s->auxsl, s->auxsl_depth, s->auxw_stack);
+        build_query_blob(s);
         pth::build_gamma_thresholds(s->thr);
     } catch (const std::exception& e) {
         return fail(PT_E_SCENE, e.what());
@@ -550,6 +608,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.S.box_extent = s->box_extent;
     wp.S.anc_info = ds.anc_info;
     wp.S.anc = ds.anc;
+    set_blob(wp.S, s, ds.blob);
     wp.aux = ds.auxsl;
     wp.n_aux = (uint32_t)s->auxsl.size();
     wp.cam = ss->cam;
@@ -589,13 +648,13 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             const char* wgp = getenv("PT_WGPROF");
             if (wgp && *wgp) {
                 // diagnostics: per-round isect workgroup timelines appended to $PT_WGPROF
-                if (!ss->wg_prof) HIP_TRY(hipMalloc(&ss->wg_prof, 40ull * ss->isect_grid));
-                HIP_TRY(hipMemsetAsync(ss->wg_prof, 0, 40ull * ss->isect_grid, ss->stream));
+                if (!ss->wg_prof) HIP_TRY(hipMalloc(&ss->wg_prof, 72ull * ss->isect_grid));
+                HIP_TRY(hipMemsetAsync(ss->wg_prof, 0, 72ull * ss->isect_grid, ss->stream));
                 wp.wg_prof = ss->wg_prof;
             }
             HIP_TRY(pt_launch_wave_round(wp, ss->isect_grid, ss->shade_grid, ss->stream));
             if (wp.wg_prof) {
-                std::vector<unsigned long long> h(5ull * ss->isect_grid);
+                std::vector<unsigned long long> h(9ull * ss->isect_grid);
                 HIP_TRY(hipMemcpyAsync(h.data(), wp.wg_prof, h.size() * 8, hipMemcpyDeviceToHost, ss->stream));
                 HIP_TRY(hipStreamSynchronize(ss->stream));
                 if (FILE* f = fopen(wgp, "ab")) {
@@ -941,7 +1000,7 @@ int pt_selftest_ray_intersection(pt_scene* s, int32_t traversal, uint32_t n, con
         if (traversal == PT_TRAVERSAL_REPLAY) {
             pt::QCounts Q{0u, 0u, 0u, 0u};
             uint32_t ex = 0;
-            id = pt::q_run(V, s->auxsl.data(), (uint32_t)s->auxsl.size(), r, stk, h, Q, ex);
+            id = pt::q_run(V, r, stk, h, Q, ex);
             if (Q.planes & 0x80000000u) return fail(PT_E_INVALID, "recomputed closest hit differs from the query's");
             C.rays++;
             C.nodes += Q.nodes; C.ptests += Q.ptests; C.planes += Q.planes; C.aux += Q.aux; C.fallbacks += ex;
@@ -996,7 +1055,7 @@ int pt_selftest_render_host(pt_scene* s, int32_t traversal, uint32_t x0, uint32_
                         auto q = [&](const pt::Ray& rr, pt::Hit& hh, pt::Counts& cc) {
                             pt::QCounts Q{};
                             uint32_t ex = 0;
-                            const int id = pt::q_run(V, s->auxsl.data(), (uint32_t)s->auxsl.size(), rr, stk, hh, Q, ex);
+                            const int id = pt::q_run(V, rr, stk, hh, Q, ex);
                             cc.fallbacks += ex;
                             if (Q.planes & 0x80000000u) cc.errs |= 4u;   // recomputed hit differs (checked below)
 #ifdef PT_QDIAG
