@@ -3,16 +3,18 @@
 
 Workload (N=1): config 3 of BASELINE.json -- the md5-pinned ~90k-triangle
 dragon stand-in (scenes/make_scene.py c3; the reference's dragon_100k file is
-missing) at 1920x1080, RAY_DEPTH 6.  One "step" = one sample for every pixel
-of the frame (the reference's spp loop advanced by one: each pixel's
-minstd_rand stream and f32 sum stay resident in HBM, so K steps are exactly
-the first K of the 256 spp).  `value` = Mray/s = closest-hit queries
-(Scene::RayIntersection calls, counted on the GPU) over the timed region.
+missing) at 1920x1080, RAY_DEPTH 6.  One "step" = `--spp-per-step` (default 4)
+samples for every pixel of the frame: the reference's spp loop advanced by
+that many (each pixel's minstd_rand stream and f32 sum stay resident in HBM,
+so K steps are exactly the first K*spp of the 256 spp).  `value` = Mray/s =
+closest-hit queries (Scene::RayIntersection calls, counted on the GPU) over
+the timed region.
 
 Multi-GPU (torchrun, one process per GPU): the frame's 16x16 tiles are dealt
-round-robin to ranks (no data-path collective); the timed region ends with
-the framebuffer resolve (tonemap on device) and an RCCL gather of the packed
-8-bit tiles to rank 0.  Total work is fixed as N grows ("strong" scaling).
+round-robin to ranks (no data-path collective) and every rank advances its
+pixels by spp-per-step x N samples per step, so the per-GPU work is fixed as N
+grows ("weak" scaling); the timed region ends with the framebuffer resolve
+(tonemap on device) and an RCCL gather of the packed 8-bit tiles to rank 0.
 
 Also reported: roofline of the dominant kernel (k_trace) from in-kernel
 counters and HIP-event launch times, and the reference CPU renderer timed on
@@ -127,7 +129,7 @@ def main():
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3")
-    ap.add_argument("--spp-per-step", type=int, default=1)
+    ap.add_argument("--spp-per-step", type=int, default=4, help="samples per pixel per step, per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, nargs=2, default=[480, 270])
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
@@ -166,8 +168,9 @@ def main():
     ss = pt.Session(scene, device=local, rank=rank, world=world, traversal=trav)
     ss.sync()
     t_ready = time.perf_counter()
+    spp = args.spp_per_step * world   # weak scaling: a rank owns 1/world of the pixels
     for _ in range(args.warmup):
-        ss.trace(args.spp_per_step)
+        ss.trace(spp)
     ss.sync()
     st0 = ss.stats()
 
@@ -175,7 +178,7 @@ def main():
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        ss.trace(args.spp_per_step)
+        ss.trace(spp)
     ss.resolve(dev_out=packed.data_ptr() if ss.packed_bytes else None)
     ss.sync()
     img = gather_tiles(dist, packed[: ss.packed_bytes], rank, world, W, H, device)
@@ -203,18 +206,23 @@ def main():
     if rank == 0:
         T = float(tmax[0])
         total_rays = float(tsum[1])
-        # roofline of k_trace: algorithmic bytes per launch / mean launch time (rank 0's launches)
-        launches = args.steps
+        # roofline of the dominant kernel (k_wisect, the closest-hit query): algorithmic bytes
+        # per launch / mean launch time, both from rank 0; launch times are HIP events
+        # recorded around each k_wisect launch on the session's stream
+        launches = max(st1["isect_launches"] - st0["isect_launches"], 1)
+        isect_ms = st1["isect_ms"] - st0["isect_ms"]
         alg_bytes = (nodes * st1["node_bytes"] + ptests * st1["prim_bytes"] + auxv * st1["aux_bytes"]) / launches
-        launch_s = (kms / 1e3) / launches
+        launch_s = (isect_ms / 1e3) / launches
         achieved = alg_bytes / launch_s / 1e9 if launch_s > 0 else 0.0
         traffic = None
         traffic_src = None
         if os.path.exists(args.traffic_json):
             try:
                 tj = json.load(open(args.traffic_json))
-                key = "%s_spp%d_n%d" % (args.config, args.spp_per_step, world)
+                key = "%s_spp%d_n%d" % (args.config, spp, world)
                 if key in tj:
+                    # profiled per-launch fabric bytes x (this run's launches / the profile's):
+                    # kept per launch like `achieved`
                     traffic = tj[key]["hbm_bytes_per_launch"]
                     traffic_src = tj[key].get("source")
             except Exception:
@@ -228,24 +236,27 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": T * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: md5-pinned 89,928-triangle dragon stand-in (SURVEY §8d), per-pixel reference seeds",
             "config": {"workload": "config 3: %s %dx%d, %d spp per step (of 256), RAY_DEPTH %d; %s traversal of the "
-                                   "reference tree (bit-exact)" % (args.config, W, H, args.spp_per_step,
+                                   "reference tree (bit-exact)" % (args.config, W, H, spp,
                                                                    info["ray_depth"], args.traversal),
-                       "pixels": W * H, "samples_per_step": W * H * args.spp_per_step,
+                       "pixels": W * H, "samples_per_step": W * H * spp,
                        "parallelism": "pixel tiles x%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_trace", "alg_bytes_per_launch": alg_bytes, "launch_ms": launch_s * 1e3,
-                         "traffic_source": traffic_src,
-                         "note": "algorithmic = reference node records (32 B) + aux BVH nodes (64 B) + leaf "
-                                 "primitive records (80 B) fetched; the ~24 MB working set is L2/MALL-resident, "
-                                 "so DRAM traffic << algorithmic"},
+                         "kernel": "k_wisect", "alg_bytes_per_launch": alg_bytes, "launch_ms": launch_s * 1e3,
+                         "launches": launches, "traffic_source": traffic_src,
+                         "note": "algorithmic = 4-wide aux BVH nodes (128 B) + reference node records (32 B) + "
+                                 "compact primitive records (48 B) per visit; the ~25 MB working set is "
+                                 "L2/Infinity-Cache resident, and the kernel is bound by dependent-load latency, "
+                                 "not bandwidth (DESIGN.md §4)"},
+            "wavefront_rounds": int(st1["rounds"] - st0["rounds"]),
+            "kernel_ms_per_step": kms / args.steps,
             "rays": total_rays,
-            "msamples_per_s": W * H * args.spp_per_step * args.steps / T / 1e6,
+            "msamples_per_s": W * H * spp * args.steps / T / 1e6,
             "node_visits_per_ray": float(tsum[2]) / max(total_rays, 1),
             "aux_visits_per_ray": float(tsum[6]) / max(total_rays, 1),
             "fallback_rate": float(tsum[7]) / max(total_rays, 1),
@@ -254,7 +265,7 @@ def main():
             "wall": {"load_s": t_prep - t_load, "prepare_bvh_s": t_sess - t_prep, "session_upload_s": t_ready - t_sess},
             "framebuffer_gathered": img is not None and img.shape == (H, W, 3),
         }
-        res["projected_c3_render_s"] = (256.0 / (args.spp_per_step * args.steps)) * T
+        res["projected_c3_render_s"] = (256.0 / (spp * args.steps)) * T
         if world == 1 and not args.no_cpu_baseline:
             try:
                 res["cpu_baseline"] = cpu_baseline(pt, args)

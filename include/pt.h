@@ -112,6 +112,9 @@ typedef struct pt_stats {
     uint64_t prim_bytes;
     uint64_t aux_bytes;
     uint64_t fallbacks_ray;  /* of `fallbacks`: rays with non-finite origin/direction (exact DFS by design) */
+    double isect_ms;         /* wavefront engine: time of the closest-hit kernel launches (HIP events) */
+    uint64_t isect_launches;
+    uint64_t rounds;         /* wavefront rounds run */
 } pt_stats;
 
 /* Scene::Render minus the stream write: renders W*H*3 u8 (row-major, top row

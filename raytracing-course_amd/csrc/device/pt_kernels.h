@@ -49,7 +49,8 @@ struct TraceParams {
 // ---- wavefront renderer (pt_wave.hip) ----------------------------------
 struct RayQ {                     // rays waiting for a closest-hit query
     F4* ro;                       // {o.xyz, u32 slot}
-    F4* rd;                       // {d.xyz, -}
+    F4* rd;                       // {d.xyz, P = closest plane t (computed by the producer)}
+    int* pid;                     // the closest plane's prim (-1 none)
 };
 struct DoneQ {                    // finished queries, input of the shade kernel
     F4* ro;                       // {o.xyz, u32 slot}
@@ -105,5 +106,7 @@ hipError_t pt_launch_trace(const pt::TraceParams& p, int variant, uint32_t lds_b
 // wavefront pipeline (pt_wave.hip): start a pass (first camera ray of every
 // owned pixel), then rounds of {closest-hit, exact, shade}
 hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s);
-hipError_t pt_launch_wave_round(pt::WaveParams p, uint32_t isect_grid, uint32_t shade_grid, hipStream_t s);
+// e0/e1 (optional): events recorded around the k_wisect launch (its time for the roofline)
+hipError_t pt_launch_wave_round(pt::WaveParams p, uint32_t isect_grid, uint32_t shade_grid, hipStream_t s,
+                                hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t pt_launch_resolve(const pt::ResolveParams& p, uint32_t n_tiles, hipStream_t s);

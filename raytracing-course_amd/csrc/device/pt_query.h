@@ -126,17 +126,25 @@ struct QCounts {
 };
 
 // planes (src/scene.cpp:50-57), then the BVH set-up
-PT_HD void q_init(const SceneView& S, const Ray& ray, Query& q, QCounts& C) {
-    q.ray = ray;
-    q.res_id = -1;
-    q.res_t = PT_INF;
-    float closest = PT_INF;
+// the planes part of RayIntersection (src/scene.cpp:50-57): closest plane t and
+// its prim (-1 none).  Run by the ray's producer (camera / shade kernels), so
+// the query kernel starts at the BVH.
+PT_HD void q_planes(const SceneView& S, const Ray& ray, float& P, int& pid) {
+    P = PT_INF;
+    pid = -1;
     for (uint32_t k = 0; k < S.n_planes; ++k) {
         const uint32_t pi = S.planes[k];
         Hit h;
-        C.planes++;
-        if (plane_intersect(S.prims[pi], ray, h) && h.t < closest) { closest = h.t; q.res_t = h.t; q.res_id = (int)pi; }
+        if (plane_intersect(S.prims[pi], ray, h) && h.t < P) { P = h.t; pid = (int)pi; }
     }
+}
+
+// BVH query set-up for a ray whose plane result (P, pid) is known
+PT_HD void q_init(const SceneView& S, const Ray& ray, float P, int pid, Query& q) {
+    q.ray = ray;
+    q.res_id = pid;
+    q.res_t = P;
+    const float closest = P;
     q.P = closest;
     q.bt = PT_INF;
     q.nh = 0;
@@ -279,6 +287,21 @@ PT_HD uint32_t q_leaf_certain(Query& q, const Node& nd) {
     q.mc = m;
     q.robust = (!q.par && t1 + m <= t2 - m && t2 - m >= 0.f) ? 1u : 0u;
     if (q.robust && lo >= t1 + m) return 1u;
+    // certain reject: node_enter's decisions on the same quotients (exact division when close)
+    if (!q.par) {
+        const float e1 = fabsf(t1) * 0x1p-20f + 1e-30f, e2 = fabsf(t2) * 0x1p-20f + 1e-30f;
+        const float d12 = t1 - t2;
+        if (e1 < 1e20f && e2 < 1e20f && fabsf(d12) > 2.f * (e1 + e2)) {
+            if (d12 > 0.f) return 0u;                                 // slab miss
+            if (fabsf(t2) > e2 && t2 < 0.f) return 0u;                // box behind the ray
+            if (fabsf(t2) > e2 && fabsf(t1) > e1 && t1 > 0.f) {
+                const float eb = 2.f * e1 + fabsf(hi) * 0x1p-22f;
+                if (fabsf(hi - t1) > eb) return hi < t1 ? 0u : 2u;    // pruned even against hi
+            } else if (fabsf(t2) > e2 && fabsf(t1) > e1) {
+                return 2u;                                            // interior: never pruned
+            }
+        }
+    }
     if (!node_enter(nd, q.ray, q.inv, hi, q.par != 0u)) return 0u;
     return 2u;
 }
@@ -339,23 +362,24 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
         for (int k = 0; k < PT_AUXW; ++k) {
             const F4 ea = r[2 * k], eb = r[2 * k + 1];
             const uint32_t code = f2u(eb.w);
-            if (code == 0xffffffffu) continue;
+            // every entry's box is conservative: a reference leaf passing it is a
+            // candidate (its exact slab test runs in the candidate step -- a leaf
+            // failing that test is never entered, src/bvh.cpp:188-198)
+            const bool hit = code != 0xffffffffu &&
+                             (q.par ? aux_box_par(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, q.ray, q.inv, oinv)
+                                    : aux_box(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, q.inv, oinv));
+            if (!hit) continue;
             if (code & 0x80000000u) {
                 const uint32_t leaf = code & 0x7fffffffu;
                 if (leaf < q.lb) continue;
-                Node nd;
-                nd.a = ea;
-                nd.b = eb;
-                if (node_enter(nd, q.ray, q.inv, PT_INF, q.par != 0u)) {
 #ifdef PT_QDIAG
-                    C.cands++;
+                C.cands++;
 #endif
-                    q_insert(q, leaf);
-                }
-            } else if (q.par ? aux_box_par(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, q.ray, q.inv, oinv)
-                             : aux_box(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, q.inv, oinv)) {
-                if (next == 0xffffffffu) next = code;
-                else stk.set(q.sp++, code);
+                q_insert(q, leaf);
+            } else if (next == 0xffffffffu) {
+                next = code;
+            } else {
+                stk.set(q.sp++, code);
             }
         }
         if (next == 0xffffffffu && q.sp > 0u) next = stk.get(--q.sp);
@@ -408,19 +432,29 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
         }
     } else if (q.walk == R_LEAF) {
         // one primitive of the entered leaf (src/bvh.cpp:205-213: first strict min)
-        Prim pr;
+        Hit h;
+        bool ok;
         if (q.li & 0x80000000u) {
+            Prim pr;
             pr.p0 = r[0]; pr.p1 = r[1]; pr.p2 = r[2]; pr.p3 = r[3]; pr.p4 = r[4];
             q.li &= 0x7fffffffu;
+            ok = bvh_prim_intersect(pr, q.ray, h);
         } else if (f2u(r[0].w) & PT_QP_FULL) {
             q.li |= 0x80000000u;              // not representable compactly: full record next step
             return;
+        } else if (f2u(r[0].w) == T_TRIANGLE) {
+            // plain triangle (pos = +0, identity rotation): the world->local rotation
+            // changes at most the sign of zero components, which changes neither the
+            // accept decision nor t (a signed zero only matters in a sum that is
+            // exactly zero, where every compare here is false either way); the
+            // consumer recomputes n with the full transform
+            ok = isect_triangle(q.ray, mk3(r[0].x, r[0].y, r[0].z), mk3(r[1].x, r[1].y, r[1].z),
+                                mk3(r[1].w, r[2].x, r[2].y), h);
         } else {
-            pr = qprim_expand(r[0], r[1], r[2]);
+            ok = bvh_prim_intersect(qprim_expand(r[0], r[1], r[2]), q.ray, h);
         }
-        Hit h;
         C.ptests++;
-        if (bvh_prim_intersect(pr, q.ray, h) && h.t < q.lt) { q.lt = h.t; q.lid = (int)(q.lref + q.li); }
+        if (ok && h.t < q.lt) { q.lt = h.t; q.lid = (int)(q.lref + q.li); }
         if (++q.li < q.lcnt) return;
         if (!q_leaf_done(q)) {
             q.phase = Q_EXACT;
@@ -516,7 +550,11 @@ PT_HD int q_exact(const SceneView& S, const Ray& ray, Stack& stk, Hit& out, QCou
 template <class Stack>
 PT_HD int q_run(const SceneView& S, const Ray& ray, Stack& stk, Hit& out, QCounts& C, uint32_t& exact_used) {
     Query q;
-    q_init(S, ray, q, C);
+    float P;
+    int pid;
+    q_planes(S, ray, P, pid);
+    C.planes += S.n_planes;
+    q_init(S, ray, P, pid, q);
     while (q.phase == Q_AUX || q.phase == Q_REPLAY) q_step(S, q, C, stk);
     exact_used = q.phase == Q_EXACT ? 1u : 0u;
     if (exact_used) return q_exact(S, ray, stk, out, C);

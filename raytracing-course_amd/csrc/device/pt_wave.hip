@@ -50,6 +50,17 @@ __device__ __forceinline__ void slot_xy(const TileMap& tm, uint32_t slot, uint32
     slot_pixel(tm, slot >> 8, slot & 255u, x, y);
 }
 
+// enqueue a fresh ray with its plane result (RayIntersection's plane loop)
+__device__ __forceinline__ void push_ray(const WaveParams& P, const RayQ& Q, uint32_t qi, const Ray& ray,
+                                         uint32_t slot) {
+    float pt;
+    int pid;
+    q_planes(P.S, ray, pt, pid);
+    Q.ro[qi] = F4{ray.o.x, ray.o.y, ray.o.z, u2f(slot)};
+    Q.rd[qi] = F4{ray.d.x, ray.d.y, ray.d.z, pt};
+    Q.pid[qi] = pid;
+}
+
 // src/scene.cpp:193-196: one sample's jitter draws and camera ray
 __device__ __forceinline__ Ray camera_sample(const CamView& cam, Rng& R, uint32_t x, uint32_t y) {
     const float fx = (float)x + rng_uniform(R);
@@ -86,12 +97,12 @@ __global__ void __launch_bounds__(256) k_wcamera(WaveParams P) {
     }
     uint32_t* ctl = P.ctl + 8u * P.parity;
     const uint32_t qi = wave_append(ctl + C_FRESH, want);
-    if (want) {
-        P.fq[P.parity].ro[qi] = F4{ray.o.x, ray.o.y, ray.o.z, u2f(slot)};
-        P.fq[P.parity].rd[qi] = F4{ray.d.x, ray.d.y, ray.d.z, 0.f};
-    }
+    if (want) push_ray(P, P.fq[P.parity], qi, ray, slot);
 }
 
+#ifndef PT_VOTE
+#define PT_VOTE 0
+#endif
 #define PT_SUSPENDED 0xfffffffeu   // done.id of a query suspended to the next round
 #define PT_BATCH 64u
 #define PT_REFILL_MIN 16u
@@ -156,7 +167,8 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
                     ray.d = mk3(d.x, d.y, d.z);
                     slot = f2u(o.w);
                     rays++;
-                    q_init(P.S, ray, q, C);
+                    C.planes += P.S.n_planes;
+                    q_init(P.S, ray, d.w, FQ.pid[wi], q);
                     if (q.phase == Q_EXACT) init_exact++;
                 } else {
                     // resume a suspended query: state, slot, then its aux stack into LDS
@@ -178,8 +190,22 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
         nact += (uint64_t)__popcll(__ballot(active));
         naux += (uint64_t)__popcll(pm);
 #endif
+        // phase vote: the step code of one phase kind per trip (the kinds' code
+        // paths would otherwise all be issued every trip); lanes of other kinds wait
+        const uint32_t kind = !active ? 7u : q.phase == Q_AUX ? 0u : q.phase == Q_REPLAY ? 1u + q.walk : 6u;
+        uint32_t pick = 6u;
+#if PT_VOTE
+        {
+            uint32_t best = 0u;
+#pragma unroll
+            for (uint32_t k = 0; k < 5u; ++k) {
+                const uint32_t c = (uint32_t)__popcll(__ballot(kind == k));
+                if (c > best) { best = c; pick = k; }
+            }
+        }
+#endif
         if (active) {
-            if (q.phase == Q_AUX || q.phase == Q_REPLAY) q_step(P.S, q, C, stk);
+            if ((q.phase == Q_AUX || q.phase == Q_REPLAY) && (!PT_VOTE || kind == pick)) q_step(P.S, q, C, stk);
             if (q.phase == Q_DONE) {
                 // results stay at the work index: no compaction, no atomics
                 const uint32_t k = wi;
@@ -329,10 +355,7 @@ __global__ void __launch_bounds__(256) k_wshade(WaveParams P) {
             store_rng(P.st, slot, R);
         }
         const uint32_t qn = wave_append(out + C_FRESH, emit);
-        if (emit) {
-            N.ro[qn] = F4{ray.o.x, ray.o.y, ray.o.z, u2f(slot)};
-            N.rd[qn] = F4{ray.d.x, ray.d.y, ray.d.z, 0.f};
-        }
+        if (emit) push_ray(P, N, qn, ray, slot);
     }
 }
 
@@ -347,10 +370,13 @@ hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t pt_launch_wave_round(pt::WaveParams p, uint32_t isect_grid, uint32_t shade_grid, hipStream_t s) {
+hipError_t pt_launch_wave_round(pt::WaveParams p, uint32_t isect_grid, uint32_t shade_grid, hipStream_t s,
+                                hipEvent_t e0, hipEvent_t e1) {
     hipError_t e = hipMemsetAsync(p.ctl + 8u * (1u - p.parity), 0, 4u * 8u, s);
     if (e != hipSuccess) return e;
+    if (e0 && (e = hipEventRecord(e0, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(pt::k_wisect, dim3(isect_grid), dim3(256), 1024u * p.aux_stack, s, p);
+    if (e1 && (e = hipEventRecord(e1, s)) != hipSuccess) return e;
     const uint32_t exact_lds = 64u * 4u * (p.max_stack ? p.max_stack : 1u);
     hipLaunchKernelGGL(pt::k_wexact, dim3(64), dim3(64), exact_lds, s, p);
     hipLaunchKernelGGL(pt::k_wshade, dim3(shade_grid), dim3(256), 0, s, p);

@@ -99,14 +99,16 @@ struct pt_session {
     uint32_t* nsamp = nullptr;    // samples completed per slot
     pt::F4* qbuf = nullptr;       // 8 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd
     uint32_t* hid = nullptr;      // n_slots (done.id)
+    uint32_t* pidbuf = nullptr;   // 2 * n_slots (fresh queues' plane prims)
     uint32_t* carry = nullptr;    // 2 * carry_cap * carry_words
     uint32_t carry_cap = 0, carry_words = 0, straggler_steps = 64;
     uint32_t* ctl = nullptr;      // 2 x 8 round counters
     uint32_t* ctl_host = nullptr; // pinned copy of one counter set
     uint32_t isect_grid = 0, shade_grid = 0, rounds = 0;
     hipStream_t stream = nullptr;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
-    double kernel_ms = 0.0, resolve_ms = 0.0;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, pending_isect;
+    double kernel_ms = 0.0, resolve_ms = 0.0, isect_ms = 0.0;
+    uint64_t isect_launches = 0;
     uint64_t samples_done = 0;
     pt::CamView cam{};
     int traversal = PT_TRAVERSAL_REPLAY;
@@ -343,6 +345,13 @@ int finish_pending(pt_session* ss) {
         (void)hipEventDestroy(e.second);
     }
     ss->pending.clear();
+    for (auto& e : ss->pending_isect) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) ss->isect_ms += ms;
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+    }
+    ss->pending_isect.clear();
     return PT_OK;
 }
 
@@ -556,6 +565,7 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         if (const char* g = getenv("PT_STRAGGLER")) ss->straggler_steps = (uint32_t)std::max(1, atoi(g));
         if (hipMalloc(&ss->pstate, n * 4) != hipSuccess || hipMalloc(&ss->qbuf, 8 * n * 16) != hipSuccess ||
             hipMalloc(&ss->hid, n * 4) != hipSuccess || hipMalloc(&ss->nsamp, n * 4) != hipSuccess ||
+            hipMalloc(&ss->pidbuf, 2 * n * 4) != hipSuccess ||
             hipMalloc(&ss->carry, 2ull * ss->carry_cap * ss->carry_words * 4) != hipSuccess ||
             hipMalloc(&ss->ctl, 64) != hipSuccess || hipHostMalloc(&ss->ctl_host, 64) != hipSuccess)
             return cleanup(fail(PT_E_OOM, "device allocation failed (wavefront buffers)"));
@@ -618,10 +628,10 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.pstate = ss->pstate;
     wp.nsamp = ss->nsamp;
     const size_t n = std::max<size_t>(ss->n_slots, 1);
-    wp.fq[0] = pt::RayQ{ss->qbuf, ss->qbuf + n};
-    wp.fq[1] = pt::RayQ{ss->qbuf + 2 * n, ss->qbuf + 3 * n};
+    wp.fq[0] = pt::RayQ{ss->qbuf, ss->qbuf + n, reinterpret_cast<int*>(ss->pidbuf)};
+    wp.fq[1] = pt::RayQ{ss->qbuf + 2 * n, ss->qbuf + 3 * n, reinterpret_cast<int*>(ss->pidbuf) + n};
     wp.done = pt::DoneQ{ss->qbuf + 4 * n, ss->qbuf + 5 * n, ss->hid};
-    wp.ex = pt::RayQ{ss->qbuf + 6 * n, ss->qbuf + 7 * n};
+    wp.ex = pt::RayQ{ss->qbuf + 6 * n, ss->qbuf + 7 * n, nullptr};
     wp.cq[0] = ss->carry;
     wp.cq[1] = ss->carry + (size_t)ss->carry_cap * ss->carry_words;
     wp.carry_cap = ss->carry_cap;
@@ -652,7 +662,12 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 HIP_TRY(hipMemsetAsync(ss->wg_prof, 0, 72ull * ss->isect_grid, ss->stream));
                 wp.wg_prof = ss->wg_prof;
             }
-            HIP_TRY(pt_launch_wave_round(wp, ss->isect_grid, ss->shade_grid, ss->stream));
+            hipEvent_t i0, i1;
+            HIP_TRY(hipEventCreate(&i0));
+            HIP_TRY(hipEventCreate(&i1));
+            ss->pending_isect.emplace_back(i0, i1);
+            ss->isect_launches++;
+            HIP_TRY(pt_launch_wave_round(wp, ss->isect_grid, ss->shade_grid, ss->stream, i0, i1));
             if (wp.wg_prof) {
                 std::vector<unsigned long long> h(9ull * ss->isect_grid);
                 HIP_TRY(hipMemcpyAsync(h.data(), wp.wg_prof, h.size() * 8, hipMemcpyDeviceToHost, ss->stream));
@@ -810,7 +825,13 @@ int pt_session_stats(pt_session* ss, pt_stats* st) {
     st->resolve_ms = ss->resolve_ms;
     st->node_bytes = sizeof(pt::Node);
     st->prim_bytes = sizeof(pt::Prim);
-    st->aux_bytes = ss->wave ? sizeof(pt::AuxSL) : sizeof(pt::AuxNode);
+    // algorithmic bytes per counted unit: wavefront query = 4-wide aux node (128 B),
+    // reference node record (32 B), compact primitive record (48 B)
+    st->aux_bytes = ss->wave ? PT_AUXW * sizeof(pt::AuxSL) : sizeof(pt::AuxNode);
+    if (ss->wave) st->prim_bytes = 48;
+    st->isect_ms = ss->isect_ms;
+    st->isect_launches = ss->isect_launches;
+    st->rounds = ss->rounds;
     return PT_OK;
 }
 
@@ -824,7 +845,7 @@ void pt_session_free(pt_session* ss) {
     (void)hipFree(ss->st.rng_x); (void)hipFree(ss->st.rng_saved); (void)hipFree(ss->st.rng_flag);
     (void)hipFree(ss->st.sum); (void)hipFree(ss->vscratch); (void)hipFree(ss->counters);
     (void)hipFree(ss->out); (void)hipFree(ss->rad); (void)hipFree(ss->wg_prof);
-    (void)hipFree(ss->pstate); (void)hipFree(ss->qbuf); (void)hipFree(ss->hid); (void)hipFree(ss->nsamp);
+    (void)hipFree(ss->pstate); (void)hipFree(ss->qbuf); (void)hipFree(ss->hid); (void)hipFree(ss->nsamp); (void)hipFree(ss->pidbuf);
     (void)hipFree(ss->carry); (void)hipFree(ss->ctl);
     if (ss->ctl_host) (void)hipHostFree(ss->ctl_host);
     if (ss->stream) (void)hipStreamDestroy(ss->stream);
@@ -942,7 +963,10 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
         agg.rays += st.rays; agg.node_visits += st.node_visits; agg.prim_tests += st.prim_tests;
         agg.plane_tests += st.plane_tests; agg.samples += st.samples; agg.errors += st.errors;
         agg.aux_visits += st.aux_visits; agg.fallbacks += st.fallbacks;
-        agg.fallbacks_ray += st.fallbacks_ray; agg.aux_bytes = st.aux_bytes;
+        agg.fallbacks_ray += st.fallbacks_ray;
+        agg.isect_ms = std::max(agg.isect_ms, st.isect_ms);
+        agg.isect_launches += st.isect_launches;
+        agg.rounds += st.rounds; agg.aux_bytes = st.aux_bytes;
         agg.kernel_ms = std::max(agg.kernel_ms, st.kernel_ms);
         agg.resolve_ms = std::max(agg.resolve_ms, st.resolve_ms);
         agg.node_bytes = st.node_bytes; agg.prim_bytes = st.prim_bytes;

@@ -252,8 +252,8 @@ namespace pth {
 // pair tree collapsed greedily (the child with the largest box area is
 // replaced by its two children until W children or only leaves remain).
 // Node n = entries [n*W, n*W + W) in the AuxSL layout; entry code:
-// internal child node index, 0x80000000 | reference leaf (box = the leaf's
-// exact center/half-size record), or 0xffffffff (empty).
+// internal child node index, 0x80000000 | reference leaf, or 0xffffffff
+// (empty); every box is the conservative inflated box of its subtree.
 void build_aux_wide(const std::vector<pt::AuxNode>& pairs, const std::vector<pt::Node>& dnodes, uint32_t W,
                     std::vector<pt::AuxSL>& out, uint32_t& max_depth, uint32_t& max_stack) {
     struct Ch { uint32_t code; float lo[3], hi[3]; };
@@ -303,8 +303,10 @@ void build_aux_wide(const std::vector<pt::AuxNode>& pairs, const std::vector<pt:
             if (k >= ch.size()) {
                 u[7] = 0xFFFFFFFFu;
             } else if (ch[k].code & 0x80000000u) {
-                const pt::Node& r = dnodes[ch[k].code & 0x7fffffffu];
-                f[0] = r.a.x; f[1] = r.a.y; f[2] = r.a.z; f[3] = r.a.w; f[4] = r.b.x; f[5] = r.b.y;
+                // reference leaf: its inflated (conservative) box, like an internal child;
+                // the exact test of the leaf record happens in the replay's candidate step
+                f[0] = ch[k].lo[0]; f[1] = ch[k].lo[1]; f[2] = ch[k].lo[2];
+                f[3] = ch[k].hi[0]; f[4] = ch[k].hi[1]; f[5] = ch[k].hi[2];
                 u[7] = ch[k].code;
             } else {
                 f[0] = ch[k].lo[0]; f[1] = ch[k].lo[1]; f[2] = ch[k].lo[2];

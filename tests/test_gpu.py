@@ -133,3 +133,23 @@ def test_cli_drop_in_config1(pt, tmp_path):
     assert r.returncode == 0, r.stderr
     assert "Loading: [ ########## 100% ]" in r.stdout
     assert U.md5(out.read_bytes()) == M["full"]["c1"]["md5"]
+
+
+@pytest.mark.parametrize("straggler", ["1", "3"])
+@pytest.mark.parametrize("name", ["c3s4_win_944_520_16x16", "c4glass_s4_win_900_560_16x16", "dragon_64x64x16",
+                                  "hw3s4_48x48x8"])
+def test_suspended_queries_resume_bit_exact(pt, name, straggler, monkeypatch):
+    """Force the wavefront engine to suspend almost every query after 1-3 steps
+    past its wave's last fetch (PT_STRAGGLER, read at session creation): queries
+    then resume from the carry queue over many rounds, interleaving pixels'
+    samples arbitrarily -- results must not change."""
+    monkeypatch.setenv("PT_STRAGGLER", straggler)
+    m, img, rad = U.golden_image(name)
+    with pt.Scene.load(U.golden_scene_path(name)) as s:
+        s.prepare()
+        win = tuple(m["window"]) if m["window"] else None
+        rgb, r, st = s.render(radiance=True, window=win, traversal=0)
+    assert st["errors"] == 0
+    assert st["rounds"] > 0
+    assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
+    assert np.array_equal(rgb, img)
