@@ -115,6 +115,7 @@ typedef struct pt_stats {
     double isect_ms;         /* wavefront engine: time of the closest-hit kernel launches (HIP events) */
     uint64_t isect_launches;
     uint64_t rounds;         /* wavefront rounds run */
+    uint64_t gather_rccl;    /* 1: the multi-GPU framebuffer was gathered with RCCL (ncclGather over xGMI) */
 } pt_stats;
 
 /* Scene::Render minus the stream write: renders W*H*3 u8 (row-major, top row

@@ -177,41 +177,52 @@ PT_HD bool node_slab(const Node& nd, const Ray& ray, float& t, uint32_t& interio
 // (slab()).  Requires replay_ok_ray(ray) (finite, non-tiny d: |rinv| < 1e30).
 // Returns true iff the node is entered (hit and not pruned).
 // exact = true: always the IEEE-division form (rays with near-zero direction components).
-PT_HD bool node_enter(const Node& nd, const Ray& ray, f3 rinv, float bound, bool exact = false) {
-    const f3 c = mk3(nd.a.x, nd.a.y, nd.a.z);
-    const f3 s = mk3(nd.a.w, nd.b.x, nd.b.y);
+// approximate slab interval of a (center, half-size) box: the reference's
+// numerators (same IEEE ops) times the per-ray reciprocal
+PT_HD void slab_approx(F4 a, F4 b, const Ray& ray, f3 rinv, float& t1, float& t2) {
+    const f3 c = mk3(a.x, a.y, a.z);
+    const f3 s = mk3(a.w, b.x, b.y);
     const f3 o = ray.o + -1.f * c;                 // src/bvh.cpp:92 (same IEEE adds)
     const f3 nlo = -1.f * s - o, nhi = s - o;      // src/primitives.cpp:71-72 numerators
     const float ax = nlo.x * rinv.x, bx = nhi.x * rinv.x;
     const float ay = nlo.y * rinv.y, by = nhi.y * rinv.y;
     const float az = nlo.z * rinv.z, bz = nhi.z * rinv.z;
-    const float t1 = smax(smax(smin(ax, bx), smin(ay, by)), smin(az, bz));
-    const float t2 = smin(smin(smax(ax, bx), smax(ay, by)), smax(az, bz));
+    t1 = smax(smax(smin(ax, bx), smin(ay, by)), smin(az, bz));
+    t2 = smin(smin(smax(ax, bx), smax(ay, by)), smax(az, bz));
+}
+
+// node_enter's decision from the approximate interval: 0 = not entered,
+// 1 = entered, 2 = too close to call (redo with the exact division)
+PT_HD uint32_t enter_decide(float t1, float t2, float bound) {
     const float e1 = fabsf(t1) * 0x1p-20f + 1e-30f, e2 = fabsf(t2) * 0x1p-20f + 1e-30f;
-    const float m12 = 2.f * (e1 + e2);
     const float d12 = t1 - t2;
-    // certain outcomes (every comparison separated by more than its error margin)
-    bool amb = exact || !(e1 < 1e20f && e2 < 1e20f) || !(fabsf(d12) > m12);
-    bool enter = false;
-    if (!amb) {
-        if (d12 > 0.f) return false;                            // t1 > t2: miss
-        if (!(fabsf(t2) > e2)) amb = true;
-        else if (t2 < 0.f) return false;                        // box behind the ray
-        else if (!(fabsf(t1) > e1)) amb = true;
-        else if (t1 < 0.f) return true;                         // interior: never pruned
-        else {
-            const float eb = 2.f * e1 + fabsf(bound) * 0x1p-22f;
-            if (!(fabsf(bound - t1) > eb)) amb = true;
-            else enter = !(bound < t1);
-        }
-    }
-    if (amb) {
-        float t;
-        uint32_t in;
-        if (!slab(o, ray.d, s, t, in)) return false;
-        return !(bound < t && !in);
-    }
-    return enter;
+    if (!(e1 < 1e20f && e2 < 1e20f) || !(fabsf(d12) > 2.f * (e1 + e2))) return 2u;
+    if (d12 > 0.f) return 0u;                                   // t1 > t2: miss
+    if (!(fabsf(t2) > e2)) return 2u;
+    if (t2 < 0.f) return 0u;                                    // box behind the ray
+    if (!(fabsf(t1) > e1)) return 2u;
+    if (t1 < 0.f) return 1u;                                    // interior: never pruned
+    const float eb = 2.f * e1 + fabsf(bound) * 0x1p-22f;
+    if (!(fabsf(bound - t1) > eb)) return 2u;
+    return bound < t1 ? 0u : 1u;
+}
+
+// the exact decision (IEEE division, the reference's slab)
+PT_HD bool enter_exact(F4 a, F4 b, const Ray& ray, float bound) {
+    const f3 c = mk3(a.x, a.y, a.z);
+    const f3 s = mk3(a.w, b.x, b.y);
+    float t;
+    uint32_t in;
+    if (!slab(ray.o + -1.f * c, ray.d, s, t, in)) return false;
+    return !(bound < t && !in);
+}
+
+PT_HD bool node_enter(const Node& nd, const Ray& ray, f3 rinv, float bound, bool exact = false) {
+    float t1, t2;
+    slab_approx(nd.a, nd.b, ray, rinv, t1, t2);
+    const uint32_t v = exact ? 2u : enter_decide(t1, t2, bound);
+    if (v == 2u) return enter_exact(nd.a, nd.b, ray, bound);
+    return v == 1u;
 }
 
 // conservative inflated-box test for rays with near-zero direction components

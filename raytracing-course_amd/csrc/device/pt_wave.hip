@@ -104,8 +104,12 @@ __global__ void __launch_bounds__(256) k_wcamera(WaveParams P) {
 #define PT_VOTE 0
 #endif
 #define PT_SUSPENDED 0xfffffffeu   // done.id of a query suspended to the next round
-#define PT_BATCH 64u
-#define PT_REFILL_MIN 16u
+#ifndef PT_BATCH
+#define PT_BATCH 64u        // queue indices a wave takes per atomic
+#endif
+#ifndef PT_REFILL_MIN
+#define PT_REFILL_MIN 4u    // idle lanes before a wave refills
+#endif
 
 __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
     extern __shared__ uint32_t lds_stack[];

@@ -5,6 +5,7 @@
 #include "pt.h"
 
 #include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
 #include <math.h>
 #include <cmath>
 #include <stdio.h>
@@ -101,7 +102,7 @@ struct pt_session {
     uint32_t* hid = nullptr;      // n_slots (done.id)
     uint32_t* pidbuf = nullptr;   // 2 * n_slots (fresh queues' plane prims)
     uint32_t* carry = nullptr;    // 2 * carry_cap * carry_words
-    uint32_t carry_cap = 0, carry_words = 0, straggler_steps = 64;
+    uint32_t carry_cap = 0, carry_words = 0, straggler_steps = 32;
     uint32_t* ctl = nullptr;      // 2 x 8 round counters
     uint32_t* ctl_host = nullptr; // pinned copy of one counter set
     uint32_t isect_grid = 0, shade_grid = 0, rounds = 0;
@@ -576,8 +577,8 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         if (hipGetDeviceProperties(&pr, ss->dev) != hipSuccess) return cleanup(fail(PT_E_HIP, "device query failed"));
         ss->shade_grid = std::min<uint32_t>((uint32_t)std::max(1, pr.multiProcessorCount) * 8u,
                                             std::max(1u, ss->n_tiles_local));
-        // persistent intersection grid: 4 workgroups (16 waves) per CU, capped by the work
-        ss->isect_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * 4u;
+        // persistent intersection grid: 3 workgroups per CU (the resident limit), capped by the work
+        ss->isect_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * 3u;
         if (const char* g = getenv("PT_ISECT_WG_PER_CU")) ss->isect_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * (uint32_t)std::max(1, atoi(g));
         ss->isect_grid = std::min(ss->isect_grid, std::max(1u, ss->n_tiles_local));
     }
@@ -885,6 +886,60 @@ int pt_unpack_tiles_f32(uint32_t W, uint32_t H, uint32_t rank, uint32_t world, c
 }
 
 // ------------------------------------------------------------- render -----
+namespace {
+// One process driving several GPUs: the packed u8 tiles of every session are
+// gathered to the first device with one grouped ncclGather over xGMI
+// (communicator cached per device set), then un-interleaved on the host.
+int gather_rccl(const std::vector<pt_session*>& sess, int dev0, uint32_t W, uint32_t H, uint8_t* rgb) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, std::vector<ncclComm_t>> comms;
+    std::lock_guard<std::mutex> lk(mu);
+    const int n = (int)sess.size();
+    auto key = std::make_pair(dev0, n);
+    if (!comms.count(key)) {
+        std::vector<int> devs(n);
+        for (int g = 0; g < n; ++g) devs[g] = dev0 + g;
+        std::vector<ncclComm_t> c(n);
+        if (ncclCommInitAll(c.data(), n, devs.data()) != ncclSuccess) return fail(PT_E_RCCL, "ncclCommInitAll failed");
+        comms[key] = c;
+    }
+    auto& c = comms[key];
+    size_t cap = 0;
+    for (auto* x : sess) cap = std::max<size_t>(cap, 3ull * x->n_slots);
+    cap = std::max<size_t>(cap, 16);
+    std::vector<uint8_t*> send(n, nullptr);
+    uint8_t* recv = nullptr;
+    auto release = [&]() {
+        for (int g = 0; g < n; ++g) { (void)hipSetDevice(dev0 + g); (void)hipFree(send[g]); }
+        (void)hipSetDevice(dev0);
+        (void)hipFree(recv);
+    };
+    for (int g = 0; g < n; ++g) {
+        HIP_TRY(hipSetDevice(dev0 + g));
+        if (hipMalloc(&send[g], cap) != hipSuccess) { release(); return fail(PT_E_OOM, "gather buffer"); }
+        if (sess[g]->n_slots)
+            HIP_TRY(hipMemcpyAsync(send[g], sess[g]->out, 3ull * sess[g]->n_slots, hipMemcpyDeviceToDevice,
+                                   sess[g]->stream));
+        if (g == 0 && hipMalloc(&recv, cap * n) != hipSuccess) { release(); return fail(PT_E_OOM, "gather buffer"); }
+    }
+    ncclResult_t r = ncclGroupStart();
+    for (int g = 0; g < n && r == ncclSuccess; ++g)
+        r = ncclGather(send[g], g == 0 ? recv : nullptr, cap, ncclUint8, 0, c[g], sess[g]->stream);
+    if (r == ncclSuccess) r = ncclGroupEnd();
+    if (r != ncclSuccess) { release(); return fail(PT_E_RCCL, std::string("ncclGather: ") + ncclGetErrorString(r)); }
+    std::vector<uint8_t> host(cap * n);
+    HIP_TRY(hipSetDevice(dev0));
+    HIP_TRY(hipMemcpyAsync(host.data(), recv, cap * n, hipMemcpyDeviceToHost, sess[0]->stream));
+    for (int g = 0; g < n; ++g) {
+        HIP_TRY(hipSetDevice(dev0 + g));
+        HIP_TRY(hipStreamSynchronize(sess[g]->stream));
+    }
+    release();
+    for (int g = 0; g < n; ++g) pt_unpack_tiles(W, H, (uint32_t)g, (uint32_t)n, host.data() + cap * g, rgb);
+    return PT_OK;
+}
+}  // namespace
+
 void pt_render_opts_default(pt_render_opts* o) {
     if (!o) return;
     memset(o, 0, sizeof(*o));
@@ -923,35 +978,62 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
     }
     const uint32_t chunk = o.spp_per_launch ? o.spp_per_launch : std::max(1u, std::min(S, 4u));
     int last = 0;
-    for (uint32_t done = 0; done < S;) {
-        const uint32_t k = std::min(chunk, S - done);
-        for (auto* x : sess)
-            if ((rc = pt_session_trace(x, k))) return cleanup(rc);
-        done += k;
-        if (o.progress) {
-            for (auto* x : sess)
-                if ((rc = pt_session_sync(x))) return cleanup(rc);
-            progress_bar(done, S, last);
+    // one host thread per GPU drives its session (the wavefront rounds sync on
+    // their own stream); thread 0 reports progress
+    std::vector<int> trc((size_t)ngpu, PT_OK);
+    std::vector<std::string> terr((size_t)ngpu);
+    auto drive = [&](int g) {
+        pt_session* x = sess[(size_t)g];
+        for (uint32_t done = 0; done < S;) {
+            const uint32_t k = std::min(chunk, S - done);
+            int r = pt_session_trace(x, k);
+            if (!r && (o.progress || ngpu > 1)) r = pt_session_sync(x);
+            if (r) { trc[(size_t)g] = r; terr[(size_t)g] = pt_last_error(); return; }
+            done += k;
+            if (g == 0 && o.progress) progress_bar(done, S, last);
         }
+    };
+    if (ngpu == 1) {
+        drive(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int g = 0; g < ngpu; ++g) th.emplace_back(drive, g);
+        for (auto& t : th) t.join();
     }
-    // resolve per device, then gather on the host
-    // (multi-GPU: every rank's packed tiles are copied back and interleaved)
+    for (int g = 0; g < ngpu; ++g)
+        if (trc[(size_t)g]) return cleanup(fail(trc[(size_t)g], terr[(size_t)g]));
+    // resolve per device (tonemap + quantise on the GPU), then gather the packed
+    // 8-bit tiles: over RCCL to device `o.device` when ngpu > 1, else one copy
     pt_stats agg;
     memset(&agg, 0, sizeof(agg));
+    std::vector<float*> drads((size_t)ngpu, nullptr);
     for (int g = 0; g < ngpu; ++g) {
         pt_session* x = sess[(size_t)g];
         if ((rc = pt_session_sync(x))) return cleanup(rc);
-        float* drad = nullptr;
         if (radiance && x->n_slots) {
             if (hipMalloc(&x->rad, 12ull * x->n_slots) != hipSuccess) return cleanup(fail(PT_E_OOM, "radiance buffer"));
-            drad = x->rad;
+            drads[(size_t)g] = x->rad;
         }
-        if ((rc = pt_session_resolve(x, nullptr, drad))) return cleanup(rc);
-        std::vector<uint8_t> packed(3ull * x->n_slots);
-        if (rgb && x->n_slots) {
-            if ((rc = pt_session_read_packed(x, packed.data(), packed.size()))) return cleanup(rc);
-            pt_unpack_tiles(W, H, (uint32_t)g, (uint32_t)ngpu, packed.data(), rgb);
+        if ((rc = pt_session_resolve(x, nullptr, drads[(size_t)g]))) return cleanup(rc);
+    }
+    if (rgb) {
+        if (ngpu > 1 && gather_rccl(sess, o.device, W, H, rgb) == PT_OK) {
+            agg.gather_rccl = 1;
+        } else {
+            if (ngpu > 1) fprintf(stderr, "pt_render: RCCL gather unavailable (%s); gathering through the host\n",
+                                  pt_last_error());
+            for (int g = 0; g < ngpu; ++g) {
+                pt_session* x = sess[(size_t)g];
+                if (!x->n_slots) continue;
+                std::vector<uint8_t> packed(3ull * x->n_slots);
+                if ((rc = pt_session_read_packed(x, packed.data(), packed.size()))) return cleanup(rc);
+                pt_unpack_tiles(W, H, (uint32_t)g, (uint32_t)ngpu, packed.data(), rgb);
+            }
         }
+    }
+    for (int g = 0; g < ngpu; ++g) {
+        pt_session* x = sess[(size_t)g];
+        float* drad = drads[(size_t)g];
         if (radiance && x->n_slots) {
             std::vector<float> pr(3ull * x->n_slots);
             if (hipMemcpy(pr.data(), drad, pr.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)

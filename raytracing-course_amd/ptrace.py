@@ -61,7 +61,7 @@ class Stats(C.Structure):
                 ("kernel_ms", C.c_double), ("resolve_ms", C.c_double), ("wall_ms", C.c_double),
                 ("node_bytes", C.c_uint64), ("prim_bytes", C.c_uint64), ("aux_bytes", C.c_uint64),
                 ("fallbacks_ray", C.c_uint64), ("isect_ms", C.c_double), ("isect_launches", C.c_uint64),
-                ("rounds", C.c_uint64)]
+                ("rounds", C.c_uint64), ("gather_rccl", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
