@@ -118,6 +118,13 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
     const uint32_t* in = P.ctl + 8u * p;
     uint32_t* out = P.ctl + 8u * (1u - p);
     const uint32_t n_fresh = in[C_FRESH], n_total = n_fresh + in[C_CARRY];
+    // Sparse rounds (the end of a pass: only the slowest pixels' rays are left)
+    // are latency-bound: spread the rays over all waves (small batches) and let
+    // each query run longer before it is suspended (a suspension costs a round).
+    const uint32_t n_waves = gridDim.x * (blockDim.x / 64u);
+    uint32_t bsz = n_total / n_waves;
+    bsz = bsz < 1u ? 1u : (bsz > PT_BATCH ? PT_BATCH : bsz);
+    const uint32_t budget = P.straggler_steps * (PT_BATCH / bsz);
     const RayQ FQ = P.fq[p];
     const uint32_t* CQ = P.cq[p];
     uint32_t* CQout = P.cq[1u - p];
@@ -147,11 +154,11 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
             while (nidle > 0u) {
                 if (bleft == 0u) {
                     uint32_t v = 0u;
-                    if (lane_id() == 0u) v = atomicAdd(out + C_HEAD, PT_BATCH);
+                    if (lane_id() == 0u) v = atomicAdd(out + C_HEAD, bsz);
                     v = __builtin_amdgcn_readfirstlane(v);
                     if (v >= n_total) { exhausted = true; break; }
                     bbase = v;
-                    bleft = n_total - v < PT_BATCH ? n_total - v : PT_BATCH;
+                    bleft = n_total - v < bsz ? n_total - v : bsz;
                 }
                 const uint32_t take = nidle < bleft ? nidle : bleft;
                 if (!active && !got) {
@@ -223,7 +230,7 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
                 P.ex.rd[k] = F4{q.ray.d.x, q.ray.d.y, q.ray.d.z, u2f(wi)};
                 fallbacks++;
                 active = false;
-            } else if (exhausted && ++post >= P.straggler_steps) {
+            } else if (exhausted && ++post >= budget) {
                 // this wave has nothing left to pull: suspend instead of holding up the round
                 const uint32_t k = atomicAdd(out + C_CARRY, 1u);
                 if (k < P.carry_cap) {
