@@ -3,7 +3,7 @@
 
 Workload (N=1): config 3 of BASELINE.json -- the md5-pinned ~90k-triangle
 dragon stand-in (scenes/make_scene.py c3; the reference's dragon_100k file is
-missing) at 1920x1080, RAY_DEPTH 6.  One "step" = `--spp-per-step` (default 4)
+missing) at 1920x1080, RAY_DEPTH 6.  One "step" = `--spp-per-step` (default 16)
 samples for every pixel of the frame: the reference's spp loop advanced by
 that many (each pixel's minstd_rand stream and f32 sum stay resident in HBM,
 so K steps are exactly the first K*spp of the 256 spp).  `value` = Mray/s =
@@ -129,7 +129,7 @@ def main():
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3")
-    ap.add_argument("--spp-per-step", type=int, default=4, help="samples per pixel per step, per GPU")
+    ap.add_argument("--spp-per-step", type=int, default=16, help="samples per pixel per step, per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, nargs=2, default=[480, 270])
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))

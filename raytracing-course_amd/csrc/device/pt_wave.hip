@@ -117,7 +117,7 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
     const uint32_t p = P.parity;
     const uint32_t* in = P.ctl + 8u * p;
     uint32_t* out = P.ctl + 8u * (1u - p);
-    const uint32_t n_fresh = in[C_FRESH], n_total = n_fresh + in[C_CARRY];
+    const uint32_t n_carry = in[C_CARRY], n_total = in[C_FRESH] + n_carry;
     // Sparse rounds (the end of a pass: only the slowest pixels' rays are left)
     // are latency-bound: spread the rays over all waves (small batches) and let
     // each query run longer before it is suspended (a suspension costs a round).
@@ -128,7 +128,8 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
     const RayQ FQ = P.fq[p];
     const uint32_t* CQ = P.cq[p];
     uint32_t* CQout = P.cq[1u - p];
-    // wave-uniform batch of work indices: [0, n_fresh) fresh rays, then suspended queries
+    // wave-uniform batch of work indices: [0, n_carry) suspended queries first (they
+    // are the slow pixels' rays: fetched early they get the whole round), then fresh rays
     uint32_t bbase = 0u, bleft = 0u;
     bool exhausted = false;
     bool active = false;
@@ -171,19 +172,20 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
             }
             if (got) {
                 post = 0u;
-                if (wi < n_fresh) {
-                    const F4 o = FQ.ro[wi], d = FQ.rd[wi];
+                if (wi >= n_carry) {
+                    const uint32_t fi = wi - n_carry;   // fresh-queue index (wi stays the done index)
+                    const F4 o = FQ.ro[fi], d = FQ.rd[fi];
                     Ray ray;
                     ray.o = mk3(o.x, o.y, o.z);
                     ray.d = mk3(d.x, d.y, d.z);
                     slot = f2u(o.w);
                     rays++;
                     C.planes += P.S.n_planes;
-                    q_init(P.S, ray, d.w, FQ.pid[wi], q);
+                    q_init(P.S, ray, d.w, FQ.pid[fi], q);
                     if (q.phase == Q_EXACT) init_exact++;
                 } else {
                     // resume a suspended query: state, slot, then its aux stack into LDS
-                    const uint32_t* w = CQ + (size_t)(wi - n_fresh) * P.carry_words;
+                    const uint32_t* w = CQ + (size_t)wi * P.carry_words;
                     q = *reinterpret_cast<const Query*>(w);
                     const uint32_t* tail = w + sizeof(Query) / 4u;
                     slot = tail[0];

@@ -102,7 +102,7 @@ struct pt_session {
     uint32_t* hid = nullptr;      // n_slots (done.id)
     uint32_t* pidbuf = nullptr;   // 2 * n_slots (fresh queues' plane prims)
     uint32_t* carry = nullptr;    // 2 * carry_cap * carry_words
-    uint32_t carry_cap = 0, carry_words = 0, straggler_steps = 32;
+    uint32_t carry_cap = 0, carry_words = 0, straggler_steps = 64;
     uint32_t* ctl = nullptr;      // 2 x 8 round counters
     uint32_t* ctl_host = nullptr; // pinned copy of one counter set
     uint32_t isect_grid = 0, shade_grid = 0, rounds = 0;
