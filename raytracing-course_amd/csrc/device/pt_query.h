@@ -134,8 +134,22 @@ PT_HD void q_planes(const SceneView& S, const Ray& ray, float& P, int& pid) {
     pid = -1;
     for (uint32_t k = 0; k < S.n_planes; ++k) {
         const uint32_t pi = S.planes[k];
+        const Prim pr = S.prims[pi];
         Hit h;
-        if (plane_intersect(S.prims[pi], ray, h) && h.t < P) { P = h.t; pid = (int)pi; }
+        bool ok;
+        if (f2u(pr.p1.x) == 0u && f2u(pr.p1.y) == 0u && f2u(pr.p1.z) == 0u && f2u(pr.p1.w) == 0x3f800000u) {
+            // identity rotation: the local ray equals (o - pos, d) up to the sign of
+            // zero components, which changes neither the accept decision nor t
+            // (a signed zero only matters in a sum that is exactly zero, where
+            // every test below fails either way); the normal is not needed here
+            Ray lr;
+            lr.o = ray.o + -1.f * mk3(pr.p0.x, pr.p0.y, pr.p0.z);
+            lr.d = ray.d;
+            ok = isect_plane(lr, mk3(pr.p2.x, pr.p2.y, pr.p2.z), h);
+        } else {
+            ok = plane_intersect(pr, ray, h);
+        }
+        if (ok && h.t < P) { P = h.t; pid = (int)pi; }
     }
 }
 
