@@ -64,4 +64,38 @@ __device__ __forceinline__ void wave_add_u64(unsigned long long* dst, unsigned l
     if ((threadIdx.x & 63u) == 0u && v != 0ull) atomicAdd(dst, v);
 }
 
+// The XCD (of 8) this wave runs on (HW_REG_XCC_ID).  Same-address atomics from
+// the whole chip serialise at ~11.5 ns each on MI355X (tools/micro/atomics.hip);
+// one copy of a hot counter per XCD, each on its own 128-B line, cuts that 8x.
+__device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u; }
+
+// this XCD's copy of the statistics counters (PT_CTR_COPIES x PT_CTR_STRIDE u64; the host sums them)
+__device__ __forceinline__ unsigned long long* ctr_copy(unsigned long long* counters) {
+    return counters + PT_CTR_STRIDE * xcc_id();
+}
+
+// block-aggregated append: ONE atomic per workgroup (every thread of the block
+// must call it, NW = waves per block); returns this lane's position (want lanes only)
+template <uint32_t NW>
+__device__ __forceinline__ uint32_t block_append(uint32_t* counter, bool want, uint32_t* lds) {
+    const unsigned long long m = __ballot(want);
+    const uint32_t w = threadIdx.x >> 6;
+    if (lane_id() == 0u) lds[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0u) {
+        uint32_t tot = 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < NW; ++k) {
+            const uint32_t c = lds[k];
+            lds[k] = tot;
+            tot += c;
+        }
+        lds[NW] = tot ? atomicAdd(counter, tot) : 0u;
+    }
+    __syncthreads();
+    const uint32_t r = lds[NW] + lds[w] + lanes_below(m);
+    __syncthreads();   // lds is reused by the next call
+    return r;
+}
+
 }  // namespace pt

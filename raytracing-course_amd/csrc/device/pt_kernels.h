@@ -60,8 +60,13 @@ struct DoneQ {                    // finished queries, input of the shade kernel
 // per-slot path state (pstate = nv | end << 8)
 enum : uint32_t { PE_LIVE = 0u, PE_MISS = 1u, PE_CUT = 2u, PE_TERM = 3u };
 
-// round counters: set p = ctl + 8p
-enum : uint32_t { C_FRESH = 0u, C_CARRY = 1u, C_HEAD = 2u, C_DONE = 3u, C_EXACT = 4u };
+// round counters: set p = ctl + PT_CTL_SET * p; the work-batch heads are one per
+// XCD, each on its own 128-B line (C_HEADS + 32 x)
+enum : uint32_t { C_FRESH = 0u, C_CARRY = 1u, C_DONE = 3u, C_EXACT = 4u, C_HEADS = 32u };
+#define PT_CTL_SET 288u          // words per counter set (C_HEADS + 8 x 32)
+// statistics counters: one copy per XCD (PT_CTR_COPIES x PT_CTR_STRIDE u64), summed by the host
+#define PT_CTR_COPIES 8u
+#define PT_CTR_STRIDE 16u
 
 struct WaveParams {
     SceneView S;
@@ -78,7 +83,7 @@ struct WaveParams {
     uint32_t carry_cap, carry_words;
     DoneQ done;
     RayQ ex;                      // rays handed to the exact DFS this round
-    uint32_t* ctl;                // 2 x 8 round counters
+    uint32_t* ctl;                // 2 x PT_CTL_SET round counters
     unsigned long long* counters; // rays, nodes, prim tests, plane tests, errors, aux visits, fallbacks, ray fallbacks
     uint32_t depth;
     uint32_t parity;

@@ -74,13 +74,14 @@ __global__ void __launch_bounds__(256) k_trace(TraceParams P) {
         P.st.sum[P.st.n_slots + slot] = sum.y;
         P.st.sum[2u * P.st.n_slots + slot] = sum.z;
     }
-    wave_add_u64(P.counters + 0, C.rays);
-    wave_add_u64(P.counters + 1, C.nodes);
-    wave_add_u64(P.counters + 2, C.ptests);
-    wave_add_u64(P.counters + 3, C.planes);
-    wave_add_u64(P.counters + 4, (unsigned long long)C.errs);
-    wave_add_u64(P.counters + 5, C.aux);
-    wave_add_u64(P.counters + 6, C.fallbacks);
+    unsigned long long* ctr = ctr_copy(P.counters);
+    wave_add_u64(ctr + 0, C.rays);
+    wave_add_u64(ctr + 1, C.nodes);
+    wave_add_u64(ctr + 2, C.ptests);
+    wave_add_u64(ctr + 3, C.planes);
+    wave_add_u64(ctr + 4, (unsigned long long)C.errs);
+    wave_add_u64(ctr + 5, C.aux);
+    wave_add_u64(ctr + 6, C.fallbacks);
     if (P.wg_prof) {
         __syncthreads();
         if (threadIdx.x == 0) {

@@ -95,8 +95,9 @@ __global__ void __launch_bounds__(256) k_wcamera(WaveParams P) {
         }
         store_rng(P.st, slot, R);
     }
-    uint32_t* ctl = P.ctl + 8u * P.parity;
-    const uint32_t qi = wave_append(ctl + C_FRESH, want);
+    __shared__ uint32_t agg[5];
+    uint32_t* ctl = P.ctl + PT_CTL_SET * P.parity;
+    const uint32_t qi = block_append<4u>(ctl + C_FRESH, want, agg);
     if (want) push_ray(P, P.fq[P.parity], qi, ray, slot);
 }
 
@@ -115,8 +116,8 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
     extern __shared__ uint32_t lds_stack[];
     LdsMem stk{lds_stack + threadIdx.x};
     const uint32_t p = P.parity;
-    const uint32_t* in = P.ctl + 8u * p;
-    uint32_t* out = P.ctl + 8u * (1u - p);
+    const uint32_t* in = P.ctl + PT_CTL_SET * p;
+    uint32_t* out = P.ctl + PT_CTL_SET * (1u - p);
     const uint32_t n_carry = in[C_CARRY], n_total = in[C_FRESH] + n_carry;
     // Sparse rounds (the end of a pass: only the slowest pixels' rays are left)
     // are latency-bound: spread the rays over all waves (small batches) and let
@@ -130,6 +131,12 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
     uint32_t* CQout = P.cq[1u - p];
     // wave-uniform batch of work indices: [0, n_carry) suspended queries first (they
     // are the slow pixels' rays: fetched early they get the whole round), then fresh rays
+    // Batches are handed out by one counter per XCD: batch b = 8k + x is the k-th
+    // of XCD x's counter and covers [b*bsz, (b+1)*bsz) -- the XCDs advance together,
+    // so the global order (carried first) holds approximately; a wave whose XCD's
+    // share is used up steals from the next XCD's counter (xs = counters found empty).
+    const uint32_t xcc = xcc_id();
+    uint32_t xs = 0u;
     uint32_t bbase = 0u, bleft = 0u;
     bool exhausted = false;
     bool active = false;
@@ -154,10 +161,18 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
             bool got = false;
             while (nidle > 0u) {
                 if (bleft == 0u) {
-                    uint32_t v = 0u;
-                    if (lane_id() == 0u) v = atomicAdd(out + C_HEAD, bsz);
+                    uint32_t v = 0xffffffffu;
+                    if (lane_id() == 0u) {
+                        while (xs < 8u) {
+                            const uint32_t y = (xcc + xs) & 7u;
+                            const uint64_t b = 8ull * atomicAdd(out + C_HEADS + 32u * y, 1u) + y;
+                            if (b * bsz < n_total) { v = (uint32_t)(b * bsz); break; }
+                            ++xs;
+                        }
+                    }
                     v = __builtin_amdgcn_readfirstlane(v);
-                    if (v >= n_total) { exhausted = true; break; }
+                    xs = __builtin_amdgcn_readfirstlane(xs);
+                    if (v == 0xffffffffu) { exhausted = true; break; }
                     bbase = v;
                     bleft = n_total - v < bsz ? n_total - v : bsz;
                 }
@@ -234,31 +249,29 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
                 active = false;
             } else if (exhausted && ++post >= budget) {
                 // this wave has nothing left to pull: suspend instead of holding up the round
-                const uint32_t k = atomicAdd(out + C_CARRY, 1u);
-                if (k < P.carry_cap) {
-                    uint32_t* w = CQout + (size_t)k * P.carry_words;
-                    *reinterpret_cast<Query*>(w) = q;
-                    uint32_t* tail = w + sizeof(Query) / 4u;
-                    tail[0] = slot;
-                    for (uint32_t j = 0; j < q.sp; ++j) tail[1u + j] = stk.get(j);
-                    P.done.id[wi] = PT_SUSPENDED;
-                    active = false;
-                } else {
-                    atomicSub(out + C_CARRY, 1u);   // carry queue full: keep running
-                }
+                // (carry_cap = pixel slots >= rays in flight: the queue never overflows)
+                const uint32_t k = wave_append(out + C_CARRY, true);
+                uint32_t* w = CQout + (size_t)k * P.carry_words;
+                *reinterpret_cast<Query*>(w) = q;
+                uint32_t* tail = w + sizeof(Query) / 4u;
+                tail[0] = slot;
+                for (uint32_t j = 0; j < q.sp; ++j) tail[1u + j] = stk.get(j);
+                P.done.id[wi] = PT_SUSPENDED;
+                active = false;
             }
         }
 #ifdef PT_WPROF
         cyc_step += __builtin_amdgcn_s_memtime() - c1;
 #endif
     }
-    wave_add_u64(P.counters + 0, rays);
-    wave_add_u64(P.counters + 1, C.nodes);
-    wave_add_u64(P.counters + 2, C.ptests);
-    wave_add_u64(P.counters + 3, C.planes);
-    wave_add_u64(P.counters + 5, C.aux);
-    wave_add_u64(P.counters + 6, fallbacks);
-    wave_add_u64(P.counters + 7, init_exact);
+    unsigned long long* ctr = ctr_copy(P.counters);
+    wave_add_u64(ctr + 0, rays);
+    wave_add_u64(ctr + 1, C.nodes);
+    wave_add_u64(ctr + 2, C.ptests);
+    wave_add_u64(ctr + 3, C.planes);
+    wave_add_u64(ctr + 5, C.aux);
+    wave_add_u64(ctr + 6, fallbacks);
+    wave_add_u64(ctr + 7, init_exact);
     if (P.wg_prof) {
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -281,7 +294,7 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
 // exact stack DFS for the handed-back rays; 64-lane workgroups, stack in LDS
 __global__ void __launch_bounds__(64) k_wexact(WaveParams P) {
     extern __shared__ uint32_t lds_stack[];
-    uint32_t* out = P.ctl + 8u * (1u - P.parity);
+    uint32_t* out = P.ctl + PT_CTL_SET * (1u - P.parity);
     const uint32_t n = out[C_EXACT];
     LdsMemN<64u> stk{lds_stack + threadIdx.x};
     QCounts C{0u, 0u, 0u, 0u};
@@ -297,18 +310,20 @@ __global__ void __launch_bounds__(64) k_wexact(WaveParams P) {
         P.done.rd[j] = F4{d.x, d.y, d.z, 0.f};
         P.done.id[j] = id < 0 ? 0xffffffffu : (uint32_t)id;
     }
-    wave_add_u64(P.counters + 1, C.nodes);
-    wave_add_u64(P.counters + 2, C.ptests);
-    wave_add_u64(P.counters + 3, C.planes);
+    unsigned long long* ctr = ctr_copy(P.counters);
+    wave_add_u64(ctr + 1, C.nodes);
+    wave_add_u64(ctr + 2, C.ptests);
+    wave_add_u64(ctr + 3, C.planes);
 }
 
 __global__ void __launch_bounds__(256) k_wshade(WaveParams P) {
-    const uint32_t* in = P.ctl + 8u * P.parity;
-    uint32_t* out = P.ctl + 8u * (1u - P.parity);
+    __shared__ uint32_t agg[5];
+    const uint32_t* in = P.ctl + PT_CTL_SET * P.parity;
+    uint32_t* out = P.ctl + PT_CTL_SET * (1u - P.parity);
     const uint32_t n = in[C_FRESH] + in[C_CARRY];   // work indices of this round
     const RayQ N = P.fq[1u - P.parity];
     const uint32_t stride = gridDim.x * 256u;
-    // grid-stride with a uniform trip count so the wave-aggregated append sees every lane
+    // grid-stride with a block-uniform trip count (the block-aggregated append needs every thread)
     for (uint32_t base = blockIdx.x * 256u; base < n; base += stride) {
         const uint32_t i = base + threadIdx.x;
         bool emit = false;
@@ -367,7 +382,7 @@ __global__ void __launch_bounds__(256) k_wshade(WaveParams P) {
             P.pstate[slot] = nv;
             store_rng(P.st, slot, R);
         }
-        const uint32_t qn = wave_append(out + C_FRESH, emit);
+        const uint32_t qn = block_append<4u>(out + C_FRESH, emit, agg);
         if (emit) push_ray(P, N, qn, ray, slot);
     }
 }
@@ -376,7 +391,7 @@ __global__ void __launch_bounds__(256) k_wshade(WaveParams P) {
 
 extern "C++" {
 hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(p.ctl, 0, 4u * 16u, s);
+    hipError_t e = hipMemsetAsync(p.ctl, 0, 4u * 2u * PT_CTL_SET, s);
     if (e != hipSuccess) return e;
     p.parity = 0u;
     hipLaunchKernelGGL(pt::k_wcamera, dim3(p.n_tiles_local), dim3(256), 0, s, p);
@@ -385,7 +400,7 @@ hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s) {
 
 hipError_t pt_launch_wave_round(pt::WaveParams p, uint32_t isect_grid, uint32_t shade_grid, hipStream_t s,
                                 hipEvent_t e0, hipEvent_t e1) {
-    hipError_t e = hipMemsetAsync(p.ctl + 8u * (1u - p.parity), 0, 4u * 8u, s);
+    hipError_t e = hipMemsetAsync(p.ctl + PT_CTL_SET * (1u - p.parity), 0, 4u * PT_CTL_SET, s);
     if (e != hipSuccess) return e;
     if (e0 && (e = hipEventRecord(e0, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(pt::k_wisect, dim3(isect_grid), dim3(256), 1024u * p.aux_stack, s, p);

@@ -103,7 +103,7 @@ struct pt_session {
     uint32_t* pidbuf = nullptr;   // 2 * n_slots (fresh queues' plane prims)
     uint32_t* carry = nullptr;    // 2 * carry_cap * carry_words
     uint32_t carry_cap = 0, carry_words = 0, straggler_steps = 64;
-    uint32_t* ctl = nullptr;      // 2 x 8 round counters
+    uint32_t* ctl = nullptr;      // 2 x PT_CTL_SET round counters
     uint32_t* ctl_host = nullptr; // pinned copy of one counter set
     uint32_t isect_grid = 0, shade_grid = 0, rounds = 0;
     hipStream_t stream = nullptr;
@@ -551,7 +551,7 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
     if (hipStreamCreateWithFlags(&ss->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&ss->st.rng_x, n * 4) != hipSuccess || hipMalloc(&ss->st.rng_saved, n * 4) != hipSuccess ||
         hipMalloc(&ss->st.rng_flag, n * 4) != hipSuccess || hipMalloc(&ss->st.sum, 3 * n * 4) != hipSuccess ||
-        hipMalloc(&ss->vscratch, vwords * 4) != hipSuccess || hipMalloc(&ss->counters, 8 * 8) != hipSuccess ||
+        hipMalloc(&ss->vscratch, vwords * 4) != hipSuccess || hipMalloc(&ss->counters, 8 * PT_CTR_COPIES * PT_CTR_STRIDE) != hipSuccess ||
         hipMalloc(&ss->out, 3 * n) != hipSuccess)
         return cleanup(fail(PT_E_OOM, "device allocation failed"));
     ss->st.n_slots = ss->n_slots;
@@ -562,13 +562,16 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
     if (ss->wave) {
         // suspended-query records: Query | slot | aux stack, rounded to 16 B
         ss->carry_words = ((uint32_t)(sizeof(pt::Query) / 4) + 1u + std::max<uint32_t>(s->auxw_stack, 1u) + 3u) & ~3u;
-        ss->carry_cap = (uint32_t)std::max<size_t>(4096, n / 16);
+        // a pixel has at most one ray in flight, so at most n queries are ever
+        // suspended at once: the carry queue can never overflow (an over-full
+        // queue would make its queries run to the end inside the round)
+        ss->carry_cap = (uint32_t)n;
         if (const char* g = getenv("PT_STRAGGLER")) ss->straggler_steps = (uint32_t)std::max(1, atoi(g));
         if (hipMalloc(&ss->pstate, n * 4) != hipSuccess || hipMalloc(&ss->qbuf, 8 * n * 16) != hipSuccess ||
             hipMalloc(&ss->hid, n * 4) != hipSuccess || hipMalloc(&ss->nsamp, n * 4) != hipSuccess ||
             hipMalloc(&ss->pidbuf, 2 * n * 4) != hipSuccess ||
             hipMalloc(&ss->carry, 2ull * ss->carry_cap * ss->carry_words * 4) != hipSuccess ||
-            hipMalloc(&ss->ctl, 64) != hipSuccess || hipHostMalloc(&ss->ctl_host, 64) != hipSuccess)
+            hipMalloc(&ss->ctl, 8 * PT_CTL_SET) != hipSuccess || hipHostMalloc(&ss->ctl_host, 64) != hipSuccess)
             return cleanup(fail(PT_E_OOM, "device allocation failed (wavefront buffers)"));
         if (hipMemsetAsync(ss->nsamp, 0, n * 4, ss->stream) != hipSuccess ||
             hipMemsetAsync(ss->pstate, 0, n * 4, ss->stream) != hipSuccess)
@@ -582,7 +585,7 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         if (const char* g = getenv("PT_ISECT_WG_PER_CU")) ss->isect_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * (uint32_t)std::max(1, atoi(g));
         ss->isect_grid = std::min(ss->isect_grid, std::max(1u, ss->n_tiles_local));
     }
-    if (hipMemsetAsync(ss->counters, 0, 64, ss->stream) != hipSuccess) return cleanup(fail(PT_E_HIP, "memset failed"));
+    if (hipMemsetAsync(ss->counters, 0, 8 * PT_CTR_COPIES * PT_CTR_STRIDE, ss->stream) != hipSuccess) return cleanup(fail(PT_E_HIP, "memset failed"));
     if (ss->n_tiles_local) {
         pt::InitParams ip;
         ip.tm = ss->tm;
@@ -681,7 +684,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             ss->rounds++;
             p ^= 1u;
         }
-        HIP_TRY(hipMemcpyAsync(ss->ctl_host, ss->ctl + 8u * p, 8, hipMemcpyDeviceToHost, ss->stream));
+        HIP_TRY(hipMemcpyAsync(ss->ctl_host, ss->ctl + PT_CTL_SET * p, 8, hipMemcpyDeviceToHost, ss->stream));
         HIP_TRY(hipStreamSynchronize(ss->stream));
         if (ss->ctl_host[pt::C_FRESH] == 0u && ss->ctl_host[pt::C_CARRY] == 0u) break;
         if (guard > 100000u) return fail(PT_E_HIP, "wavefront rounds did not drain");
@@ -803,8 +806,10 @@ int pt_session_stats(pt_session* ss, pt_stats* st) {
     if (!ss || !st) return fail(PT_E_INVALID, "null argument");
     int rc = pt_session_sync(ss);
     if (rc) return rc;
-    unsigned long long c[8] = {0};
-    HIP_TRY(hipMemcpy(c, ss->counters, 64, hipMemcpyDeviceToHost));
+    unsigned long long cc[PT_CTR_COPIES * PT_CTR_STRIDE], c[8] = {0};
+    HIP_TRY(hipMemcpy(cc, ss->counters, sizeof(cc), hipMemcpyDeviceToHost));
+    for (uint32_t x = 0; x < PT_CTR_COPIES; ++x)
+        for (uint32_t k = 0; k < 8; ++k) c[k] += cc[PT_CTR_STRIDE * x + k];
     memset(st, 0, sizeof(*st));
     st->rays = c[0];
     st->node_visits = c[1];
