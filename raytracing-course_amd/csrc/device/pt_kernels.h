@@ -93,7 +93,22 @@ struct WaveParams {
     uint32_t aux_stack;           // wide aux traversal stack words per lane (LDS)
     uint32_t straggler_steps;     // steps a query may run after its wave ran out of work, before suspending
     unsigned long long* wg_prof;  // optional (diagnostics): per isect workgroup {start, end, HW_ID, XCC_ID, steps}
+    // path engine (k_wpath): chains continue inside the kernel
+    uint32_t path;                // 1 = path engine rounds (k_wshade then shades the exact-DFS results only)
+    uint32_t path_budget;         // loop trips a query wave keeps its chains going after the round's work ran out
+    F4* ring;                     // per-workgroup ray/done rings, PT_RING_F4 F4 per workgroup
 };
+
+// path engine geometry: PT_NQ query waves + 1 shade wave per workgroup; at most
+// PT_CMAX chains resident per workgroup (= the capacity of its two rings)
+#ifndef PT_NQ
+#define PT_NQ 3u
+#endif
+#define PT_PATH_WG (64u * (PT_NQ + 1u))
+#ifndef PT_CMAX
+#define PT_CMAX 512u
+#endif
+#define PT_RING_F4 (4u * PT_CMAX + PT_CMAX / 4u)   // rq ro, rq rd, dq ro, dq rd, rq plane ids
 
 struct ResolveParams {
     PixelState st;
@@ -113,5 +128,8 @@ hipError_t pt_launch_trace(const pt::TraceParams& p, int variant, uint32_t lds_b
 hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s);
 // e0/e1 (optional): events recorded around the k_wisect launch (its time for the roofline)
 hipError_t pt_launch_wave_round(pt::WaveParams p, uint32_t isect_grid, uint32_t shade_grid, hipStream_t s,
+                                hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+// path engine round: {k_wpath, k_wexact, k_wshade (exact results)}
+hipError_t pt_launch_path_round(pt::WaveParams p, uint32_t path_grid, uint32_t shade_grid, hipStream_t s,
                                 hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t pt_launch_resolve(const pt::ResolveParams& p, uint32_t n_tiles, hipStream_t s);

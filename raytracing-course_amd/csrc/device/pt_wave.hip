@@ -68,6 +68,62 @@ __device__ __forceinline__ Ray camera_sample(const CamView& cam, Rng& R, uint32_
     return camera_ray(cam, fx, fy);
 }
 
+// One finished query of a pixel's chain (src/scene.cpp:91-177 for the vertex,
+// :198 for the fold): the vertex and its fold record -- or the miss -- and, at
+// path end, the backward fold into the pixel sum.  Returns true with `ray` set
+// to the chain's next ray (the child, or the next sample's camera ray); false
+// when the pixel has reached this pass's target.  `ray` enters as the query ray.
+__device__ __forceinline__ bool shade_item(const WaveParams& P, uint32_t slot, Ray& ray, uint32_t hid) {
+    bool emit = false;
+    uint32_t nv = P.pstate[slot] & 0xffu;
+    uint32_t end = PE_LIVE;
+    Rng R = load_rng(P.st, slot);
+    if (hid == 0xffffffffu) {
+        end = PE_MISS;
+    } else {
+        // the closest hit's t, normal and side: recomputed from its primitive
+        // (the query's own test, same operations -> same bits)
+        Hit h;
+        (void)prim_intersect(P.S.prims[hid], ray, h);
+        uint32_t idm;
+        float s1, s2;
+        const bool cont = shade_vertex(P.S, R, ray, h, (int)hid, idm, s1, s2);
+        HbmVStore vs{P.vscratch + slot, P.st.n_slots};
+        vs.put(nv, idm, s1, s2);
+        ++nv;
+        if (!cont) end = PE_TERM;
+        else if (nv >= P.depth) end = PE_CUT;   // RayTrace(.., 0) = 0
+        else emit = true;
+    }
+    if (end != PE_LIVE) {
+        // path over: backward fold (deepest vertex first), src/scene.cpp:198 sum += ...
+        f3 L = end == PE_MISS ? P.S.bg : mk3(0.f, 0.f, 0.f);
+        HbmVStore vs{P.vscratch + slot, P.st.n_slots};
+        for (uint32_t k = nv; k > 0u; --k) {
+            uint32_t idm;
+            float s1, s2;
+            vs.get(k - 1u, idm, s1, s2);
+            L = fold_vertex(P.S, L, idm, s1, s2);
+        }
+        P.st.sum[slot] = P.st.sum[slot] + L.x;
+        P.st.sum[P.st.n_slots + slot] = P.st.sum[P.st.n_slots + slot] + L.y;
+        P.st.sum[2u * P.st.n_slots + slot] = P.st.sum[2u * P.st.n_slots + slot] + L.z;
+        const uint32_t done = P.nsamp[slot] + 1u;
+        P.nsamp[slot] = done;
+        nv = 0u;
+        if (done < P.target) {
+            // the pixel's next sample: jitter draws + camera ray
+            uint32_t x, y;
+            slot_xy(P.tm, slot, x, y);
+            ray = camera_sample(P.cam, R, x, y);
+            emit = true;
+        }
+    }
+    P.pstate[slot] = nv;
+    store_rng(P.st, slot, R);
+    return emit;
+}
+
 __global__ void __launch_bounds__(256) k_wcamera(WaveParams P) {
     const uint32_t slot = blockIdx.x * 256u + threadIdx.x;
     uint32_t x, y;
@@ -291,6 +347,400 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
     }
 }
 
+// ---- path engine -------------------------------------------------------------
+// k_wpath: persistent and warp-specialised.  A workgroup is PT_NQ query waves
+// plus one shade wave.  A pixel's chain (its one ray in flight) is always in
+// exactly one place: a query lane, the done ring (query finished, waiting to be
+// shaded), a shade lane, or the ray ring (its next ray, waiting for a query
+// lane).  Query lanes refill from the ray ring first and from the round's work
+// (suspended queries, then fresh rays) second, so a chain keeps going inside the
+// kernel instead of advancing one query per round -- with fewer pixels than
+// lanes (a rank of a multi-GPU render, the end of a pass) the lanes stay busy.
+// Once the round's work is used up a query wave keeps its chains going for
+// `path_budget` more trips, then suspends its queries to the carry queue; the
+// shade wave, last out, hands the remaining chains' next rays to the fresh queue
+// of the next round.  Rounds then only rebalance chains between workgroups.
+//
+// Rings: entries in global memory (per workgroup), positions and per-entry ready
+// flags in LDS, ordered by workgroup-scope release/acquire fences (the waves of a
+// workgroup share one CU and its L1).  At most PT_CMAX chains are resident per
+// workgroup and a chain has at most one ring entry, so neither ring overflows and
+// no entry is overwritten before it has been read.
+struct PathLds {
+    uint32_t rq_head;             // next ray-ring entry to take (query waves, CAS)
+    uint32_t rq_tail;             // ray-ring entries published (shade wave)
+    uint32_t dq_tail;             // done-ring entries reserved (query waves)
+    uint32_t resident;            // chains held by this workgroup
+    uint32_t qw_done;             // query waves that have left
+    uint32_t dq_flag[PT_CMAX];    // done-ring entry ready
+};
+
+__device__ __forceinline__ uint32_t lds_read(const uint32_t& v) { return *(const volatile uint32_t*)&v; }
+__device__ __forceinline__ void lds_write(uint32_t& v, uint32_t x) { *(volatile uint32_t*)&v = x; }
+
+struct PathRing {
+    F4* rq_ro;                    // ray ring: {o.xyz, slot}
+    F4* rq_rd;                    //           {d.xyz, P}
+    int* rq_pid;                  //           closest plane
+    F4* dq_ro;                    // done ring: {o.xyz, slot}
+    F4* dq_rd;                    //            {d.xyz, u32 closest prim | 0xffffffff}
+};
+
+#ifndef PT_PATH_WAVES_PER_EU
+#define PT_PATH_WAVES_PER_EU 3
+#endif
+#define PT_NOWORK 0xffffffffu
+#define PT_CAPPED 0xfffffffeu
+
+__device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L, const PathRing& G,
+                                                uint32_t* lds_stack) {
+    LdsMemN<64u * PT_NQ> stk{lds_stack + threadIdx.x};
+    const uint32_t p = P.parity;
+    const uint32_t* in = P.ctl + PT_CTL_SET * p;
+    uint32_t* out = P.ctl + PT_CTL_SET * (1u - p);
+    const uint32_t n_carry = in[C_CARRY], n_total = in[C_FRESH] + n_carry;
+    const uint32_t n_waves = gridDim.x * PT_NQ;
+    uint32_t bsz = n_total / n_waves;
+    bsz = bsz < 1u ? 1u : (bsz > PT_BATCH ? PT_BATCH : bsz);
+    const RayQ FQ = P.fq[p];
+    const uint32_t* CQ = P.cq[p];
+    uint32_t* CQout = P.cq[1u - p];
+    const uint32_t xcc = xcc_id();
+    uint32_t xs = 0u;                 // XCD batch counters found empty
+    uint32_t bbase = 0u, bleft = 0u;  // this wave's batch of the round's work not yet handed out
+    bool exhausted = false;
+    uint32_t wpost = 0u;              // trips since the round's work ran out
+    uint32_t trip = 0u;
+    uint32_t pend = 0u;               // done-ring entry written last trip, flag not yet set (+1)
+    bool active = false;
+    uint32_t slot = 0u;
+    Query q;
+    QCounts C{0u, 0u, 0u, 0u};
+    uint32_t rays = 0u, fallbacks = 0u, init_exact = 0u;
+#ifdef PT_WPROF
+    uint64_t pf_trips = 0, pf_act = 0, pf_sleep = 0, pf_ring = 0;
+#endif
+    for (;;) {
+        const unsigned long long idle = __ballot(!active);
+        const uint32_t nidle = (uint32_t)__popcll(idle);
+#ifdef PT_WPROF
+        pf_trips++;
+        pf_act += 64u - nidle;
+#endif
+        if (!exhausted && (++trip & 15u) == 0u) {
+            // A wave whose lanes stay busy with its workgroup's chains does not pull,
+            // so it would never find the round's work used up and would run its
+            // chains to the end of the pass: look at the 8 batch counters instead.
+            bool used = true;
+            if (lane_id() < 8u) {
+                const uint32_t h = __hip_atomic_load(out + C_HEADS + 32u * lane_id(), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                used = (8ull * h + lane_id()) * bsz >= n_total;
+            }
+            exhausted = __ballot(!used) == 0ull;
+        }
+        if (exhausted && bleft == 0u) {
+            if (wpost >= P.path_budget) {
+                // the round is over for this wave: suspend its running queries
+                if (active) {
+                    const uint32_t k = wave_append(out + C_CARRY, true);
+                    uint32_t* w = CQout + (size_t)k * P.carry_words;
+                    *reinterpret_cast<Query*>(w) = q;
+                    uint32_t* tail = w + sizeof(Query) / 4u;
+                    tail[0] = slot;
+                    for (uint32_t j = 0; j < q.sp; ++j) tail[1u + j] = stk.get(j);
+                }
+                const uint32_t ns = (uint32_t)__popcll(__ballot(active));
+                if (lane_id() == 0u && ns) atomicSub(&L.resident, ns);
+                break;
+            }
+            if (nidle == 64u && lds_read(L.resident) == 0u) break;   // no chain left anywhere
+            ++wpost;
+        }
+        if (nidle > 0u) {
+            // refill: this wave's batch leftovers, then the ray ring, then new batches
+            const uint32_t pos = lanes_below(idle);   // this idle lane's rank
+            uint32_t given = 0u, src = 0u, gi = 0u;   // src 1 = work item gi, 2 = ray-ring entry gi
+            {
+                const uint32_t take = nidle < bleft ? nidle : bleft;
+                if (!active && pos < take) { src = 1u; gi = bbase + pos; }
+                bbase += take;
+                bleft -= take;
+                given = take;
+            }
+            if (given < nidle) {
+                uint32_t h = 0u, take = 0u;
+                if (lane_id() == 0u) {
+                    for (;;) {
+                        h = lds_read(L.rq_head);
+                        const uint32_t t = lds_read(L.rq_tail), want = nidle - given;
+                        take = t - h < want ? t - h : want;
+                        if (take == 0u || atomicCAS(&L.rq_head, h, h + take) == h) break;
+                    }
+                }
+                h = __builtin_amdgcn_readfirstlane(h);
+                take = __builtin_amdgcn_readfirstlane(take);
+                if (!active && pos >= given && pos < given + take) { src = 2u; gi = (h + pos - given) % PT_CMAX; }
+                given += take;
+#ifdef PT_WPROF
+                pf_ring += take;
+#endif
+            }
+            while (given < nidle && !exhausted) {
+                uint32_t v = PT_NOWORK, cnt = 0u;
+                if (lane_id() == 0u) {
+                    if (atomicAdd(&L.resident, bsz) + bsz > PT_CMAX) {
+                        atomicSub(&L.resident, bsz);   // workgroup full: its chains first
+                        v = PT_CAPPED;
+                    } else {
+                        while (xs < 8u) {
+                            const uint32_t y = (xcc + xs) & 7u;
+                            const uint64_t b = 8ull * atomicAdd(out + C_HEADS + 32u * y, 1u) + y;
+                            if (b * bsz < n_total) { v = (uint32_t)(b * bsz); break; }
+                            ++xs;
+                        }
+                        if (v == PT_NOWORK) {
+                            atomicSub(&L.resident, bsz);
+                        } else {
+                            cnt = n_total - v < bsz ? n_total - v : bsz;
+                            if (cnt < bsz) atomicSub(&L.resident, bsz - cnt);
+                        }
+                    }
+                }
+                v = __builtin_amdgcn_readfirstlane(v);
+                xs = __builtin_amdgcn_readfirstlane(xs);
+                cnt = __builtin_amdgcn_readfirstlane(cnt);
+                if (v == PT_CAPPED) break;
+                if (v == PT_NOWORK) { exhausted = true; break; }
+                bbase = v;
+                bleft = cnt;
+                const uint32_t take = nidle - given < bleft ? nidle - given : bleft;
+                if (!active && pos >= given && pos < given + take) { src = 1u; gi = bbase + pos - given; }
+                bbase += take;
+                bleft -= take;
+                given += take;
+            }
+            if (src == 2u) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (src == 1u && gi < n_carry) {
+                // resume a suspended query: state, slot, then its aux stack into LDS
+                const uint32_t* w = CQ + (size_t)gi * P.carry_words;
+                q = *reinterpret_cast<const Query*>(w);
+                const uint32_t* tail = w + sizeof(Query) / 4u;
+                slot = tail[0];
+                for (uint32_t k = 0; k < q.sp; ++k) stk.set(k, tail[1u + k]);
+                active = true;
+            } else if (src != 0u) {
+                // a fresh ray of the round, or a chain's next ray from the ray ring
+                F4 o, d;
+                int pid;
+                if (src == 1u) {
+                    const uint32_t fi = gi - n_carry;
+                    o = FQ.ro[fi];
+                    d = FQ.rd[fi];
+                    pid = FQ.pid[fi];
+                } else {
+                    o = G.rq_ro[gi];
+                    d = G.rq_rd[gi];
+                    pid = G.rq_pid[gi];
+                }
+                Ray ray;
+                ray.o = mk3(o.x, o.y, o.z);
+                ray.d = mk3(d.x, d.y, d.z);
+                slot = f2u(o.w);
+                rays++;
+                C.planes += P.S.n_planes;
+                q_init(P.S, ray, d.w, pid, q);
+                if (q.phase == Q_EXACT) init_exact++;
+                active = true;
+            }
+        }
+        if (__ballot(active) == 0ull) {
+#ifdef PT_WPROF
+            pf_sleep++;
+#endif
+            __builtin_amdgcn_s_sleep(2);   // nothing to run: chains are being shaded (no `continue`:
+        }                                  // a second back edge costs ~30 VGPRs)
+        if (active && (q.phase == Q_AUX || q.phase == Q_REPLAY)) q_step(P.S, q, C, stk);
+        // Publish the done-ring entries written last trip: their stores were issued before
+        // this trip's loads, which have completed (in-order vmcnt), so the release fence
+        // here does not wait on fresh stores.
+        if (__ballot(pend != 0u) != 0ull) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (pend != 0u) lds_write(L.dq_flag[pend - 1u], 1u);
+            pend = 0u;
+        }
+        if (active) {
+            if (q.phase == Q_DONE) {
+                // to the done ring (the shade wave recomputes t, n, side from the prim)
+                const uint32_t j = wave_append(&L.dq_tail, true) % PT_CMAX;
+                G.dq_ro[j] = F4{q.ray.o.x, q.ray.o.y, q.ray.o.z, u2f(slot)};
+                G.dq_rd[j] = F4{q.ray.d.x, q.ray.d.y, q.ray.d.z, u2f(q.res_id < 0 ? 0xffffffffu : (uint32_t)q.res_id)};
+                pend = j + 1u;
+                active = false;
+            } else if (q.phase == Q_EXACT) {
+                // rare: the exact stack DFS after this kernel; the chain leaves the workgroup
+                const uint32_t k = atomicAdd(out + C_EXACT, 1u);
+                P.ex.ro[k] = F4{q.ray.o.x, q.ray.o.y, q.ray.o.z, u2f(slot)};
+                P.ex.rd[k] = F4{q.ray.d.x, q.ray.d.y, q.ray.d.z, u2f(k)};
+                atomicSub(&L.resident, 1u);
+                fallbacks++;
+                active = false;
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (pend != 0u) lds_write(L.dq_flag[pend - 1u], 1u);
+    unsigned long long* ctr = ctr_copy(P.counters);
+    wave_add_u64(ctr + 0, rays);
+    wave_add_u64(ctr + 1, C.nodes);
+    wave_add_u64(ctr + 2, C.ptests);
+    wave_add_u64(ctr + 3, C.planes);
+    wave_add_u64(ctr + 5, C.aux);
+    wave_add_u64(ctr + 6, fallbacks);
+    wave_add_u64(ctr + 7, init_exact);
+#ifdef PT_WPROF
+    if (P.wg_prof && lane_id() == 0u) {
+        unsigned long long* w = P.wg_prof + 16ull * blockIdx.x;
+        atomicAdd(w + 2, pf_trips);
+        atomicAdd(w + 3, pf_act);
+        atomicAdd(w + 4, pf_sleep);
+        atomicAdd(w + 5, pf_ring);
+        atomicAdd(w + 6, (unsigned long long)rays);
+    }
+#endif
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane_id() == 0u) atomicAdd(&L.qw_done, 1u);
+}
+
+__device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L, const PathRing& G) {
+    uint32_t* out = P.ctl + PT_CTL_SET * (1u - P.parity);
+    const RayQ N = P.fq[1u - P.parity];
+    const RayQ RQ{G.rq_ro, G.rq_rd, G.rq_pid};
+    const uint32_t lane = lane_id();
+    uint32_t head = 0u, tail = 0u;    // done ring consumed / ray ring published (this wave only)
+#ifdef PT_WPROF
+    uint64_t pf_batches = 0, pf_items = 0, pf_spin = 0, pf_cyc = 0, pf_res = 0, pf_dq = 0, pf_rq = 0, pf_samp = 0;
+#endif
+    for (;;) {
+#ifdef PT_WPROF
+        pf_samp++;
+        pf_res += lds_read(L.resident);
+        pf_dq += lds_read(L.dq_tail) - head;
+        pf_rq += tail - lds_read(L.rq_head);
+#endif
+        const uint32_t j = (head + lane) % PT_CMAX;
+        unsigned long long m = __ballot(lds_read(L.dq_flag[j]) != 0u);
+        if ((m & 1ull) == 0ull) {
+            if (lds_read(L.qw_done) == PT_NQ) {
+                // every query wave has left: one more look, then done
+                m = __ballot(lds_read(L.dq_flag[j]) != 0u);
+                if ((m & 1ull) == 0ull) break;
+                continue;
+            }
+#ifdef PT_WPROF
+            pf_spin++;
+#endif
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        const uint32_t n = m == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~m);   // ready run from head
+#ifdef PT_WPROF
+        const uint64_t c0 = __builtin_amdgcn_s_memtime();
+        pf_batches++;
+        pf_items += n;
+#endif
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const bool have = lane < n;
+        Ray ray;
+        uint32_t slot = 0u;
+        bool emit = false;
+        if (have) {
+            const F4 o = G.dq_ro[j], d = G.dq_rd[j];
+            lds_write(L.dq_flag[j], 0u);
+            slot = f2u(o.w);
+            ray.o = mk3(o.x, o.y, o.z);
+            ray.d = mk3(d.x, d.y, d.z);
+            emit = shade_item(P, slot, ray, f2u(d.w));
+        }
+        head += n;
+        const bool flush = __builtin_amdgcn_readfirstlane(lds_read(L.qw_done)) == PT_NQ;
+        const unsigned long long me = __ballot(emit);
+        uint32_t gone = (uint32_t)__popcll(__ballot(have && !emit));   // pixels done with this pass
+        if (flush) {
+            // no query wave left to take it: the next round's fresh queue
+            const uint32_t k = wave_append(out + C_FRESH, emit);
+            if (emit) push_ray(P, N, k, ray, slot);
+            gone += (uint32_t)__popcll(me);
+        } else {
+            if (emit) push_ray(P, RQ, (tail + lanes_below(me)) % PT_CMAX, ray, slot);
+            tail += (uint32_t)__popcll(me);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0u) lds_write(L.rq_tail, tail);
+        }
+        if (lane == 0u && gone) atomicSub(&L.resident, gone);
+#ifdef PT_WPROF
+        pf_cyc += __builtin_amdgcn_s_memtime() - c0;
+#endif
+    }
+#ifdef PT_WPROF
+    if (P.wg_prof && lane == 0u) {
+        unsigned long long* w = P.wg_prof + 16ull * blockIdx.x;
+        w[7] = pf_batches;
+        w[8] = pf_items;
+        w[9] = pf_spin;
+        w[10] = pf_cyc;
+        w[11] = pf_samp;
+        w[12] = pf_res;
+        w[13] = pf_dq;
+        w[14] = pf_rq;
+        w[1] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+    // the ray ring's leftovers (no query wave takes from it any more) -> next round
+    const uint32_t h = lds_read(L.rq_head);
+    for (uint32_t b = h; b < tail; b += 64u) {
+        const uint32_t i = b + lane;
+        const bool has = i < tail;
+        F4 o, d;
+        int pid = -1;
+        if (has) {
+            const uint32_t e = i % PT_CMAX;
+            o = G.rq_ro[e];
+            d = G.rq_rd[e];
+            pid = G.rq_pid[e];
+        }
+        const uint32_t k = wave_append(out + C_FRESH, has);
+        if (has) {
+            N.ro[k] = o;
+            N.rd[k] = d;
+            N.pid[k] = pid;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(PT_PATH_WG) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAVES_PER_EU, PT_PATH_WAVES_PER_EU))) k_wpath(WaveParams P) {
+    extern __shared__ uint32_t lds_stack[];
+    __shared__ PathLds L;
+    F4* r = P.ring + (size_t)blockIdx.x * PT_RING_F4;
+    const PathRing G{r, r + PT_CMAX, reinterpret_cast<int*>(r + 4u * PT_CMAX), r + 2u * PT_CMAX, r + 3u * PT_CMAX};
+    if (threadIdx.x == 0u) {
+        L.rq_head = L.rq_tail = L.dq_tail = L.resident = L.qw_done = 0u;
+    }
+    for (uint32_t i = threadIdx.x; i < PT_CMAX; i += PT_PATH_WG) L.dq_flag[i] = 0u;
+#ifdef PT_WPROF
+    if (P.wg_prof && threadIdx.x == 0u) P.wg_prof[16ull * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
+    __syncthreads();
+#ifndef PT_PATH_ONLY
+    if ((threadIdx.x >> 6) == PT_NQ) path_shade_wave(P, L, G);
+    else path_query_wave(P, L, G, lds_stack);
+#elif PT_PATH_ONLY == 1
+    path_query_wave(P, L, G, lds_stack);
+#else
+    path_shade_wave(P, L, G);
+#endif
+}
+
 // exact stack DFS for the handed-back rays; 64-lane workgroups, stack in LDS
 __global__ void __launch_bounds__(64) k_wexact(WaveParams P) {
     extern __shared__ uint32_t lds_stack[];
@@ -320,7 +770,8 @@ __global__ void __launch_bounds__(256) k_wshade(WaveParams P) {
     __shared__ uint32_t agg[5];
     const uint32_t* in = P.ctl + PT_CTL_SET * P.parity;
     uint32_t* out = P.ctl + PT_CTL_SET * (1u - P.parity);
-    const uint32_t n = in[C_FRESH] + in[C_CARRY];   // work indices of this round
+    // round engine: every work index of the round; path engine: the exact-DFS results only
+    const uint32_t n = P.path ? out[C_EXACT] : in[C_FRESH] + in[C_CARRY];
     const RayQ N = P.fq[1u - P.parity];
     const uint32_t stride = gridDim.x * 256u;
     // grid-stride with a block-uniform trip count (the block-aggregated append needs every thread)
@@ -335,52 +786,7 @@ __global__ void __launch_bounds__(256) k_wshade(WaveParams P) {
             slot = f2u(o.w);
             ray.o = mk3(o.x, o.y, o.z);
             ray.d = mk3(d.x, d.y, d.z);
-            uint32_t nv = P.pstate[slot] & 0xffu;
-            uint32_t end = PE_LIVE;
-            Rng R = load_rng(P.st, slot);
-            if (hid == 0xffffffffu) {
-                end = PE_MISS;
-            } else {
-                // the closest hit's t, normal and side: recomputed from its primitive
-                // (the query's own test, same operations -> same bits)
-                Hit h;
-                (void)prim_intersect(P.S.prims[hid], ray, h);
-                uint32_t idm;
-                float s1, s2;
-                const bool cont = shade_vertex(P.S, R, ray, h, (int)hid, idm, s1, s2);
-                HbmVStore vs{P.vscratch + slot, P.st.n_slots};
-                vs.put(nv, idm, s1, s2);
-                ++nv;
-                if (!cont) end = PE_TERM;
-                else if (nv >= P.depth) end = PE_CUT;   // RayTrace(.., 0) = 0
-                else emit = true;
-            }
-            if (end != PE_LIVE) {
-                // path over: backward fold (deepest vertex first), src/scene.cpp:198 sum += ...
-                f3 L = end == PE_MISS ? P.S.bg : mk3(0.f, 0.f, 0.f);
-                HbmVStore vs{P.vscratch + slot, P.st.n_slots};
-                for (uint32_t k = nv; k > 0u; --k) {
-                    uint32_t idm;
-                    float s1, s2;
-                    vs.get(k - 1u, idm, s1, s2);
-                    L = fold_vertex(P.S, L, idm, s1, s2);
-                }
-                P.st.sum[slot] = P.st.sum[slot] + L.x;
-                P.st.sum[P.st.n_slots + slot] = P.st.sum[P.st.n_slots + slot] + L.y;
-                P.st.sum[2u * P.st.n_slots + slot] = P.st.sum[2u * P.st.n_slots + slot] + L.z;
-                const uint32_t done = P.nsamp[slot] + 1u;
-                P.nsamp[slot] = done;
-                nv = 0u;
-                if (done < P.target) {
-                    // the pixel's next sample: jitter draws + camera ray
-                    uint32_t x, y;
-                    slot_xy(P.tm, slot, x, y);
-                    ray = camera_sample(P.cam, R, x, y);
-                    emit = true;
-                }
-            }
-            P.pstate[slot] = nv;
-            store_rng(P.st, slot, R);
+            emit = shade_item(P, slot, ray, hid);
         }
         const uint32_t qn = block_append<4u>(out + C_FRESH, emit, agg);
         if (emit) push_ray(P, N, qn, ray, slot);
@@ -395,6 +801,20 @@ hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s) {
     if (e != hipSuccess) return e;
     p.parity = 0u;
     hipLaunchKernelGGL(pt::k_wcamera, dim3(p.n_tiles_local), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_path_round(pt::WaveParams p, uint32_t path_grid, uint32_t shade_grid, hipStream_t s,
+                                hipEvent_t e0, hipEvent_t e1) {
+    hipError_t e = hipMemsetAsync(p.ctl + PT_CTL_SET * (1u - p.parity), 0, 4u * PT_CTL_SET, s);
+    if (e != hipSuccess) return e;
+    p.path = 1u;
+    if (e0 && (e = hipEventRecord(e0, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(pt::k_wpath, dim3(path_grid), dim3(PT_PATH_WG), 4u * 64u * PT_NQ * p.aux_stack, s, p);
+    if (e1 && (e = hipEventRecord(e1, s)) != hipSuccess) return e;
+    const uint32_t exact_lds = 64u * 4u * (p.max_stack ? p.max_stack : 1u);
+    hipLaunchKernelGGL(pt::k_wexact, dim3(64), dim3(64), exact_lds, s, p);
+    hipLaunchKernelGGL(pt::k_wshade, dim3(shade_grid), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 

@@ -96,6 +96,9 @@ struct pt_session {
     unsigned long long* wg_prof = nullptr;
     // wavefront engine buffers (replay traversal)
     bool wave = false;
+    bool path = false;            // path engine (k_wpath) rounds instead of {k_wisect, k_wshade}
+    pt::F4* ring = nullptr;       // path engine: path_grid * PT_RING_F4
+    uint32_t path_grid = 0, path_budget = 256;
     uint32_t* pstate = nullptr;
     uint32_t* nsamp = nullptr;    // samples completed per slot
     pt::F4* qbuf = nullptr;       // 8 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd
@@ -584,6 +587,14 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         ss->isect_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * 3u;
         if (const char* g = getenv("PT_ISECT_WG_PER_CU")) ss->isect_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * (uint32_t)std::max(1, atoi(g));
         ss->isect_grid = std::min(ss->isect_grid, std::max(1u, ss->n_tiles_local));
+        // path engine: PT_NQ query waves + 1 shade wave per workgroup, 3 workgroups per CU
+        const char* eng = getenv("PT_ENGINE");
+        ss->path = !(eng && strcmp(eng, "round") == 0);
+        if (const char* b = getenv("PT_PATH_BUDGET")) ss->path_budget = (uint32_t)std::max(1, atoi(b));
+        ss->path_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * 3u;
+        if (const char* g = getenv("PT_PATH_WG_PER_CU")) ss->path_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * (uint32_t)std::max(1, atoi(g));
+        if (ss->path && hipMalloc(&ss->ring, (size_t)ss->path_grid * PT_RING_F4 * sizeof(pt::F4)) != hipSuccess)
+            return cleanup(fail(PT_E_OOM, "device allocation failed (path rings)"));
     }
     if (hipMemsetAsync(ss->counters, 0, 8 * PT_CTR_COPIES * PT_CTR_STRIDE, ss->stream) != hipSuccess) return cleanup(fail(PT_E_HIP, "memset failed"));
     if (ss->n_tiles_local) {
@@ -648,6 +659,9 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.max_stack = std::max<uint32_t>(s->max_stack, 1u);
     wp.aux_stack = std::max<uint32_t>(s->auxw_stack, 1u);
     wp.straggler_steps = ss->straggler_steps;
+    wp.path = ss->path ? 1u : 0u;
+    wp.path_budget = ss->path_budget;
+    wp.ring = ss->ring;
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
@@ -662,8 +676,10 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             const char* wgp = getenv("PT_WGPROF");
             if (wgp && *wgp) {
                 // diagnostics: per-round isect workgroup timelines appended to $PT_WGPROF
-                if (!ss->wg_prof) HIP_TRY(hipMalloc(&ss->wg_prof, 72ull * ss->isect_grid));
-                HIP_TRY(hipMemsetAsync(ss->wg_prof, 0, 72ull * ss->isect_grid, ss->stream));
+                // round engine: 9 u64 per isect workgroup; path engine: 16 u64 per path workgroup
+                const size_t wgb = ss->path ? 128ull * ss->path_grid : 72ull * ss->isect_grid;
+                if (!ss->wg_prof) HIP_TRY(hipMalloc(&ss->wg_prof, 128ull * std::max(ss->isect_grid, ss->path_grid)));
+                HIP_TRY(hipMemsetAsync(ss->wg_prof, 0, wgb, ss->stream));
                 wp.wg_prof = ss->wg_prof;
             }
             hipEvent_t i0, i1;
@@ -671,9 +687,12 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             HIP_TRY(hipEventCreate(&i1));
             ss->pending_isect.emplace_back(i0, i1);
             ss->isect_launches++;
-            HIP_TRY(pt_launch_wave_round(wp, ss->isect_grid, ss->shade_grid, ss->stream, i0, i1));
+            if (ss->path)
+                HIP_TRY(pt_launch_path_round(wp, ss->path_grid, 64u, ss->stream, i0, i1));
+            else
+                HIP_TRY(pt_launch_wave_round(wp, ss->isect_grid, ss->shade_grid, ss->stream, i0, i1));
             if (wp.wg_prof) {
-                std::vector<unsigned long long> h(9ull * ss->isect_grid);
+                std::vector<unsigned long long> h(ss->path ? 16ull * ss->path_grid : 9ull * ss->isect_grid);
                 HIP_TRY(hipMemcpyAsync(h.data(), wp.wg_prof, h.size() * 8, hipMemcpyDeviceToHost, ss->stream));
                 HIP_TRY(hipStreamSynchronize(ss->stream));
                 if (FILE* f = fopen(wgp, "ab")) {
@@ -852,7 +871,7 @@ void pt_session_free(pt_session* ss) {
     (void)hipFree(ss->st.sum); (void)hipFree(ss->vscratch); (void)hipFree(ss->counters);
     (void)hipFree(ss->out); (void)hipFree(ss->rad); (void)hipFree(ss->wg_prof);
     (void)hipFree(ss->pstate); (void)hipFree(ss->qbuf); (void)hipFree(ss->hid); (void)hipFree(ss->nsamp); (void)hipFree(ss->pidbuf);
-    (void)hipFree(ss->carry); (void)hipFree(ss->ctl);
+    (void)hipFree(ss->carry); (void)hipFree(ss->ctl); (void)hipFree(ss->ring);
     if (ss->ctl_host) (void)hipHostFree(ss->ctl_host);
     if (ss->stream) (void)hipStreamDestroy(ss->stream);
     delete ss;

@@ -135,15 +135,17 @@ def test_cli_drop_in_config1(pt, tmp_path):
     assert U.md5(out.read_bytes()) == M["full"]["c1"]["md5"]
 
 
+@pytest.mark.parametrize("engine", ["path", "round"])
 @pytest.mark.parametrize("straggler", ["1", "3"])
 @pytest.mark.parametrize("name", ["c3s4_win_944_520_16x16", "c4glass_s4_win_900_560_16x16", "dragon_64x64x16",
                                   "hw3s4_48x48x8"])
-def test_suspended_queries_resume_bit_exact(pt, name, straggler, monkeypatch):
+def test_suspended_queries_resume_bit_exact(pt, name, straggler, engine, monkeypatch):
     """Force the wavefront engine to suspend almost every query after 1-3 steps
     past its wave's last fetch (PT_STRAGGLER, read at session creation): queries
     then resume from the carry queue over many rounds, interleaving pixels'
     samples arbitrarily -- results must not change."""
-    monkeypatch.setenv("PT_STRAGGLER", straggler)
+    monkeypatch.setenv("PT_STRAGGLER", straggler)     # round engine
+    monkeypatch.setenv("PT_PATH_BUDGET", straggler)   # path engine: trips after the round's work ran out
     m, img, rad = U.golden_image(name)
     with pt.Scene.load(U.golden_scene_path(name)) as s:
         s.prepare()
@@ -151,5 +153,21 @@ def test_suspended_queries_resume_bit_exact(pt, name, straggler, monkeypatch):
         rgb, r, st = s.render(radiance=True, window=win, traversal=0)
     assert st["errors"] == 0
     assert st["rounds"] > 0
+    assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
+    assert np.array_equal(rgb, img)
+
+
+@pytest.mark.parametrize("name", ["c3s4_win_944_520_16x16", "c4glass_s4_win_900_560_16x16", "dragon_64x64x16",
+                                  "hw3s4_48x48x8", "c2_win_240_200_24x24"])
+def test_round_engine_bit_exact(pt, name, monkeypatch):
+    """The round engine ({k_wisect, k_wshade} per round, PT_ENGINE=round) on the
+    golden fixtures (the default path engine is covered above)."""
+    monkeypatch.setenv("PT_ENGINE", "round")
+    m, img, rad = U.golden_image(name)
+    with pt.Scene.load(U.golden_scene_path(name)) as s:
+        s.prepare()
+        win = tuple(m["window"]) if m["window"] else None
+        rgb, r, st = s.render(radiance=True, window=win, traversal=0)
+    assert st["errors"] == 0
     assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
     assert np.array_equal(rgb, img)

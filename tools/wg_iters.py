@@ -1,20 +1,27 @@
 #!/usr/bin/env python3
 """Summarise a PT_WGPROF dump (9 x u64 per isect workgroup per round: start, end
-(100 MHz realtime), HW_ID, XCC_ID, loop trips, [PT_WPROF cycles]) -> per-round
-span, trips and time per trip."""
+(100 MHz realtime), HW_ID, XCC_ID, loop trips, and with a -DPT_WPROF build the
+wave-0 cycles in refill / step, active lane-trips, aux lane-trips) -> per-round
+span, trips, time per trip, lane utilisation."""
 import sys
 import numpy as np
 
 a = np.fromfile(sys.argv[1], np.uint64).reshape(-1, int(sys.argv[2]), 9).astype(np.int64)
-spans, trips, wgdur = [], [], []
+rows = []
 for r in a:
     r = r[r[:, 0] > 0]
     if len(r) == 0:
         continue
-    spans.append((r[:, 1].max() - r[:, 0].min()) / 100.0)
-    trips.append(r[:, 4].max())
-    wgdur.append(((r[:, 1] - r[:, 0]) / 100.0).mean())
-spans, trips, wgdur = map(np.array, (spans, trips, wgdur))
-print("rounds %d: span us mean %.1f p50 %.1f p90 %.1f; max trips/WG mean %.1f p50 %.0f; mean WG dur %.1f us; us/trip %.2f"
-      % (len(spans), spans.mean(), np.median(spans), np.percentile(spans, 90), trips.mean(), np.median(trips),
-         wgdur.mean(), (spans / np.maximum(trips, 1)).mean()))
+    span = (r[:, 1].max() - r[:, 0].min()) / 100.0
+    dur = (r[:, 1] - r[:, 0]) / 100.0
+    trips = r[:, 4]
+    util = r[:, 7].sum() / max(64 * trips.sum(), 1)
+    refill = r[:, 5].sum() / max(r[:, 5].sum() + r[:, 6].sum(), 1)
+    rows.append((span, trips.max(), trips.mean(), dur.mean(), util, refill, r[:, 8].sum() / max(r[:, 7].sum(), 1)))
+R = np.array(rows)
+print("rounds %d" % len(R))
+for name, k in [("span us", 0), ("max trips", 1), ("mean trips", 2), ("mean WG dur us", 3), ("lane util", 4),
+                ("refill cycle frac", 5), ("aux frac of active", 6)]:
+    v = R[:, k]
+    print("  %-20s mean %9.3f p10 %9.3f p50 %9.3f p90 %9.3f" % (name, v.mean(), *np.percentile(v, [10, 50, 90])))
+print("  us per trip (span/max trips) p50 %.2f; total span ms %.1f" % (np.median(R[:, 0] / np.maximum(R[:, 1], 1)), R[:, 0].sum() / 1e3))
