@@ -108,7 +108,8 @@ struct WaveParams {
 #ifndef PT_CMAX
 #define PT_CMAX 512u
 #endif
-#define PT_RING_F4 (4u * PT_CMAX + PT_CMAX / 4u)   // rq ro, rq rd, dq ro, dq rd, rq plane ids
+// per workgroup: ray ring ro, rd; PT_NQ done rings ro, rd; ray-ring plane ids
+#define PT_RING_F4 ((2u + 2u * PT_NQ) * PT_CMAX + PT_CMAX / 4u)
 
 struct ResolveParams {
     PixelState st;

@@ -361,18 +361,20 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
 // shade wave, last out, hands the remaining chains' next rays to the fresh queue
 // of the next round.  Rounds then only rebalance chains between workgroups.
 //
-// Rings: entries in global memory (per workgroup), positions and per-entry ready
-// flags in LDS, ordered by workgroup-scope release/acquire fences (the waves of a
-// workgroup share one CU and its L1).  At most PT_CMAX chains are resident per
-// workgroup and a chain has at most one ring entry, so neither ring overflows and
-// no entry is overwritten before it has been read.
+// Rings: entries in global memory (per workgroup), positions in LDS, ordered by
+// workgroup-scope release/acquire fences (the waves of a workgroup share one CU
+// and its L1).  Every ring has ONE producer, which publishes its entries in order,
+// so a consumer takes a contiguous range: the ray ring is written by the shade
+// wave, and each query wave has its own done ring.  At most PT_CMAX chains are
+// resident per workgroup and a chain has at most one ring entry, so no ring
+// overflows and no entry is overwritten before it has been read.
 struct PathLds {
     uint32_t rq_head;             // next ray-ring entry to take (query waves, CAS)
     uint32_t rq_tail;             // ray-ring entries published (shade wave)
-    uint32_t dq_tail;             // done-ring entries reserved (query waves)
     uint32_t resident;            // chains held by this workgroup
     uint32_t qw_done;             // query waves that have left
-    uint32_t dq_flag[PT_CMAX];    // done-ring entry ready
+    uint32_t dq_tail[PT_NQ];      // done-ring entries published, per query wave
+    uint32_t dq_head[PT_NQ];      // done-ring entries consumed (diagnostics)
 };
 
 __device__ __forceinline__ uint32_t lds_read(const uint32_t& v) { return *(const volatile uint32_t*)&v; }
@@ -382,12 +384,18 @@ struct PathRing {
     F4* rq_ro;                    // ray ring: {o.xyz, slot}
     F4* rq_rd;                    //           {d.xyz, P}
     int* rq_pid;                  //           closest plane
-    F4* dq_ro;                    // done ring: {o.xyz, slot}
-    F4* dq_rd;                    //            {d.xyz, u32 closest prim | 0xffffffff}
+    F4* dq_ro;                    // done rings (PT_NQ x PT_CMAX): {o.xyz, slot}
+    F4* dq_rd;                    //                               {d.xyz, u32 closest prim | 0xffffffff}
 };
 
 #ifndef PT_PATH_WAVES_PER_EU
 #define PT_PATH_WAVES_PER_EU 3
+#endif
+#ifndef PT_PVOTE
+#define PT_PVOTE 1                 // one replay step kind per trip, round-robin over the kinds present
+#endif
+#ifndef PT_PATH_REFILL_MIN
+#define PT_PATH_REFILL_MIN 8u      // idle lanes before a query wave refills (any, once the round's work is out)
 #endif
 #define PT_NOWORK 0xffffffffu
 #define PT_CAPPED 0xfffffffeu
@@ -400,6 +408,10 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     uint32_t* out = P.ctl + PT_CTL_SET * (1u - p);
     const uint32_t n_carry = in[C_CARRY], n_total = in[C_FRESH] + n_carry;
     const uint32_t n_waves = gridDim.x * PT_NQ;
+    // Rounds exist to rebalance chains between workgroups.  Once the round's chains
+    // fit in the query lanes (the tail of a pass: only the slowest pixels are left)
+    // suspending gains nothing and costs a round: run them to the end.
+    const uint32_t budget = n_total <= 64u * n_waves ? 0xffffffffu : P.path_budget;
     uint32_t bsz = n_total / n_waves;
     bsz = bsz < 1u ? 1u : (bsz > PT_BATCH ? PT_BATCH : bsz);
     const RayQ FQ = P.fq[p];
@@ -411,21 +423,38 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     bool exhausted = false;
     uint32_t wpost = 0u;              // trips since the round's work ran out
     uint32_t trip = 0u;
-    uint32_t pend = 0u;               // done-ring entry written last trip, flag not yet set (+1)
+    const uint32_t wq = threadIdx.x >> 6;   // this query wave's done ring
+#if PT_PVOTE
+    uint32_t rr = 0u;                       // replay step kind served last
+#endif
+    const uint32_t dq_base = wq * PT_CMAX;
+    uint32_t dq_res = 0u;                   // done-ring entries reserved (and written)
+    uint32_t dq_pend = 0u, dq_pub = 0u;     // ... written before this trip / published
     bool active = false;
     uint32_t slot = 0u;
     Query q;
     QCounts C{0u, 0u, 0u, 0u};
     uint32_t rays = 0u, fallbacks = 0u, init_exact = 0u;
 #ifdef PT_WPROF
-    uint64_t pf_trips = 0, pf_act = 0, pf_sleep = 0, pf_ring = 0;
+    uint64_t pf_trips = 0, pf_act = 0, pf_sleep = 0, pf_ring = 0, pf_pulled = 0, pf_exit_budget = 0, pf_res = 0,
+             pf_dq = 0, pf_rq = 0, pf_tripcyc = 0, pf_qlat = 0, pf_qn = 0, pf_qsteps = 0, pf_refillcyc = 0;
+    uint64_t pf_t0 = __builtin_amdgcn_s_memtime(), pf_qstart = 0;
+    uint32_t pf_qs = 0;
 #endif
     for (;;) {
         const unsigned long long idle = __ballot(!active);
         const uint32_t nidle = (uint32_t)__popcll(idle);
 #ifdef PT_WPROF
+        {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            pf_tripcyc += t - pf_t0;
+            pf_t0 = t;
+        }
         pf_trips++;
         pf_act += 64u - nidle;
+        pf_res += lds_read(L.resident);
+        pf_dq += lds_read(L.dq_tail[wq]) - lds_read(L.dq_head[wq]);
+        pf_rq += lds_read(L.rq_tail) - lds_read(L.rq_head);
 #endif
         if (!exhausted && (++trip & 15u) == 0u) {
             // A wave whose lanes stay busy with its workgroup's chains does not pull,
@@ -440,7 +469,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
             exhausted = __ballot(!used) == 0ull;
         }
         if (exhausted && bleft == 0u) {
-            if (wpost >= P.path_budget) {
+            if (wpost >= budget) {
                 // the round is over for this wave: suspend its running queries
                 if (active) {
                     const uint32_t k = wave_append(out + C_CARRY, true);
@@ -452,12 +481,15 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 }
                 const uint32_t ns = (uint32_t)__popcll(__ballot(active));
                 if (lane_id() == 0u && ns) atomicSub(&L.resident, ns);
+#ifdef PT_WPROF
+                pf_exit_budget = 1;
+#endif
                 break;
             }
             if (nidle == 64u && lds_read(L.resident) == 0u) break;   // no chain left anywhere
             ++wpost;
         }
-        if (nidle > 0u) {
+        if (nidle >= PT_PATH_REFILL_MIN || nidle == 64u || (nidle > 0u && exhausted)) {
             // refill: this wave's batch leftovers, then the ray ring, then new batches
             const uint32_t pos = lanes_below(idle);   // this idle lane's rank
             uint32_t given = 0u, src = 0u, gi = 0u;   // src 1 = work item gi, 2 = ray-ring entry gi
@@ -514,6 +546,9 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 if (v == PT_NOWORK) { exhausted = true; break; }
                 bbase = v;
                 bleft = cnt;
+#ifdef PT_WPROF
+                pf_pulled += cnt;
+#endif
                 const uint32_t take = nidle - given < bleft ? nidle - given : bleft;
                 if (!active && pos >= given && pos < given + take) { src = 1u; gi = bbase + pos - given; }
                 bbase += take;
@@ -549,6 +584,10 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 slot = f2u(o.w);
                 rays++;
                 C.planes += P.S.n_planes;
+#ifdef PT_WPROF
+                pf_qstart = __builtin_amdgcn_s_memtime();
+                pf_qs = 0;
+#endif
                 q_init(P.S, ray, d.w, pid, q);
                 if (q.phase == Q_EXACT) init_exact++;
                 active = true;
@@ -560,23 +599,58 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
 #endif
             __builtin_amdgcn_s_sleep(2);   // nothing to run: chains are being shaded (no `continue`:
         }                                  // a second back edge costs ~30 VGPRs)
-        if (active && (q.phase == Q_AUX || q.phase == Q_REPLAY)) q_step(P.S, q, C, stk);
-        // Publish the done-ring entries written last trip: their stores were issued before
-        // this trip's loads, which have completed (in-order vmcnt), so the release fence
-        // here does not wait on fresh stores.
-        if (__ballot(pend != 0u) != 0ull) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (pend != 0u) lds_write(L.dq_flag[pend - 1u], 1u);
-            pend = 0u;
+#ifdef PT_WPROF
+        pf_refillcyc += __builtin_amdgcn_s_memtime() - pf_t0;
+        if (active) pf_qs++;
+#endif
+#if PT_PVOTE
+        {
+            // One replay step kind per trip besides the aux steps (the kinds' code paths
+            // would otherwise all be issued every trip): round-robin over the kinds present.
+            const uint32_t kind = active && q.phase == Q_REPLAY ? 1u + q.walk : active && q.phase == Q_AUX ? 0u : 7u;
+            uint32_t present = 0u;
+#pragma unroll
+            for (uint32_t k = 1; k <= 4u; ++k)
+                if (__ballot(kind == k) != 0ull) present |= 1u << k;
+            uint32_t pick = 0u;
+#pragma unroll
+            for (uint32_t j = 1; j <= 4u; ++j) {
+                const uint32_t c = (rr + j - 1u) % 4u + 1u;
+                if (pick == 0u && ((present >> c) & 1u)) pick = c;
+            }
+            if (pick) rr = pick;
+            if (kind == 0u || kind == pick) q_step(P.S, q, C, stk);
         }
+#else
+        if (active && (q.phase == Q_AUX || q.phase == Q_REPLAY)) q_step(P.S, q, C, stk);
+#endif
+        // Publish the done-ring entries written before this trip: their stores were issued
+        // before this trip's loads, which have completed (in-order vmcnt), so the release
+        // fence here does not wait on fresh stores.
+        if (dq_pend != dq_pub) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane_id() == 0u) lds_write(L.dq_tail[wq], dq_pend);
+            dq_pub = dq_pend;
+        }
+        // finished queries -> this wave's done ring, in lane order (the shade wave
+        // recomputes t, n and side from the prim)
+        const bool fin = active && q.phase == Q_DONE;
+        const unsigned long long mfin = __ballot(fin);
+        const uint32_t dq_at = dq_res;
+        dq_res += (uint32_t)__popcll(mfin);
         if (active) {
-            if (q.phase == Q_DONE) {
-                // to the done ring (the shade wave recomputes t, n, side from the prim)
-                const uint32_t j = wave_append(&L.dq_tail, true) % PT_CMAX;
+            if (fin) {
+                const uint32_t j = dq_base + (dq_at + lanes_below(mfin)) % PT_CMAX;
                 G.dq_ro[j] = F4{q.ray.o.x, q.ray.o.y, q.ray.o.z, u2f(slot)};
                 G.dq_rd[j] = F4{q.ray.d.x, q.ray.d.y, q.ray.d.z, u2f(q.res_id < 0 ? 0xffffffffu : (uint32_t)q.res_id)};
-                pend = j + 1u;
                 active = false;
+#ifdef PT_WPROF
+                if (pf_qstart) {
+                    pf_qlat += __builtin_amdgcn_s_memtime() - pf_qstart;
+                    pf_qn++;
+                    pf_qsteps += pf_qs;
+                }
+#endif
             } else if (q.phase == Q_EXACT) {
                 // rare: the exact stack DFS after this kernel; the chain leaves the workgroup
                 const uint32_t k = atomicAdd(out + C_EXACT, 1u);
@@ -587,9 +661,10 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 active = false;
             }
         }
+        dq_pend = dq_res;   // written this trip: published next trip
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (pend != 0u) lds_write(L.dq_flag[pend - 1u], 1u);
+    if (lane_id() == 0u) lds_write(L.dq_tail[wq], dq_res);
     unsigned long long* ctr = ctr_copy(P.counters);
     wave_add_u64(ctr + 0, rays);
     wave_add_u64(ctr + 1, C.nodes);
@@ -600,12 +675,25 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     wave_add_u64(ctr + 7, init_exact);
 #ifdef PT_WPROF
     if (P.wg_prof && lane_id() == 0u) {
-        unsigned long long* w = P.wg_prof + 16ull * blockIdx.x;
+        unsigned long long* w = P.wg_prof + 32ull * blockIdx.x;
         atomicAdd(w + 2, pf_trips);
         atomicAdd(w + 3, pf_act);
         atomicAdd(w + 4, pf_sleep);
         atomicAdd(w + 5, pf_ring);
         atomicAdd(w + 6, (unsigned long long)rays);
+        atomicAdd(w + 11, pf_pulled);
+        atomicAdd(w + 12, pf_exit_budget);
+        atomicAdd(w + 13, pf_res);
+        atomicAdd(w + 14, pf_dq);
+        atomicAdd(w + 15, pf_rq);
+        atomicAdd(w + 16, pf_tripcyc);
+        atomicAdd(w + 21, pf_refillcyc);
+    }
+    if (P.wg_prof) {
+        unsigned long long* w = P.wg_prof + 32ull * blockIdx.x;
+        wave_add_u64(w + 17, pf_qlat);
+        wave_add_u64(w + 18, pf_qn);
+        wave_add_u64(w + 19, pf_qsteps);
     }
 #endif
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -617,24 +705,30 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
     const RayQ N = P.fq[1u - P.parity];
     const RayQ RQ{G.rq_ro, G.rq_rd, G.rq_pid};
     const uint32_t lane = lane_id();
-    uint32_t head = 0u, tail = 0u;    // done ring consumed / ray ring published (this wave only)
+    uint32_t head[PT_NQ];             // done rings consumed (this wave only)
+#pragma unroll
+    for (uint32_t w = 0; w < PT_NQ; ++w) head[w] = 0u;
+    uint32_t tail = 0u, turn = 0u;    // ray ring published; first done ring looked at
 #ifdef PT_WPROF
-    uint64_t pf_batches = 0, pf_items = 0, pf_spin = 0, pf_cyc = 0, pf_res = 0, pf_dq = 0, pf_rq = 0, pf_samp = 0;
+    uint64_t pf_batches = 0, pf_items = 0, pf_spin = 0, pf_cyc = 0;
 #endif
     for (;;) {
-#ifdef PT_WPROF
-        pf_samp++;
-        pf_res += lds_read(L.resident);
-        pf_dq += lds_read(L.dq_tail) - head;
-        pf_rq += tail - lds_read(L.rq_head);
-#endif
-        const uint32_t j = (head + lane) % PT_CMAX;
-        unsigned long long m = __ballot(lds_read(L.dq_flag[j]) != 0u);
-        if ((m & 1ull) == 0ull) {
+        // up to 64 published entries of the done rings, starting with ring `turn`
+        uint32_t take[PT_NQ], n = 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < PT_NQ; ++k) {
+            const uint32_t w = (turn + k) % PT_NQ;
+            const uint32_t av = __builtin_amdgcn_readfirstlane(lds_read(L.dq_tail[w])) - head[w];
+            take[w] = av < 64u - n ? av : 64u - n;
+            n += take[w];
+        }
+        if (n == 0u) {
             if (lds_read(L.qw_done) == PT_NQ) {
-                // every query wave has left: one more look, then done
-                m = __ballot(lds_read(L.dq_flag[j]) != 0u);
-                if ((m & 1ull) == 0ull) break;
+                // every query wave has left (and published): one more look, then done
+                uint32_t left = 0u;
+#pragma unroll
+                for (uint32_t w = 0; w < PT_NQ; ++w) left += lds_read(L.dq_tail[w]) - head[w];
+                if (__builtin_amdgcn_readfirstlane(left) == 0u) break;
                 continue;
             }
 #ifdef PT_WPROF
@@ -643,12 +737,23 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
-        const uint32_t n = m == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~m);   // ready run from head
 #ifdef PT_WPROF
         const uint64_t c0 = __builtin_amdgcn_s_memtime();
         pf_batches++;
         pf_items += n;
 #endif
+        // this lane's entry: ring w, position head[w] + r
+        uint32_t j = 0u, r = lane;
+        bool found = false;
+#pragma unroll
+        for (uint32_t k = 0; k < PT_NQ; ++k) {
+            const uint32_t w = (turn + k) % PT_NQ;
+            if (!found && r < take[w]) { j = w * PT_CMAX + (head[w] + r) % PT_CMAX; found = true; }
+            else if (!found) r -= take[w];
+        }
+#pragma unroll
+        for (uint32_t w = 0; w < PT_NQ; ++w) head[w] += take[w];
+        turn = turn + 1u == PT_NQ ? 0u : turn + 1u;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const bool have = lane < n;
         Ray ray;
@@ -656,13 +761,14 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
         bool emit = false;
         if (have) {
             const F4 o = G.dq_ro[j], d = G.dq_rd[j];
-            lds_write(L.dq_flag[j], 0u);
             slot = f2u(o.w);
             ray.o = mk3(o.x, o.y, o.z);
             ray.d = mk3(d.x, d.y, d.z);
             emit = shade_item(P, slot, ray, f2u(d.w));
         }
-        head += n;
+#ifdef PT_WPROF
+        if (lane < PT_NQ) lds_write(L.dq_head[lane], head[lane]);
+#endif
         const bool flush = __builtin_amdgcn_readfirstlane(lds_read(L.qw_done)) == PT_NQ;
         const unsigned long long me = __ballot(emit);
         uint32_t gone = (uint32_t)__popcll(__ballot(have && !emit));   // pixels done with this pass
@@ -684,15 +790,12 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
     }
 #ifdef PT_WPROF
     if (P.wg_prof && lane == 0u) {
-        unsigned long long* w = P.wg_prof + 16ull * blockIdx.x;
+        unsigned long long* w = P.wg_prof + 32ull * blockIdx.x;
         w[7] = pf_batches;
         w[8] = pf_items;
         w[9] = pf_spin;
         w[10] = pf_cyc;
-        w[11] = pf_samp;
-        w[12] = pf_res;
-        w[13] = pf_dq;
-        w[14] = pf_rq;
+
         w[1] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
@@ -722,13 +825,14 @@ __global__ void __launch_bounds__(PT_PATH_WG) __attribute__((amdgpu_waves_per_eu
     extern __shared__ uint32_t lds_stack[];
     __shared__ PathLds L;
     F4* r = P.ring + (size_t)blockIdx.x * PT_RING_F4;
-    const PathRing G{r, r + PT_CMAX, reinterpret_cast<int*>(r + 4u * PT_CMAX), r + 2u * PT_CMAX, r + 3u * PT_CMAX};
+    const PathRing G{r, r + PT_CMAX, reinterpret_cast<int*>(r + (2u + 2u * PT_NQ) * PT_CMAX), r + 2u * PT_CMAX,
+                     r + (2u + PT_NQ) * PT_CMAX};
     if (threadIdx.x == 0u) {
-        L.rq_head = L.rq_tail = L.dq_tail = L.resident = L.qw_done = 0u;
+        L.rq_head = L.rq_tail = L.resident = L.qw_done = 0u;
     }
-    for (uint32_t i = threadIdx.x; i < PT_CMAX; i += PT_PATH_WG) L.dq_flag[i] = 0u;
+    if (threadIdx.x < PT_NQ) L.dq_tail[threadIdx.x] = L.dq_head[threadIdx.x] = 0u;
 #ifdef PT_WPROF
-    if (P.wg_prof && threadIdx.x == 0u) P.wg_prof[16ull * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    if (P.wg_prof && threadIdx.x == 0u) P.wg_prof[32ull * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #endif
     __syncthreads();
 #ifndef PT_PATH_ONLY

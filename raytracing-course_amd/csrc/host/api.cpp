@@ -677,8 +677,8 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             if (wgp && *wgp) {
                 // diagnostics: per-round isect workgroup timelines appended to $PT_WGPROF
                 // round engine: 9 u64 per isect workgroup; path engine: 16 u64 per path workgroup
-                const size_t wgb = ss->path ? 128ull * ss->path_grid : 72ull * ss->isect_grid;
-                if (!ss->wg_prof) HIP_TRY(hipMalloc(&ss->wg_prof, 128ull * std::max(ss->isect_grid, ss->path_grid)));
+                const size_t wgb = ss->path ? 256ull * ss->path_grid : 72ull * ss->isect_grid;
+                if (!ss->wg_prof) HIP_TRY(hipMalloc(&ss->wg_prof, 256ull * std::max(ss->isect_grid, ss->path_grid)));
                 HIP_TRY(hipMemsetAsync(ss->wg_prof, 0, wgb, ss->stream));
                 wp.wg_prof = ss->wg_prof;
             }
@@ -692,7 +692,14 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             else
                 HIP_TRY(pt_launch_wave_round(wp, ss->isect_grid, ss->shade_grid, ss->stream, i0, i1));
             if (wp.wg_prof) {
-                std::vector<unsigned long long> h(ss->path ? 16ull * ss->path_grid : 9ull * ss->isect_grid);
+                uint32_t cnt[2][8];
+                HIP_TRY(hipMemcpyAsync(cnt[0], ss->ctl + PT_CTL_SET * p, 32, hipMemcpyDeviceToHost, ss->stream));
+                HIP_TRY(hipMemcpyAsync(cnt[1], ss->ctl + PT_CTL_SET * (1u - p), 32, hipMemcpyDeviceToHost, ss->stream));
+                HIP_TRY(hipStreamSynchronize(ss->stream));
+                fprintf(stderr, "round %u: in fresh %u carry %u -> out fresh %u carry %u exact %u\n", ss->rounds,
+                        cnt[0][pt::C_FRESH], cnt[0][pt::C_CARRY], cnt[1][pt::C_FRESH], cnt[1][pt::C_CARRY],
+                        cnt[1][pt::C_EXACT]);
+                std::vector<unsigned long long> h(ss->path ? 32ull * ss->path_grid : 9ull * ss->isect_grid);
                 HIP_TRY(hipMemcpyAsync(h.data(), wp.wg_prof, h.size() * 8, hipMemcpyDeviceToHost, ss->stream));
                 HIP_TRY(hipStreamSynchronize(ss->stream));
                 if (FILE* f = fopen(wgp, "ab")) {

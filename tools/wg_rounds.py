@@ -1,0 +1,19 @@
+#!/usr/bin/env python3
+"""Per-round spans of a path-engine PT_WGPROF dump, next to the round log (n in)."""
+import re
+import sys
+import numpy as np
+
+a = np.fromfile(sys.argv[1], np.uint64).reshape(-1, int(sys.argv[2]), 32).astype(np.int64)
+L = [l for l in open(sys.argv[3]) if l.startswith("round")]
+tot = 0.0
+for i, r in enumerate(a):
+    rr = r[r[:, 0] > 0]
+    span = (rr[:, 1].max() - rr[:, 0].min()) / 100.0 if len(rr) else 0.0
+    tot += span
+    m = re.search(r"in fresh (\d+) carry (\d+)", L[i]) if i < len(L) else None
+    n = int(m.group(1)) + int(m.group(2)) if m else -1
+    if i < 60:
+        print("round %3d n_in %7d span %8.0f us  WG dur p50 %6.0f max %6.0f" % (
+            i, n, span, np.median((rr[:, 1] - rr[:, 0]) / 100.0) if len(rr) else 0, ((rr[:, 1] - rr[:, 0]) / 100.0).max() if len(rr) else 0))
+print("total span ms %.1f" % (tot / 1e3))
