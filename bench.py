@@ -16,9 +16,10 @@ pixels by spp-per-step x N samples per step, so the per-GPU work is fixed as N
 grows ("weak" scaling); the timed region ends with the framebuffer resolve
 (tonemap on device) and an RCCL gather of the packed 8-bit tiles to rank 0.
 
-Also reported: roofline of the dominant kernel (k_trace) from in-kernel
-counters and HIP-event launch times, and the reference CPU renderer timed on
-this host on a bounded sample of the same scene.
+Also reported: roofline of the dominant kernel (k_wpath, the persistent path
+engine: closest-hit queries + shading) from in-kernel counters and HIP-event
+launch times, and the reference CPU renderer timed on this host on a bounded
+sample of the same scene.
 """
 import argparse
 import json
@@ -206,9 +207,10 @@ def main():
     if rank == 0:
         T = float(tmax[0])
         total_rays = float(tsum[1])
-        # roofline of the dominant kernel (k_wisect, the closest-hit query): algorithmic bytes
-        # per launch / mean launch time, both from rank 0; launch times are HIP events
-        # recorded around each k_wisect launch on the session's stream
+        # roofline of the dominant kernel (k_wpath: the path engine's persistent
+        # query + shade kernel, >99% of GPU time): algorithmic bytes per launch / mean
+        # launch time, both from rank 0; launch times are HIP events recorded around
+        # each k_wpath launch on the session's stream
         launches = max(st1["isect_launches"] - st0["isect_launches"], 1)
         isect_ms = st1["isect_ms"] - st0["isect_ms"]
         alg_bytes = (nodes * st1["node_bytes"] + ptests * st1["prim_bytes"] + auxv * st1["aux_bytes"]) / launches
@@ -247,12 +249,12 @@ def main():
                        "parallelism": "pixel tiles x%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_wisect", "alg_bytes_per_launch": alg_bytes, "launch_ms": launch_s * 1e3,
+                         "kernel": "k_wpath", "alg_bytes_per_launch": alg_bytes, "launch_ms": launch_s * 1e3,
                          "launches": launches, "traffic_source": traffic_src,
                          "note": "algorithmic = 4-wide aux BVH nodes (128 B) + reference node records (32 B) + "
                                  "compact primitive records (48 B) per visit; the ~25 MB working set is "
-                                 "L2/Infinity-Cache resident, and the kernel is bound by dependent-load latency, "
-                                 "not bandwidth (DESIGN.md §4)"},
+                                 "L2/Infinity-Cache resident, and the kernel is bound by VALU issue (divergent "
+                                 "per-lane state machines), not bandwidth (DESIGN.md §4)"},
             "wavefront_rounds": int(st1["rounds"] - st0["rounds"]),
             "kernel_ms_per_step": kms / args.steps,
             "rays": total_rays,

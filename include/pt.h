@@ -144,7 +144,12 @@ typedef struct pt_session_opts {
 int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out);
 /* number of owned tiles and of packed output bytes (tiles*256*3) */
 int pt_session_layout(const pt_session* ss, uint32_t* n_tiles, uint64_t* packed_rgb_bytes);
-/* enqueue spp more samples for every owned pixel (asynchronous) */
+/* enqueue spp more samples for every owned pixel (asynchronous).  With the
+ * wavefront engine consecutive calls are coalesced into ONE pass, run by the
+ * next resolve / sync / stats / stream call: a pixel goes on with its next
+ * samples as soon as it has finished the current ones, so only the end of the
+ * coalesced pass waits for the slowest pixel.  Results are identical either way
+ * (each pixel's samples stay in stream order). */
 int pt_session_trace(pt_session* ss, uint32_t spp);
 /* tonemap the current means (sum / samples so far) into the packed tile
  * buffer: 256*3 u8 per owned tile, pixels of a tile row-major; dev_out is a

@@ -96,6 +96,7 @@ struct WaveParams {
     // path engine (k_wpath): chains continue inside the kernel
     uint32_t path;                // 1 = path engine rounds (k_wshade then shades the exact-DFS results only)
     uint32_t path_budget;         // loop trips a query wave keeps its chains going after the round's work ran out
+    uint32_t path_runend;         // a round with at most this many chains runs them to the end of the pass
     F4* ring;                     // per-workgroup ray/done rings, PT_RING_F4 F4 per workgroup
 };
 

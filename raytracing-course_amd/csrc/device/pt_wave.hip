@@ -394,6 +394,9 @@ struct PathRing {
 #ifndef PT_PVOTE
 #define PT_PVOTE 1                 // one replay step kind per trip, round-robin over the kinds present
 #endif
+#ifndef PT_PVOTE_SPARSE
+#define PT_PVOTE_SPARSE 0u         // running queries at or below which a wave runs every step kind
+#endif
 #ifndef PT_PATH_REFILL_MIN
 #define PT_PATH_REFILL_MIN 8u      // idle lanes before a query wave refills (any, once the round's work is out)
 #endif
@@ -411,7 +414,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     // Rounds exist to rebalance chains between workgroups.  Once the round's chains
     // fit in the query lanes (the tail of a pass: only the slowest pixels are left)
     // suspending gains nothing and costs a round: run them to the end.
-    const uint32_t budget = n_total <= 64u * n_waves ? 0xffffffffu : P.path_budget;
+    const uint32_t budget = n_total <= P.path_runend ? 0xffffffffu : P.path_budget;
     uint32_t bsz = n_total / n_waves;
     bsz = bsz < 1u ? 1u : (bsz > PT_BATCH ? PT_BATCH : bsz);
     const RayQ FQ = P.fq[p];
@@ -438,6 +441,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
 #ifdef PT_WPROF
     uint64_t pf_trips = 0, pf_act = 0, pf_sleep = 0, pf_ring = 0, pf_pulled = 0, pf_exit_budget = 0, pf_res = 0,
              pf_dq = 0, pf_rq = 0, pf_tripcyc = 0, pf_qlat = 0, pf_qn = 0, pf_qsteps = 0, pf_refillcyc = 0;
+    uint64_t pf_stepcyc = 0, pf_auxtrips = 0, pf_picktrips = 0, pf_stepped = 0, pf_donecyc = 0;
     uint64_t pf_t0 = __builtin_amdgcn_s_memtime(), pf_qstart = 0;
     uint32_t pf_qs = 0;
 #endif
@@ -603,6 +607,9 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
         pf_refillcyc += __builtin_amdgcn_s_memtime() - pf_t0;
         if (active) pf_qs++;
 #endif
+#ifdef PT_WPROF
+        const uint64_t pf_s0 = __builtin_amdgcn_s_memtime();
+#endif
 #if PT_PVOTE
         {
             // One replay step kind per trip besides the aux steps (the kinds' code paths
@@ -619,10 +626,22 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 if (pick == 0u && ((present >> c) & 1u)) pick = c;
             }
             if (pick) rr = pick;
-            if (kind == 0u || kind == pick) q_step(P.S, q, C, stk);
+#ifdef PT_WPROF
+            if (__ballot(kind == 0u) != 0ull) pf_auxtrips++;
+            if (pick) pf_picktrips++;
+            pf_stepped += (uint64_t)__popcll(__ballot(kind == 0u || kind == pick));
+#endif
+            // a sparse wave (few running queries) is bound by its chains' latency, not by
+            // issue: it runs every kind present
+            const bool run = 64u - nidle <= PT_PVOTE_SPARSE ? kind != 7u : (kind == 0u || kind == pick);
+            if (run) q_step(P.S, q, C, stk);
         }
 #else
         if (active && (q.phase == Q_AUX || q.phase == Q_REPLAY)) q_step(P.S, q, C, stk);
+#endif
+#ifdef PT_WPROF
+        const uint64_t pf_s1 = __builtin_amdgcn_s_memtime();
+        pf_stepcyc += pf_s1 - pf_s0;
 #endif
         // Publish the done-ring entries written before this trip: their stores were issued
         // before this trip's loads, which have completed (in-order vmcnt), so the release
@@ -662,6 +681,9 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
             }
         }
         dq_pend = dq_res;   // written this trip: published next trip
+#ifdef PT_WPROF
+        pf_donecyc += __builtin_amdgcn_s_memtime() - pf_s1;
+#endif
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane_id() == 0u) lds_write(L.dq_tail[wq], dq_res);
@@ -688,6 +710,11 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
         atomicAdd(w + 15, pf_rq);
         atomicAdd(w + 16, pf_tripcyc);
         atomicAdd(w + 21, pf_refillcyc);
+        atomicAdd(w + 22, pf_stepcyc);
+        atomicAdd(w + 23, pf_auxtrips);
+        atomicAdd(w + 24, pf_picktrips);
+        atomicAdd(w + 25, pf_stepped);
+        atomicAdd(w + 26, pf_donecyc);
     }
     if (P.wg_prof) {
         unsigned long long* w = P.wg_prof + 32ull * blockIdx.x;

@@ -98,7 +98,7 @@ struct pt_session {
     bool wave = false;
     bool path = false;            // path engine (k_wpath) rounds instead of {k_wisect, k_wshade}
     pt::F4* ring = nullptr;       // path engine: path_grid * PT_RING_F4
-    uint32_t path_grid = 0, path_budget = 256;
+    uint32_t path_grid = 0, path_budget = 256, path_runend = 0;
     uint32_t* pstate = nullptr;
     uint32_t* nsamp = nullptr;    // samples completed per slot
     pt::F4* qbuf = nullptr;       // 8 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd
@@ -114,6 +114,7 @@ struct pt_session {
     double kernel_ms = 0.0, resolve_ms = 0.0, isect_ms = 0.0;
     uint64_t isect_launches = 0;
     uint64_t samples_done = 0;
+    uint32_t deferred_spp = 0;    // wavefront engine: trace() calls not yet run (one pass at the next sync point)
     pt::CamView cam{};
     int traversal = PT_TRAVERSAL_REPLAY;
 };
@@ -593,6 +594,10 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         if (const char* b = getenv("PT_PATH_BUDGET")) ss->path_budget = (uint32_t)std::max(1, atoi(b));
         ss->path_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * 3u;
         if (const char* g = getenv("PT_PATH_WG_PER_CU")) ss->path_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * (uint32_t)std::max(1, atoi(g));
+        // a round whose chains are this few runs them to the end of the pass (a few
+        // per query wave: rebalancing them costs more rounds than it saves)
+        ss->path_runend = ss->path_grid * PT_NQ * 4u;
+        if (const char* b = getenv("PT_PATH_RUNEND")) ss->path_runend = (uint32_t)std::max(0, atoi(b));
         if (ss->path && hipMalloc(&ss->ring, (size_t)ss->path_grid * PT_RING_F4 * sizeof(pt::F4)) != hipSuccess)
             return cleanup(fail(PT_E_OOM, "device allocation failed (path rings)"));
     }
@@ -661,6 +666,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.straggler_steps = ss->straggler_steps;
     wp.path = ss->path ? 1u : 0u;
     wp.path_budget = ss->path_budget;
+    wp.path_runend = ss->path_runend;
     wp.ring = ss->ring;
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
@@ -723,11 +729,30 @@ int trace_wave(pt_session* ss, uint32_t spp) {
 }
 }  // namespace
 
+// run the coalesced trace() calls of the wavefront engine as one pass
+static int flush_trace(pt_session* ss) {
+    if (!ss->deferred_spp) return PT_OK;
+    const uint32_t spp = ss->deferred_spp;
+    ss->deferred_spp = 0;
+    HIP_TRY(hipSetDevice(ss->dev));
+    return trace_wave(ss, spp);
+}
+
 int pt_session_trace(pt_session* ss, uint32_t spp) {
     if (!ss) return fail(PT_E_INVALID, "null session");
     if (spp == 0 || ss->n_tiles_local == 0) { ss->samples_done += spp; return PT_OK; }
+    if (ss->wave) {
+        // Consecutive calls are one pass: a pixel goes on with its next samples as soon
+        // as it is done with the current ones, so only the last call waits for the
+        // slowest pixel.  The pass runs at the next resolve / sync / stats.
+        if (ss->deferred_spp > 0xffffffffu - spp) {
+            const int rc = flush_trace(ss);
+            if (rc) return rc;
+        }
+        ss->deferred_spp += spp;
+        return PT_OK;
+    }
     HIP_TRY(hipSetDevice(ss->dev));
-    if (ss->wave) return trace_wave(ss, spp);
     DevScene& ds = ss->sc->dev[ss->dev];
     pt::TraceParams tp;
     const pt_scene* s = ss->sc;
@@ -790,6 +815,7 @@ int pt_session_trace(pt_session* ss, uint32_t spp) {
 int pt_session_resolve(pt_session* ss, uint8_t* dev_out, float* dev_radiance) {
     if (!ss) return fail(PT_E_INVALID, "null session");
     if (ss->n_tiles_local == 0) return PT_OK;
+    if (const int rc = flush_trace(ss)) return rc;
     HIP_TRY(hipSetDevice(ss->dev));
     pt::ResolveParams rp;
     rp.st = ss->st;
@@ -813,6 +839,7 @@ int pt_session_resolve(pt_session* ss, uint8_t* dev_out, float* dev_radiance) {
 
 int pt_session_sync(pt_session* ss) {
     if (!ss) return fail(PT_E_INVALID, "null session");
+    if (const int rc = flush_trace(ss)) return rc;
     HIP_TRY(hipSetDevice(ss->dev));
     HIP_TRY(hipStreamSynchronize(ss->stream));
     return finish_pending(ss);
@@ -867,7 +894,11 @@ int pt_session_stats(pt_session* ss, pt_stats* st) {
     return PT_OK;
 }
 
-void* pt_session_stream(pt_session* ss) { return ss ? (void*)ss->stream : nullptr; }
+void* pt_session_stream(pt_session* ss) {
+    if (!ss) return nullptr;
+    (void)flush_trace(ss);   // work ordered after the stream sees every trace() so far (errors: pt_last_error)
+    return (void*)ss->stream;
+}
 
 void pt_session_free(pt_session* ss) {
     if (!ss) return;

@@ -26,3 +26,6 @@ print("QW trip samples: mean resident %.1f, done-ring %.1f, ray-ring %.1f; chain
          tot[12] / max(len(span) * G * 3, 1)))
 print("QW cycles per trip %.0f (refill part %.0f); query latency %.0f cycles over %.1f trips (%d queries)"
       % (tot[16] / max(tot[2], 1), tot[21] / max(tot[2], 1), tot[17] / max(tot[18], 1), tot[19] / max(tot[18], 1), tot[18]))
+print("QW cycles per trip: refill %.0f, step %.0f, done %.0f; trips with aux lanes %.3f, with a replay kind %.3f; lanes stepped per trip %.1f"
+      % (tot[21] / max(tot[2], 1), tot[22] / max(tot[2], 1), tot[26] / max(tot[2], 1), tot[23] / max(tot[2], 1),
+         tot[24] / max(tot[2], 1), tot[25] / max(tot[2], 1)))

@@ -13,7 +13,7 @@ for i, r in enumerate(a):
     tot += span
     m = re.search(r"in fresh (\d+) carry (\d+)", L[i]) if i < len(L) else None
     n = int(m.group(1)) + int(m.group(2)) if m else -1
-    if i < 60:
+    if i < 400:
         print("round %3d n_in %7d span %8.0f us  WG dur p50 %6.0f max %6.0f" % (
             i, n, span, np.median((rr[:, 1] - rr[:, 0]) / 100.0) if len(rr) else 0, ((rr[:, 1] - rr[:, 0]) / 100.0).max() if len(rr) else 0))
 print("total span ms %.1f" % (tot / 1e3))
