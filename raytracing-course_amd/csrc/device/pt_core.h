@@ -19,6 +19,13 @@
 
 namespace pt {
 
+// true if the predicate holds on any active lane of the wave (host: that thread)
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ bool pt_any(bool p) { return __ballot(p) != 0ull; }
+#else
+inline bool pt_any(bool p) { return p; }
+#endif
+
 // ------------------------------------------------------------ vectors -----
 struct f3 { float x, y, z; };
 struct alignas(16) F4 { float x, y, z, w; };

@@ -371,30 +371,40 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
         // one wide node: PT_AUXW child entries
         C.aux++;
         const f3 oinv = mk3(q.ray.o.x * q.inv.x, q.ray.o.y * q.inv.y, q.ray.o.z * q.inv.z);
-        uint32_t next = 0xffffffffu;
+        // all PT_AUXW slab tests first, branch-free (the robust form only when a lane
+        // of the wave needs it); then the bookkeeping per entry
+        bool hit[PT_AUXW];
 #pragma unroll
         for (int k = 0; k < PT_AUXW; ++k) {
             const F4 ea = r[2 * k], eb = r[2 * k + 1];
-            const uint32_t code = f2u(eb.w);
+            hit[k] = aux_box(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, q.inv, oinv);
+        }
+        if (pt_any(q.par != 0u)) {
+#pragma unroll
+            for (int k = 0; k < PT_AUXW; ++k) {
+                const F4 ea = r[2 * k], eb = r[2 * k + 1];
+                if (q.par) hit[k] = aux_box_par(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, q.ray, q.inv, oinv);
+            }
+        }
+        uint32_t next = 0xffffffffu;
+#pragma unroll
+        for (int k = 0; k < PT_AUXW; ++k) {
             // every entry's box is conservative: a reference leaf passing it is a
             // candidate (its exact slab test runs in the candidate step -- a leaf
             // failing that test is never entered, src/bvh.cpp:188-198)
-            const bool hit = code != 0xffffffffu &&
-                             (q.par ? aux_box_par(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, q.ray, q.inv, oinv)
-                                    : aux_box(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, q.inv, oinv));
-            if (!hit) continue;
-            if (code & 0x80000000u) {
-                const uint32_t leaf = code & 0x7fffffffu;
-                if (leaf < q.lb) continue;
+            const uint32_t code = f2u(r[2 * k + 1].w);
+            const bool h = hit[k] && code != 0xffffffffu;
+            const bool leaf = h && (code & 0x80000000u) != 0u && (code & 0x7fffffffu) >= q.lb;
+            const bool inner = h && (code & 0x80000000u) == 0u;
+            if (pt_any(leaf)) {
 #ifdef PT_QDIAG
-                C.cands++;
+                if (leaf) C.cands++;
 #endif
-                q_insert(q, leaf);
-            } else if (next == 0xffffffffu) {
-                next = code;
-            } else {
-                stk.set(q.sp++, code);
+                if (leaf) q_insert(q, code & 0x7fffffffu);
             }
+            const bool push = inner && next != 0xffffffffu;
+            if (inner && next == 0xffffffffu) next = code;
+            if (push) stk.set(q.sp++, code);
         }
         if (next == 0xffffffffu && q.sp > 0u) next = stk.get(--q.sp);
         if (next != 0xffffffffu) {

@@ -394,6 +394,15 @@ struct PathRing {
 #ifndef PT_PVOTE
 #define PT_PVOTE 1                 // one replay step kind per trip, round-robin over the kinds present
 #endif
+#ifndef PT_SHADE_MIN
+#define PT_SHADE_MIN 1u            // shade batches smaller than this may be held back ...
+#endif
+#ifndef PT_SHADE_DIV
+#define PT_SHADE_DIV 4u            // ... while more than PT_SHADE_DIV x the batch chains are resident ...
+#endif
+#ifndef PT_SHADE_WAIT
+#define PT_SHADE_WAIT 2000u        // ... for at most this many shader clocks
+#endif
 #ifndef PT_PVOTE_SPARSE
 #define PT_PVOTE_SPARSE 0u         // running queries at or below which a wave runs every step kind
 #endif
@@ -739,17 +748,17 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
 #ifdef PT_WPROF
     uint64_t pf_batches = 0, pf_items = 0, pf_spin = 0, pf_cyc = 0;
 #endif
+    bool waiting = false;             // holding back a small batch (since wait_t0)
+    uint64_t wait_t0 = 0;
     for (;;) {
-        // up to 64 published entries of the done rings, starting with ring `turn`
-        uint32_t take[PT_NQ], n = 0u;
+        // published entries of the done rings (ring indices are compile-time: no scratch)
+        uint32_t av[PT_NQ], total = 0u;
 #pragma unroll
-        for (uint32_t k = 0; k < PT_NQ; ++k) {
-            const uint32_t w = (turn + k) % PT_NQ;
-            const uint32_t av = __builtin_amdgcn_readfirstlane(lds_read(L.dq_tail[w])) - head[w];
-            take[w] = av < 64u - n ? av : 64u - n;
-            n += take[w];
+        for (uint32_t w = 0; w < PT_NQ; ++w) {
+            av[w] = __builtin_amdgcn_readfirstlane(lds_read(L.dq_tail[w])) - head[w];
+            total += av[w];
         }
-        if (n == 0u) {
+        if (total == 0u) {
             if (lds_read(L.qw_done) == PT_NQ) {
                 // every query wave has left (and published): one more look, then done
                 uint32_t left = 0u;
@@ -764,6 +773,33 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
+        // A shade batch costs about the same for 1 or 64 items.  With many chains in
+        // flight (more results are on their way) hold a small batch back briefly.
+        if (total < PT_SHADE_MIN && lds_read(L.qw_done) != PT_NQ &&
+            total * PT_SHADE_DIV < (uint32_t)__builtin_amdgcn_readfirstlane(lds_read(L.resident))) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            if (!waiting) {
+                waiting = true;
+                wait_t0 = now;
+            }
+            if (now - wait_t0 < PT_SHADE_WAIT) {
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+        }
+        waiting = false;
+        // up to 64 of them, starting with ring `turn`
+        uint32_t take[PT_NQ], n = 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < PT_NQ; ++k) {
+#pragma unroll
+            for (uint32_t w = 0; w < PT_NQ; ++w) {
+                if (w == (turn + k) % PT_NQ) {
+                    take[w] = av[w] < 64u - n ? av[w] : 64u - n;
+                    n += take[w];
+                }
+            }
+        }
 #ifdef PT_WPROF
         const uint64_t c0 = __builtin_amdgcn_s_memtime();
         pf_batches++;
@@ -774,9 +810,17 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
         bool found = false;
 #pragma unroll
         for (uint32_t k = 0; k < PT_NQ; ++k) {
-            const uint32_t w = (turn + k) % PT_NQ;
-            if (!found && r < take[w]) { j = w * PT_CMAX + (head[w] + r) % PT_CMAX; found = true; }
-            else if (!found) r -= take[w];
+#pragma unroll
+            for (uint32_t w = 0; w < PT_NQ; ++w) {
+                if (w == (turn + k) % PT_NQ) {
+                    if (!found && r < take[w]) {
+                        j = w * PT_CMAX + (head[w] + r) % PT_CMAX;
+                        found = true;
+                    } else if (!found) {
+                        r -= take[w];
+                    }
+                }
+            }
         }
 #pragma unroll
         for (uint32_t w = 0; w < PT_NQ; ++w) head[w] += take[w];
