@@ -201,18 +201,18 @@ PT_HD uint32_t q_pop(Query& q) {
     return v;
 }
 
-// next candidate >= skip, or end of pass (-> next pass / done)
+// next candidate (>= skip), or end of pass (-> next pass / done).  The pass's
+// candidates are distinct (each reference leaf has one aux leaf entry), inserted
+// only if >= lb (= skip at the pass end) and popped in ascending order after
+// skip = cand + 1: the smallest one left is always >= skip.
 PT_HD void q_next_candidate(Query& q) {
-    for (;;) {
-        const uint32_t v = q_pop(q);
-        if (v == 0xffffffffu) break;
+    const uint32_t v = q_pop(q);
+    if (v != 0xffffffffu) {
         q.last = v;
-        if (v >= q.skip) {
-            q.cand = v;
-            q.walk = R_CAND;
-            q.phase = Q_REPLAY;
-            return;
-        }
+        q.cand = v;
+        q.walk = R_CAND;
+        q.phase = Q_REPLAY;
+        return;
     }
     if (q.overflow) {
         // candidates above the last processed one were dropped: another aux pass
@@ -301,23 +301,11 @@ PT_HD uint32_t q_leaf_certain(Query& q, const Node& nd) {
     q.mc = m;
     q.robust = (!q.par && t1 + m <= t2 - m && t2 - m >= 0.f) ? 1u : 0u;
     if (q.robust && lo >= t1 + m) return 1u;
-    // certain reject: node_enter's decisions on the same quotients (exact division when close)
-    if (!q.par) {
-        const float e1 = fabsf(t1) * 0x1p-20f + 1e-30f, e2 = fabsf(t2) * 0x1p-20f + 1e-30f;
-        const float d12 = t1 - t2;
-        if (e1 < 1e20f && e2 < 1e20f && fabsf(d12) > 2.f * (e1 + e2)) {
-            if (d12 > 0.f) return 0u;                                 // slab miss
-            if (fabsf(t2) > e2 && t2 < 0.f) return 0u;                // box behind the ray
-            if (fabsf(t2) > e2 && fabsf(t1) > e1 && t1 > 0.f) {
-                const float eb = 2.f * e1 + fabsf(hi) * 0x1p-22f;
-                if (fabsf(hi - t1) > eb) return hi < t1 ? 0u : 2u;    // pruned even against hi
-            } else if (fabsf(t2) > e2 && fabsf(t1) > e1) {
-                return 2u;                                            // interior: never pruned
-            }
-        }
-    }
-    if (!node_enter(nd, q.ray, q.inv, hi, q.par != 0u)) return 0u;
-    return 2u;
+    // certain reject: node_enter's decision against hi on the same quotients (its
+    // slab_approx is this computation); exact division when too close to call
+    uint32_t v = q.par ? 2u : enter_decide(t1, t2, hi);
+    if (v == 2u) v = enter_exact(nd.a, nd.b, q.ray, hi) ? 1u : 0u;
+    return v == 0u ? 0u : 2u;
 }
 
 // ---- step = addresses -> one batch of 8 x 16-B loads -> compute -------------

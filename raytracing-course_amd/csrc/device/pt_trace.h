@@ -193,18 +193,20 @@ PT_HD void slab_approx(F4 a, F4 b, const Ray& ray, f3 rinv, float& t1, float& t2
 
 // node_enter's decision from the approximate interval: 0 = not entered,
 // 1 = entered, 2 = too close to call (redo with the exact division)
+// (evaluated as a chain of selects, last test first: no branches)
 PT_HD uint32_t enter_decide(float t1, float t2, float bound) {
     const float e1 = fabsf(t1) * 0x1p-20f + 1e-30f, e2 = fabsf(t2) * 0x1p-20f + 1e-30f;
     const float d12 = t1 - t2;
-    if (!(e1 < 1e20f && e2 < 1e20f) || !(fabsf(d12) > 2.f * (e1 + e2))) return 2u;
-    if (d12 > 0.f) return 0u;                                   // t1 > t2: miss
-    if (!(fabsf(t2) > e2)) return 2u;
-    if (t2 < 0.f) return 0u;                                    // box behind the ray
-    if (!(fabsf(t1) > e1)) return 2u;
-    if (t1 < 0.f) return 1u;                                    // interior: never pruned
     const float eb = 2.f * e1 + fabsf(bound) * 0x1p-22f;
-    if (!(fabsf(bound - t1) > eb)) return 2u;
-    return bound < t1 ? 0u : 1u;
+    uint32_t v = bound < t1 ? 0u : 1u;
+    v = fabsf(bound - t1) > eb ? v : 2u;
+    v = t1 < 0.f ? 1u : v;                                      // interior: never pruned
+    v = fabsf(t1) > e1 ? v : 2u;
+    v = t2 < 0.f ? 0u : v;                                      // box behind the ray
+    v = fabsf(t2) > e2 ? v : 2u;
+    v = d12 > 0.f ? 0u : v;                                     // t1 > t2: miss
+    v = (e1 < 1e20f && e2 < 1e20f) && fabsf(d12) > 2.f * (e1 + e2) ? v : 2u;
+    return v;
 }
 
 // the exact decision (IEEE division, the reference's slab)

@@ -744,7 +744,7 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
     uint32_t head[PT_NQ];             // done rings consumed (this wave only)
 #pragma unroll
     for (uint32_t w = 0; w < PT_NQ; ++w) head[w] = 0u;
-    uint32_t tail = 0u, turn = 0u;    // ray ring published; first done ring looked at
+    uint32_t tail = 0u;               // ray ring published
 #ifdef PT_WPROF
     uint64_t pf_batches = 0, pf_items = 0, pf_spin = 0, pf_cyc = 0;
 #endif
@@ -788,43 +788,28 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
             }
         }
         waiting = false;
-        // up to 64 of them, starting with ring `turn`
+        // up to 64 of them, rings in order (a ring is never starved for long: its
+        // producer's chains are the ones the other rings are not holding)
         uint32_t take[PT_NQ], n = 0u;
 #pragma unroll
-        for (uint32_t k = 0; k < PT_NQ; ++k) {
-#pragma unroll
-            for (uint32_t w = 0; w < PT_NQ; ++w) {
-                if (w == (turn + k) % PT_NQ) {
-                    take[w] = av[w] < 64u - n ? av[w] : 64u - n;
-                    n += take[w];
-                }
-            }
+        for (uint32_t w = 0; w < PT_NQ; ++w) {
+            take[w] = av[w] < 64u - n ? av[w] : 64u - n;
+            n += take[w];
         }
 #ifdef PT_WPROF
         const uint64_t c0 = __builtin_amdgcn_s_memtime();
         pf_batches++;
         pf_items += n;
 #endif
-        // this lane's entry: ring w, position head[w] + r
-        uint32_t j = 0u, r = lane;
-        bool found = false;
+        // this lane's entry: ring w, position head[w] + (lane - entries of the rings before w)
+        uint32_t j = 0u, before = 0u;
 #pragma unroll
-        for (uint32_t k = 0; k < PT_NQ; ++k) {
-#pragma unroll
-            for (uint32_t w = 0; w < PT_NQ; ++w) {
-                if (w == (turn + k) % PT_NQ) {
-                    if (!found && r < take[w]) {
-                        j = w * PT_CMAX + (head[w] + r) % PT_CMAX;
-                        found = true;
-                    } else if (!found) {
-                        r -= take[w];
-                    }
-                }
-            }
+        for (uint32_t w = 0; w < PT_NQ; ++w) {
+            if (lane >= before && lane < before + take[w]) j = w * PT_CMAX + (head[w] + lane - before) % PT_CMAX;
+            before += take[w];
         }
 #pragma unroll
         for (uint32_t w = 0; w < PT_NQ; ++w) head[w] += take[w];
-        turn = turn + 1u == PT_NQ ? 0u : turn + 1u;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const bool have = lane < n;
         Ray ray;
