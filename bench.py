@@ -76,16 +76,13 @@ def gather_tiles(dist, packed, rank, world, width, height, device):
         dist.gather(buf, parts, dst=0)
     if rank != 0:
         return None
-    img = np.zeros((height, width, 3), np.uint8)
-    tiles_x = (width + 15) // 16
+    tiles_x, tiles_y = (width + 15) // 16, (height + 15) // 16
+    pad = np.zeros((tiles_y, tiles_x, 16, 16, 3), np.uint8)   # [ty, tx, row, col, rgb]
     for r in range(world):
         p = parts[r][: per_rank[r]].cpu().numpy().reshape(-1, 16, 16, 3)
-        for lt in range(p.shape[0]):
-            gt = lt * world + r
-            tx, ty = gt % tiles_x, gt // tiles_x
-            x0, y0 = tx * 16, ty * 16
-            w, h = min(16, width - x0), min(16, height - y0)
-            img[y0:y0 + h, x0:x0 + w] = p[lt, :h, :w]
+        gt = np.arange(p.shape[0]) * world + r                  # local tile lt is global tile lt*world + r
+        pad[gt // tiles_x, gt % tiles_x] = p
+    img = pad.transpose(0, 2, 1, 3, 4).reshape(tiles_y * 16, tiles_x * 16, 3)[:height, :width]
     return img
 
 

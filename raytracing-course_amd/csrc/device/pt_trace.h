@@ -141,7 +141,7 @@ PT_HD int bvh_exact(const SceneView& S, const Ray& ray, float cb, Stack& stk, Hi
 // reference, so they change neither the result nor any bound.  Result and
 // pruning are therefore identical to the full recursion (proof: DESIGN.md §4).
 // Per-lane word memory `L`: [0, as) aux traversal stack, [as, as+cap) candidates.
-#define PT_REPLAY_HITS 4
+#define PT_REPLAY_HITS 6   // recorded replay hits before a query hands over to the exact DFS
 
 struct ReplayCfg {
     uint32_t as;    // aux stack words

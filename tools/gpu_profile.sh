@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/prof
 rm -rf $OUT
 mkdir -p $OUT
-STEPS=${STEPS:-2}
+STEPS=${STEPS:-4}
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- \
   python3 bench.py --no-cpu-baseline --steps $STEPS --warmup 1 > $OUT/bench_kt.json 2> $OUT/bench_kt.err && echo KT_OK &&
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- \
