@@ -121,6 +121,25 @@ def cpu_baseline(pt, args):
                       % (W, H, st["rays"], dt, cores, aff, "byte-identical" if same else "DIFFERS")}
 
 
+def wall_to_ppm(config):
+    """The drop-in CLI (run.sh <scene.txt> <out.ppm>) on the whole config: process
+    start -> PPM closed (parse, reference BVH, aux BVH, upload, full render,
+    tonemap, P6 write), as the reference's `run.sh` is timed."""
+    import re
+    src = scene_file(config)
+    out = os.path.join("/tmp", "pt_bench_%s_%d.ppm" % (config, os.getpid()))
+    env = dict(os.environ, PT_STATS="1", PT_QUIET="1")
+    t0 = time.perf_counter()
+    r = subprocess.run([os.path.join(REPO, "run.sh"), src, out], env=env, capture_output=True, text=True)
+    dt = time.perf_counter() - t0
+    if r.returncode != 0:
+        raise RuntimeError(r.stderr.strip()[-300:])
+    os.unlink(out)
+    rays = int(re.search(r"rays=(\d+)", r.stderr).group(1))
+    return {"config": config, "seconds": dt, "rays": rays, "mray_s": rays / dt / 1e6,
+            "what": "run.sh <scene> <out.ppm> on one GPU, process start to PPM closed (all spp of the config)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -129,6 +148,7 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--spp-per-step", type=int, default=16, help="samples per pixel per step, per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-wallclock", action="store_true", help="skip the full-config CLI run (wall_to_ppm)")
     ap.add_argument("--cpu-sample", type=int, nargs=2, default=[480, 270])
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     ap.add_argument("--traversal", default="replay", choices=["replay", "exact"])
@@ -273,6 +293,12 @@ def main():
                 res["cpu_baseline"] = None
         else:
             res["cpu_baseline"] = None
+        if world == 1 and not args.no_wallclock:
+            try:
+                res["wall_to_ppm"] = wall_to_ppm(args.config)
+            except Exception as e:
+                log("wall-clock run failed:", e)
+                res["wall_to_ppm"] = None
         print(json.dumps(res))
     ss.close()
     scene.close()
