@@ -1038,7 +1038,9 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
         so.win_h = o.win_h;
         if ((rc = pt_session_create(s, &so, &sess[(size_t)g]))) return cleanup(rc);
     }
-    const uint32_t chunk = o.spp_per_launch ? o.spp_per_launch : std::max(1u, std::min(S, 4u));
+    // samples per trace call: one pass for all of them unless a progress bar wants
+    // about 20 updates (every sync ends a pass, and a pass ends with its slowest pixel)
+    const uint32_t chunk = o.spp_per_launch ? o.spp_per_launch : o.progress ? std::max(1u, (S + 19u) / 20u) : std::max(S, 1u);
     int last = 0;
     // one host thread per GPU drives its session (the wavefront rounds sync on
     // their own stream); thread 0 reports progress
