@@ -24,7 +24,7 @@
 //   * replay per candidate: its leaf record (certain accept / certain reject),
 //     else its ancestor list below the LCA with the last hit, 4 entries then
 //     their 4 records per step; entered leaves test one primitive per step.
-// Rays with non-finite components or a fifth replay hit take the exact stack
+// Rays with non-finite components or more than PT_REPLAY_HITS replay hits take the exact stack
 // DFS (bvh_exact) in a separate pass.
 #pragma once
 #include "pt_trace.h"
