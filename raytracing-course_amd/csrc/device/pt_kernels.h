@@ -132,6 +132,7 @@ hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s);
 hipError_t pt_launch_wave_round(pt::WaveParams p, uint32_t isect_grid, uint32_t shade_grid, hipStream_t s,
                                 hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 // path engine round: {k_wpath, k_wexact, k_wshade (exact results)}
-hipError_t pt_launch_path_round(pt::WaveParams p, uint32_t path_grid, uint32_t shade_grid, hipStream_t s,
+// sparse: the end-of-pass kernel (few chains: every step kind and several steps per trip)
+hipError_t pt_launch_path_round(pt::WaveParams p, uint32_t path_grid, uint32_t shade_grid, hipStream_t s, bool sparse,
                                 hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t pt_launch_resolve(const pt::ResolveParams& p, uint32_t n_tiles, hipStream_t s);

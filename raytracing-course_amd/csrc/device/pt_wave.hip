@@ -406,12 +406,20 @@ struct PathRing {
 #ifndef PT_PVOTE_SPARSE
 #define PT_PVOTE_SPARSE 0u         // running queries at or below which a wave runs every step kind
 #endif
+#ifndef PT_SPARSE_STEPS
+#define PT_SPARSE_STEPS 4u         // steps per trip of the sparse (end-of-pass) kernel
+#endif
 #ifndef PT_PATH_REFILL_MIN
 #define PT_PATH_REFILL_MIN 8u      // idle lanes before a query wave refills (any, once the round's work is out)
 #endif
 #define PT_NOWORK 0xffffffffu
 #define PT_CAPPED 0xfffffffeu
 
+// SPARSE: the kernel of the rounds at the end of a pass (few chains, heavy queries:
+// bound by each chain's latency, not by issue): a trip runs every step kind and
+// up to PT_SPARSE_STEPS steps.  A separate instantiation, so its registers do not
+// weigh on the main kernel.
+template <bool SPARSE>
 __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L, const PathRing& G,
                                                 uint32_t* lds_stack) {
     LdsMemN<64u * PT_NQ> stk{lds_stack + threadIdx.x};
@@ -620,7 +628,14 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
         const uint64_t pf_s0 = __builtin_amdgcn_s_memtime();
 #endif
 #if PT_PVOTE
-        {
+        if constexpr (SPARSE) {
+#pragma unroll 1
+            for (uint32_t it = 0; it < PT_SPARSE_STEPS; ++it) {
+                const bool run = active && (q.phase == Q_AUX || q.phase == Q_REPLAY);
+                if (__ballot(run) == 0ull) break;
+                if (run) q_step(P.S, q, C, stk);
+            }
+        } else {
             // One replay step kind per trip besides the aux steps (the kinds' code paths
             // would otherwise all be issued every trip): round-robin over the kinds present.
             const uint32_t kind = active && q.phase == Q_REPLAY ? 1u + q.walk : active && q.phase == Q_AUX ? 0u : 7u;
@@ -877,6 +892,7 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
     }
 }
 
+template <bool SPARSE>
 __global__ void __launch_bounds__(PT_PATH_WG) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAVES_PER_EU, PT_PATH_WAVES_PER_EU))) k_wpath(WaveParams P) {
     extern __shared__ uint32_t lds_stack[];
     __shared__ PathLds L;
@@ -893,9 +909,9 @@ __global__ void __launch_bounds__(PT_PATH_WG) __attribute__((amdgpu_waves_per_eu
     __syncthreads();
 #ifndef PT_PATH_ONLY
     if ((threadIdx.x >> 6) == PT_NQ) path_shade_wave(P, L, G);
-    else path_query_wave(P, L, G, lds_stack);
+    else path_query_wave<SPARSE>(P, L, G, lds_stack);
 #elif PT_PATH_ONLY == 1
-    path_query_wave(P, L, G, lds_stack);
+    path_query_wave<SPARSE>(P, L, G, lds_stack);
 #else
     path_shade_wave(P, L, G);
 #endif
@@ -964,13 +980,16 @@ hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t pt_launch_path_round(pt::WaveParams p, uint32_t path_grid, uint32_t shade_grid, hipStream_t s,
+hipError_t pt_launch_path_round(pt::WaveParams p, uint32_t path_grid, uint32_t shade_grid, hipStream_t s, bool sparse,
                                 hipEvent_t e0, hipEvent_t e1) {
     hipError_t e = hipMemsetAsync(p.ctl + PT_CTL_SET * (1u - p.parity), 0, 4u * PT_CTL_SET, s);
     if (e != hipSuccess) return e;
     p.path = 1u;
     if (e0 && (e = hipEventRecord(e0, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(pt::k_wpath, dim3(path_grid), dim3(PT_PATH_WG), 4u * 64u * PT_NQ * p.aux_stack, s, p);
+    if (sparse)
+        hipLaunchKernelGGL(pt::k_wpath<true>, dim3(path_grid), dim3(PT_PATH_WG), 4u * 64u * PT_NQ * p.aux_stack, s, p);
+    else
+        hipLaunchKernelGGL(pt::k_wpath<false>, dim3(path_grid), dim3(PT_PATH_WG), 4u * 64u * PT_NQ * p.aux_stack, s, p);
     if (e1 && (e = hipEventRecord(e1, s)) != hipSuccess) return e;
     const uint32_t exact_lds = 64u * 4u * (p.max_stack ? p.max_stack : 1u);
     hipLaunchKernelGGL(pt::k_wexact, dim3(64), dim3(64), exact_lds, s, p);

@@ -98,7 +98,7 @@ struct pt_session {
     bool wave = false;
     bool path = false;            // path engine (k_wpath) rounds instead of {k_wisect, k_wshade}
     pt::F4* ring = nullptr;       // path engine: path_grid * PT_RING_F4
-    uint32_t path_grid = 0, path_budget = 256, path_runend = 0;
+    uint32_t path_grid = 0, path_budget = 256, path_runend = 0, path_sparse = 0;
     uint32_t* pstate = nullptr;
     uint32_t* nsamp = nullptr;    // samples completed per slot
     pt::F4* qbuf = nullptr;       // 8 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd
@@ -598,6 +598,9 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // per query wave: rebalancing them costs more rounds than it saves)
         ss->path_runend = ss->path_grid * PT_NQ * 4u;
         if (const char* b = getenv("PT_PATH_RUNEND")) ss->path_runend = (uint32_t)std::max(0, atoi(b));
+        // rounds with fewer chains than this run the end-of-pass (sparse) kernel
+        ss->path_sparse = ss->path_grid * PT_NQ * 32u;
+        if (const char* b = getenv("PT_PATH_SPARSE")) ss->path_sparse = (uint32_t)std::max(0, atoi(b));
         if (ss->path && hipMalloc(&ss->ring, (size_t)ss->path_grid * PT_RING_F4 * sizeof(pt::F4)) != hipSuccess)
             return cleanup(fail(PT_E_OOM, "device allocation failed (path rings)"));
     }
@@ -676,6 +679,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     // rounds until no fresh ray and no suspended query is left; counts are
     // checked every few rounds (empty rounds are cheap, syncs are not free)
     uint32_t p = 0, batch = 4;
+    bool sparse = false;   // the chains of the last counted round are few: end-of-pass kernel
     for (uint32_t guard = 0;; ++guard) {
         for (uint32_t r = 0; r < batch; ++r) {
             wp.parity = p;
@@ -694,7 +698,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             ss->pending_isect.emplace_back(i0, i1);
             ss->isect_launches++;
             if (ss->path)
-                HIP_TRY(pt_launch_path_round(wp, ss->path_grid, 64u, ss->stream, i0, i1));
+                HIP_TRY(pt_launch_path_round(wp, ss->path_grid, 64u, ss->stream, sparse, i0, i1));
             else
                 HIP_TRY(pt_launch_wave_round(wp, ss->isect_grid, ss->shade_grid, ss->stream, i0, i1));
             if (wp.wg_prof) {
@@ -721,6 +725,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
         if (ss->ctl_host[pt::C_FRESH] == 0u && ss->ctl_host[pt::C_CARRY] == 0u) break;
         if (guard > 100000u) return fail(PT_E_HIP, "wavefront rounds did not drain");
         batch = ss->ctl_host[pt::C_FRESH] + ss->ctl_host[pt::C_CARRY] > 4096u ? 4u : 2u;
+        sparse = ss->ctl_host[pt::C_FRESH] + ss->ctl_host[pt::C_CARRY] < ss->path_sparse;
     }
     HIP_TRY(hipEventRecord(e1, ss->stream));
     ss->pending.emplace_back(e0, e1);

@@ -135,7 +135,7 @@ def test_cli_drop_in_config1(pt, tmp_path):
     assert U.md5(out.read_bytes()) == M["full"]["c1"]["md5"]
 
 
-@pytest.mark.parametrize("engine", ["path", "round"])
+@pytest.mark.parametrize("engine", ["path", "path_dense", "round"])
 @pytest.mark.parametrize("straggler", ["1", "3"])
 @pytest.mark.parametrize("name", ["c3s4_win_944_520_16x16", "c4glass_s4_win_900_560_16x16", "dragon_64x64x16",
                                   "hw3s4_48x48x8"])
@@ -143,7 +143,11 @@ def test_suspended_queries_resume_bit_exact(pt, name, straggler, engine, monkeyp
     """Force the wavefront engine to suspend almost every query after 1-3 steps
     past its wave's last fetch (PT_STRAGGLER, read at session creation): queries
     then resume from the carry queue over many rounds, interleaving pixels'
-    samples arbitrarily -- results must not change."""
+    samples arbitrarily -- results must not change.  "path" lets the path engine
+    switch to its end-of-pass (sparse) kernel once few chains are left, as it does
+    by default; "path_dense" keeps the main kernel for every round."""
+    monkeypatch.setenv("PT_ENGINE", "round" if engine == "round" else "path")
+    monkeypatch.setenv("PT_PATH_SPARSE", "0" if engine == "path_dense" else "100000000")
     monkeypatch.setenv("PT_STRAGGLER", straggler)     # round engine
     monkeypatch.setenv("PT_PATH_BUDGET", straggler)   # path engine: trips after the round's work ran out
     m, img, rad = U.golden_image(name)
