@@ -225,9 +225,10 @@ def main():
         T = float(tmax[0])
         total_rays = float(tsum[1])
         # roofline of the dominant kernel (k_wpath: the path engine's persistent
-        # query + shade kernel, >99% of GPU time): algorithmic bytes per launch / mean
-        # launch time, both from rank 0; launch times are HIP events recorded around
-        # each k_wpath launch on the session's stream
+        # query + shade kernel, >99% of GPU time, both instantiations -- main and
+        # end-of-pass): algorithmic bytes per launch / mean launch time, both from
+        # rank 0; launch times are HIP events recorded around each k_wpath launch on
+        # the session's stream
         launches = max(st1["isect_launches"] - st0["isect_launches"], 1)
         isect_ms = st1["isect_ms"] - st0["isect_ms"]
         alg_bytes = (nodes * st1["node_bytes"] + ptests * st1["prim_bytes"] + auxv * st1["aux_bytes"]) / launches

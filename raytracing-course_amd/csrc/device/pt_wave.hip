@@ -406,9 +406,6 @@ struct PathRing {
 #ifndef PT_PVOTE_SPARSE
 #define PT_PVOTE_SPARSE 0u         // running queries at or below which a wave runs every step kind
 #endif
-#ifndef PT_SPARSE_STEPS
-#define PT_SPARSE_STEPS 4u         // steps per trip of the sparse (end-of-pass) kernel
-#endif
 #ifndef PT_PATH_REFILL_MIN
 #define PT_PATH_REFILL_MIN 8u      // idle lanes before a query wave refills (any, once the round's work is out)
 #endif
@@ -417,7 +414,7 @@ struct PathRing {
 
 // SPARSE: the kernel of the rounds at the end of a pass (few chains, heavy queries:
 // bound by each chain's latency, not by issue): a trip runs every step kind and
-// up to PT_SPARSE_STEPS steps.  A separate instantiation, so its registers do not
+// up to P.sparse_steps steps.  A separate instantiation, so its registers do not
 // weigh on the main kernel.
 template <bool SPARSE>
 __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L, const PathRing& G,
@@ -630,7 +627,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
 #if PT_PVOTE
         if constexpr (SPARSE) {
 #pragma unroll 1
-            for (uint32_t it = 0; it < PT_SPARSE_STEPS; ++it) {
+            for (uint32_t it = 0; it < P.sparse_steps; ++it) {
                 const bool run = active && (q.phase == Q_AUX || q.phase == Q_REPLAY);
                 if (__ballot(run) == 0ull) break;
                 if (run) q_step(P.S, q, C, stk);

@@ -98,7 +98,7 @@ struct pt_session {
     bool wave = false;
     bool path = false;            // path engine (k_wpath) rounds instead of {k_wisect, k_wshade}
     pt::F4* ring = nullptr;       // path engine: path_grid * PT_RING_F4
-    uint32_t path_grid = 0, path_budget = 256, path_runend = 0, path_sparse = 0;
+    uint32_t path_grid = 0, path_budget = 1024, path_runend = 0, path_sparse = 0, sparse_steps = 8;
     uint32_t* pstate = nullptr;
     uint32_t* nsamp = nullptr;    // samples completed per slot
     pt::F4* qbuf = nullptr;       // 8 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd
@@ -601,6 +601,7 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // rounds with fewer chains than this run the end-of-pass (sparse) kernel
         ss->path_sparse = ss->path_grid * PT_NQ * 32u;
         if (const char* b = getenv("PT_PATH_SPARSE")) ss->path_sparse = (uint32_t)std::max(0, atoi(b));
+        if (const char* b = getenv("PT_SPARSE_STEPS")) ss->sparse_steps = (uint32_t)std::max(1, atoi(b));
         if (ss->path && hipMalloc(&ss->ring, (size_t)ss->path_grid * PT_RING_F4 * sizeof(pt::F4)) != hipSuccess)
             return cleanup(fail(PT_E_OOM, "device allocation failed (path rings)"));
     }
@@ -670,6 +671,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.path = ss->path ? 1u : 0u;
     wp.path_budget = ss->path_budget;
     wp.path_runend = ss->path_runend;
+    wp.sparse_steps = ss->sparse_steps;
     wp.ring = ss->ring;
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));

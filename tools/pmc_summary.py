@@ -19,11 +19,22 @@ import os
 import shutil
 
 
-def per_kernel(path):
+def per_kernel(path, kernel=None, last=0):
+    """{kernel: ({counter: sum}, dispatches)}; with `kernel` (substring) and `last`
+    > 0, only the last `last` dispatches of the matching kernels, pooled under `kernel`."""
+    rows = list(csv.DictReader(open(path)))
+    keep = None
+    if kernel and last:
+        ids = sorted({int(r["Dispatch_Id"]) for r in rows if kernel in r["Kernel_Name"]})
+        keep = set(ids[-last:])
     vals = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
-    for r in csv.DictReader(open(path)):
+    for r in rows:
         k = r["Kernel_Name"]
+        if keep is not None:
+            if int(r["Dispatch_Id"]) not in keep:
+                continue
+            k = kernel
         vals[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k].add(r["Dispatch_Id"])
     return {k: ({c: v for c, v in d.items()}, len(disp[k])) for k, d in vals.items()}
@@ -33,11 +44,21 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("prof")
     ap.add_argument("out")
-    ap.add_argument("--kernel", default="pt::k_trace")
+    ap.add_argument("--kernel", default="pt::k_wpath",
+                    help="substring of the kernel name; every instantiation that matches is pooled (calls-weighted)")
     ap.add_argument("--key", default="c3_spp1_n1")
     ap.add_argument("--traffic-json", default=os.path.join(os.path.dirname(__file__), "..", "profiles",
                                                             "traffic.json"))
+    ap.add_argument("--timed", type=int, default=-1,
+                    help="average over the last N launches only (default: the bench's timed launches, "
+                         "roofline.launches of bench_kt.json; 0 = all launches)")
     a = ap.parse_args()
+    if a.timed < 0:
+        a.timed = 0
+        try:
+            a.timed = int(json.load(open(os.path.join(a.prof, "bench_kt.json")))["roofline"]["launches"])
+        except Exception:
+            pass
     os.makedirs(a.out, exist_ok=True)
     kt = os.path.join(a.prof, "kt")
     for f in ("run_kernel_stats.csv",):
@@ -48,14 +69,27 @@ def main():
     lines.append("| kernel | calls | avg ms | total ms | % |")
     lines.append("|---|---|---|---|---|")
     avg_ns = None
+    calls = tot_ns = 0.0
     for r in csv.DictReader(open(os.path.join(kt, "run_kernel_stats.csv"))):
         lines.append("| `%s` | %s | %.3f | %.3f | %s |" % (r["Name"][:60], r["Calls"], float(r["AverageNs"]) / 1e6,
                                                           float(r["TotalDurationNs"]) / 1e6, r["Percentage"]))
-        if r["Name"].startswith(a.kernel):
-            avg_ns = float(r["AverageNs"])
+        if a.kernel in r["Name"]:
+            calls += float(r["Calls"])
+            tot_ns += float(r["TotalDurationNs"])
+    if calls:
+        avg_ns = tot_ns / calls
+        lines += ["", "`%s` (all instantiations): %d launches, mean %.3f ms" % (a.kernel, calls, avg_ns / 1e6)]
+    if a.timed:
+        # the bench's timed region = the last `timed` launches (the warm-up pass comes first)
+        d = sorted((int(r["Dispatch_Id"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                   for r in csv.DictReader(open(os.path.join(kt, "run_kernel_trace.csv"))) if a.kernel in r["Kernel_Name"])
+        d = [x[1] for x in d[-a.timed:]]
+        avg_ns = sum(d) / len(d)
+        lines += ["`%s` over the bench's timed region (last %d launches, kernel trace): mean %.3f ms"
+                  % (a.kernel, len(d), avg_ns / 1e6)]
     # resources of the kernel from the trace
     for r in csv.DictReader(open(os.path.join(kt, "run_kernel_trace.csv"))):
-        if r["Kernel_Name"].startswith(a.kernel):
+        if a.kernel in r["Kernel_Name"]:
             lines += ["", "`%s`: VGPR %s, SGPR %s, scratch %s B, LDS (static) %s B, grid %s x wg %s" % (
                 a.kernel, r["VGPR_Count"], r["SGPR_Count"], r["Scratch_Size"], r["LDS_Block_Size"],
                 r["Grid_Size_X"], r["Workgroup_Size_X"])]
@@ -64,11 +98,16 @@ def main():
     for sub in sorted(os.listdir(a.prof)):
         p = os.path.join(a.prof, sub, "run_counter_collection.csv")
         if sub.startswith("pmc") and os.path.exists(p):
-            for k, (d, n) in per_kernel(p).items():
-                if k.startswith(a.kernel):
+            tot, nd = collections.defaultdict(float), 0
+            for k, (d, n) in per_kernel(p, a.kernel, a.timed).items():
+                if a.kernel in k:
+                    nd += n
                     for c, v in d.items():
-                        pmc[c] = v / n
-    lines += ["", "## PMC, per %s launch (separate --pmc passes)" % a.kernel, ""]
+                        tot[c] += v
+            for c, v in tot.items():
+                pmc[c] = v / nd
+    lines += ["", "## PMC, per %s launch (separate --pmc passes%s)"
+              % (a.kernel, ", last %d launches" % a.timed if a.timed else ""), ""]
     for c, v in sorted(pmc.items()):
         lines.append("* %s = %.6g" % (c, v))
     res = {}
