@@ -403,6 +403,9 @@ struct PathRing {
 #ifndef PT_SHADE_WAIT
 #define PT_SHADE_WAIT 2000u        // ... for at most this many shader clocks
 #endif
+#ifndef PT_PVOTE_K
+#define PT_PVOTE_K 1               // replay step kinds served per trip (round-robin)
+#endif
 #ifndef PT_PVOTE_SPARSE
 #define PT_PVOTE_SPARSE 0u         // running queries at or below which a wave runs every step kind
 #endif
@@ -640,13 +643,16 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
 #pragma unroll
             for (uint32_t k = 1; k <= 4u; ++k)
                 if (__ballot(kind == k) != 0ull) present |= 1u << k;
-            uint32_t pick = 0u;
+            uint32_t pick = 0u, pick2 = 0u;
 #pragma unroll
             for (uint32_t j = 1; j <= 4u; ++j) {
                 const uint32_t c = (rr + j - 1u) % 4u + 1u;
-                if (pick == 0u && ((present >> c) & 1u)) pick = c;
+                if ((present >> c) & 1u) {
+                    if (pick == 0u) pick = c;
+                    else if (PT_PVOTE_K > 1 && pick2 == 0u) pick2 = c;
+                }
             }
-            if (pick) rr = pick;
+            if (pick) rr = pick2 ? pick2 : pick;
 #ifdef PT_WPROF
             if (__ballot(kind == 0u) != 0ull) pf_auxtrips++;
             if (pick) pf_picktrips++;
@@ -654,7 +660,8 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
 #endif
             // a sparse wave (few running queries) is bound by its chains' latency, not by
             // issue: it runs every kind present
-            const bool run = 64u - nidle <= PT_PVOTE_SPARSE ? kind != 7u : (kind == 0u || kind == pick);
+            const bool run = 64u - nidle <= PT_PVOTE_SPARSE ? kind != 7u
+                                                            : (kind == 0u || kind == pick || (pick2 && kind == pick2));
             if (run) q_step(P.S, q, C, stk);
         }
 #else
