@@ -403,6 +403,9 @@ struct PathRing {
 #ifndef PT_SHADE_WAIT
 #define PT_SHADE_WAIT 2000u        // ... for at most this many shader clocks
 #endif
+#ifndef PT_ROTATE_SHADE
+#define PT_ROTATE_SHADE 0          // 1: the shade wave's index rotates with blockIdx.x
+#endif
 #ifndef PT_PVOTE_K
 #define PT_PVOTE_K 1               // replay step kinds served per trip (round-robin)
 #endif
@@ -421,8 +424,8 @@ struct PathRing {
 // weigh on the main kernel.
 template <bool SPARSE>
 __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L, const PathRing& G,
-                                                uint32_t* lds_stack) {
-    LdsMemN<64u * PT_NQ> stk{lds_stack + threadIdx.x};
+                                                uint32_t* lds_stack, uint32_t qw) {
+    LdsMemN<64u * PT_NQ> stk{lds_stack + 64u * qw + lane_id()};
     const uint32_t p = P.parity;
     const uint32_t* in = P.ctl + PT_CTL_SET * p;
     uint32_t* out = P.ctl + PT_CTL_SET * (1u - p);
@@ -443,7 +446,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     bool exhausted = false;
     uint32_t wpost = 0u;              // trips since the round's work ran out
     uint32_t trip = 0u;
-    const uint32_t wq = threadIdx.x >> 6;   // this query wave's done ring
+    const uint32_t wq = qw;                 // this query wave's done ring
 #if PT_PVOTE
     uint32_t rr = 0u;                       // replay step kind served last
 #endif
@@ -912,10 +915,13 @@ __global__ void __launch_bounds__(PT_PATH_WG) __attribute__((amdgpu_waves_per_eu
 #endif
     __syncthreads();
 #ifndef PT_PATH_ONLY
-    if ((threadIdx.x >> 6) == PT_NQ) path_shade_wave(P, L, G);
-    else path_query_wave<SPARSE>(P, L, G, lds_stack);
+    // which wave shades: rotated over the workgroups (PT_ROTATE_SHADE), so the
+    // shade waves of a CU's workgroups do not all sit on one SIMD
+    const uint32_t wave = threadIdx.x >> 6, sw = PT_ROTATE_SHADE ? blockIdx.x % (PT_NQ + 1u) : PT_NQ;
+    if (wave == sw) path_shade_wave(P, L, G);
+    else path_query_wave<SPARSE>(P, L, G, lds_stack, wave < sw ? wave : wave - 1u);
 #elif PT_PATH_ONLY == 1
-    path_query_wave<SPARSE>(P, L, G, lds_stack);
+    path_query_wave<SPARSE>(P, L, G, lds_stack, threadIdx.x >> 6);
 #else
     path_shade_wave(P, L, G);
 #endif
