@@ -22,6 +22,7 @@ launch times, and the reference CPU renderer timed on this host on a bounded
 sample of the same scene.
 """
 import argparse
+import hashlib
 import json
 import os
 import subprocess
@@ -152,6 +153,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, nargs=2, default=[480, 270])
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     ap.add_argument("--traversal", default="replay", choices=["replay", "exact"])
+    # testing the multi-process path on a one-GPU box: every rank on cuda:0, gloo collectives
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"], help=argparse.SUPPRESS)
+    ap.add_argument("--same-device", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -159,11 +163,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    if args.same_device:
+        local = 0
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+    coll_device = device if args.dist_backend == "nccl" else torch.device("cpu")   # where collectives run
 
     def barrier():
         if world > 1:
@@ -199,7 +209,7 @@ def main():
         ss.trace(spp)
     ss.resolve(dev_out=packed.data_ptr() if ss.packed_bytes else None)
     ss.sync()
-    img = gather_tiles(dist, packed[: ss.packed_bytes], rank, world, W, H, device)
+    img = gather_tiles(dist, packed[: ss.packed_bytes].to(coll_device), rank, world, W, H, coll_device)
     barrier()
     t1 = time.perf_counter()
     st1 = ss.stats()
@@ -213,7 +223,7 @@ def main():
     kms = st1["kernel_ms"] - st0["kernel_ms"]
     errs = st1["errors"]
     t = torch.tensor([elapsed, float(rays), float(nodes), float(ptests), kms, float(errs), float(auxv), float(fb)],
-                     dtype=torch.float64, device=device)
+                     dtype=torch.float64, device=coll_device)
     if world > 1:
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -284,6 +294,7 @@ def main():
             "exactness_errors": int(tsum[5]),
             "wall": {"load_s": t_prep - t_load, "prepare_bvh_s": t_sess - t_prep, "session_upload_s": t_ready - t_sess},
             "framebuffer_gathered": img is not None and img.shape == (H, W, 3),
+            "framebuffer_md5": hashlib.md5(img.tobytes()).hexdigest() if img is not None else None,
         }
         res["projected_c3_render_s"] = (256.0 / (spp * args.steps)) * T
         if world == 1 and not args.no_cpu_baseline:
