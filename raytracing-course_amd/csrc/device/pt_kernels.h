@@ -51,6 +51,7 @@ struct RayQ {                     // rays waiting for a closest-hit query
     F4* ro;                       // {o.xyz, u32 slot}
     F4* rd;                       // {d.xyz, P = closest plane t (computed by the producer)}
     int* pid;                     // the closest plane's prim (-1 none)
+    F4* ri;                       // q_prep record {1/d.xyz, dl | par | exact} (computed by the producer)
 };
 struct DoneQ {                    // finished queries, input of the shade kernel
     F4* ro;                       // {o.xyz, u32 slot}
@@ -111,7 +112,7 @@ struct WaveParams {
 #define PT_CMAX 512u
 #endif
 // per workgroup: ray ring ro, rd; PT_NQ done rings ro, rd; ray-ring plane ids
-#define PT_RING_F4 ((2u + 2u * PT_NQ) * PT_CMAX + PT_CMAX / 4u)
+#define PT_RING_F4 ((3u + 2u * PT_NQ) * PT_CMAX + PT_CMAX / 4u)
 
 struct ResolveParams {
     PixelState st;

@@ -153,13 +153,30 @@ PT_HD void q_planes(const SceneView& S, const Ray& ray, float& P, int& pid) {
     }
 }
 
-// BVH query set-up for a ray whose plane result (P, pid) is known
-PT_HD void q_init(const SceneView& S, const Ray& ray, float P, int pid, Query& q) {
+// Per-ray set-up a query needs, computed once by the ray's producer (so the
+// IEEE divisions run on the producer's full wave, not on the few lanes a query
+// wave refills): {1/d.xyz, dl}; dl < 0 (sign bit) marks a ray with a
+// near-zero direction component (par), NaN a non-finite ray (exact stack DFS:
+// its NaN/inf slab semantics are not replayed).
+PT_HD F4 q_prep(const SceneView& S, const Ray& ray) {
+    const float big = 3e38f;
+    if (!(fabsf(ray.o.x) < big && fabsf(ray.o.y) < big && fabsf(ray.o.z) < big && fabsf(ray.d.x) < big &&
+          fabsf(ray.d.y) < big && fabsf(ray.d.z) < big))
+        return F4{0.f, 0.f, 0.f, __builtin_nanf("")};
+    const bool par = !replay_ok_ray(ray);
+    const float om = fmaxf(fmaxf(fabsf(ray.o.x), fabsf(ray.o.y)), fabsf(ray.o.z));
+    const float dm = fminf(fminf(fabsf(ray.d.x), fabsf(ray.d.y)), fabsf(ray.d.z));
+    // non-par: dm > 1e-30 and a positive numerator, so dl is +finite or +inf
+    const float dl = par ? -INFINITY : 0x1p-18f * (S.box_extent + om) / dm;
+    return F4{1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z, dl};
+}
+
+// BVH query set-up for a ray whose plane result (P, pid) and q_prep record are known
+PT_HD void q_init_pre(const Ray& ray, float P, int pid, F4 pre, Query& q) {
     q.ray = ray;
     q.res_id = pid;
     q.res_t = P;
-    const float closest = P;
-    q.P = closest;
+    q.P = P;
     q.bt = PT_INF;
     q.nh = 0;
     q.lb = 0;
@@ -168,19 +185,14 @@ PT_HD void q_init(const SceneView& S, const Ray& ray, float P, int pid, Query& q
     q.sp = 0;
 #pragma unroll
     for (int i = 0; i < PT_QK; ++i) q.c[i] = 0xffffffffu;
-    // non-finite rays: exact stack DFS (their NaN/inf slab semantics are not replayed)
-    const float big = 3e38f;
-    if (!(fabsf(ray.o.x) < big && fabsf(ray.o.y) < big && fabsf(ray.o.z) < big && fabsf(ray.d.x) < big &&
-          fabsf(ray.d.y) < big && fabsf(ray.d.z) < big)) {
-        q.phase = Q_EXACT;
-        return;
-    }
-    q.par = replay_ok_ray(ray) ? 0u : 1u;
-    q.inv = mk3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
-    const float om = fmaxf(fmaxf(fabsf(ray.o.x), fabsf(ray.o.y)), fabsf(ray.o.z));
-    const float dm = fminf(fminf(fabsf(ray.d.x), fabsf(ray.d.y)), fabsf(ray.d.z));
-    q.dl = q.par ? INFINITY : 0x1p-18f * (S.box_extent + om) / dm;
-    q.phase = Q_AUX;
+    q.inv = mk3(pre.x, pre.y, pre.z);
+    q.par = signbit(pre.w) ? 1u : 0u;
+    q.dl = fabsf(pre.w);
+    q.phase = pre.w != pre.w ? Q_EXACT : Q_AUX;
+}
+
+PT_HD void q_init(const SceneView& S, const Ray& ray, float P, int pid, Query& q) {
+    q_init_pre(ray, P, pid, q_prep(S, ray), q);
 }
 
 PT_HD void q_insert(Query& q, uint32_t v) {

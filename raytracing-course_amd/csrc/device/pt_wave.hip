@@ -59,6 +59,7 @@ __device__ __forceinline__ void push_ray(const WaveParams& P, const RayQ& Q, uin
     Q.ro[qi] = F4{ray.o.x, ray.o.y, ray.o.z, u2f(slot)};
     Q.rd[qi] = F4{ray.d.x, ray.d.y, ray.d.z, pt};
     Q.pid[qi] = pid;
+    Q.ri[qi] = q_prep(P.S, ray);
 }
 
 // src/scene.cpp:193-196: one sample's jitter draws and camera ray
@@ -252,7 +253,7 @@ __global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
                     slot = f2u(o.w);
                     rays++;
                     C.planes += P.S.n_planes;
-                    q_init(P.S, ray, d.w, FQ.pid[fi], q);
+                    q_init_pre(ray, d.w, FQ.pid[fi], FQ.ri[fi], q);
                     if (q.phase == Q_EXACT) init_exact++;
                 } else {
                     // resume a suspended query: state, slot, then its aux stack into LDS
@@ -384,6 +385,7 @@ struct PathRing {
     F4* rq_ro;                    // ray ring: {o.xyz, slot}
     F4* rq_rd;                    //           {d.xyz, P}
     int* rq_pid;                  //           closest plane
+    F4* rq_ri;                    //           q_prep record
     F4* dq_ro;                    // done rings (PT_NQ x PT_CMAX): {o.xyz, slot}
     F4* dq_rd;                    //                               {d.xyz, u32 closest prim | 0xffffffff}
 };
@@ -590,17 +592,19 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 active = true;
             } else if (src != 0u) {
                 // a fresh ray of the round, or a chain's next ray from the ray ring
-                F4 o, d;
+                F4 o, d, pre;
                 int pid;
                 if (src == 1u) {
                     const uint32_t fi = gi - n_carry;
                     o = FQ.ro[fi];
                     d = FQ.rd[fi];
                     pid = FQ.pid[fi];
+                    pre = FQ.ri[fi];
                 } else {
                     o = G.rq_ro[gi];
                     d = G.rq_rd[gi];
                     pid = G.rq_pid[gi];
+                    pre = G.rq_ri[gi];
                 }
                 Ray ray;
                 ray.o = mk3(o.x, o.y, o.z);
@@ -612,7 +616,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 pf_qstart = __builtin_amdgcn_s_memtime();
                 pf_qs = 0;
 #endif
-                q_init(P.S, ray, d.w, pid, q);
+                q_init_pre(ray, d.w, pid, pre, q);
                 if (q.phase == Q_EXACT) init_exact++;
                 active = true;
             }
@@ -761,7 +765,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
 __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L, const PathRing& G) {
     uint32_t* out = P.ctl + PT_CTL_SET * (1u - P.parity);
     const RayQ N = P.fq[1u - P.parity];
-    const RayQ RQ{G.rq_ro, G.rq_rd, G.rq_pid};
+    const RayQ RQ{G.rq_ro, G.rq_rd, G.rq_pid, G.rq_ri};
     const uint32_t lane = lane_id();
     uint32_t head[PT_NQ];             // done rings consumed (this wave only)
 #pragma unroll
@@ -882,19 +886,21 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
     for (uint32_t b = h; b < tail; b += 64u) {
         const uint32_t i = b + lane;
         const bool has = i < tail;
-        F4 o, d;
+        F4 o, d, pre;
         int pid = -1;
         if (has) {
             const uint32_t e = i % PT_CMAX;
             o = G.rq_ro[e];
             d = G.rq_rd[e];
             pid = G.rq_pid[e];
+            pre = G.rq_ri[e];
         }
         const uint32_t k = wave_append(out + C_FRESH, has);
         if (has) {
             N.ro[k] = o;
             N.rd[k] = d;
             N.pid[k] = pid;
+            N.ri[k] = pre;
         }
     }
 }
@@ -904,8 +910,8 @@ __global__ void __launch_bounds__(PT_PATH_WG) __attribute__((amdgpu_waves_per_eu
     extern __shared__ uint32_t lds_stack[];
     __shared__ PathLds L;
     F4* r = P.ring + (size_t)blockIdx.x * PT_RING_F4;
-    const PathRing G{r, r + PT_CMAX, reinterpret_cast<int*>(r + (2u + 2u * PT_NQ) * PT_CMAX), r + 2u * PT_CMAX,
-                     r + (2u + PT_NQ) * PT_CMAX};
+    const PathRing G{r, r + PT_CMAX, reinterpret_cast<int*>(r + (2u + 2u * PT_NQ) * PT_CMAX),
+                     r + (2u + 2u * PT_NQ) * PT_CMAX + PT_CMAX / 4u, r + 2u * PT_CMAX, r + (2u + PT_NQ) * PT_CMAX};
     if (threadIdx.x == 0u) {
         L.rq_head = L.rq_tail = L.resident = L.qw_done = 0u;
     }

@@ -101,7 +101,7 @@ struct pt_session {
     uint32_t path_grid = 0, path_budget = 1024, path_runend = 0, path_sparse = 0, sparse_steps = 8;
     uint32_t* pstate = nullptr;
     uint32_t* nsamp = nullptr;    // samples completed per slot
-    pt::F4* qbuf = nullptr;       // 8 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd
+    pt::F4* qbuf = nullptr;       // 10 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd, fq0.ri, fq1.ri
     uint32_t* hid = nullptr;      // n_slots (done.id)
     uint32_t* pidbuf = nullptr;   // 2 * n_slots (fresh queues' plane prims)
     uint32_t* carry = nullptr;    // 2 * carry_cap * carry_words
@@ -571,7 +571,7 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // queue would make its queries run to the end inside the round)
         ss->carry_cap = (uint32_t)n;
         if (const char* g = getenv("PT_STRAGGLER")) ss->straggler_steps = (uint32_t)std::max(1, atoi(g));
-        if (hipMalloc(&ss->pstate, n * 4) != hipSuccess || hipMalloc(&ss->qbuf, 8 * n * 16) != hipSuccess ||
+        if (hipMalloc(&ss->pstate, n * 4) != hipSuccess || hipMalloc(&ss->qbuf, 10 * n * 16) != hipSuccess ||
             hipMalloc(&ss->hid, n * 4) != hipSuccess || hipMalloc(&ss->nsamp, n * 4) != hipSuccess ||
             hipMalloc(&ss->pidbuf, 2 * n * 4) != hipSuccess ||
             hipMalloc(&ss->carry, 2ull * ss->carry_cap * ss->carry_words * 4) != hipSuccess ||
@@ -652,10 +652,10 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.pstate = ss->pstate;
     wp.nsamp = ss->nsamp;
     const size_t n = std::max<size_t>(ss->n_slots, 1);
-    wp.fq[0] = pt::RayQ{ss->qbuf, ss->qbuf + n, reinterpret_cast<int*>(ss->pidbuf)};
-    wp.fq[1] = pt::RayQ{ss->qbuf + 2 * n, ss->qbuf + 3 * n, reinterpret_cast<int*>(ss->pidbuf) + n};
+    wp.fq[0] = pt::RayQ{ss->qbuf, ss->qbuf + n, reinterpret_cast<int*>(ss->pidbuf), ss->qbuf + 8 * n};
+    wp.fq[1] = pt::RayQ{ss->qbuf + 2 * n, ss->qbuf + 3 * n, reinterpret_cast<int*>(ss->pidbuf) + n, ss->qbuf + 9 * n};
     wp.done = pt::DoneQ{ss->qbuf + 4 * n, ss->qbuf + 5 * n, ss->hid};
-    wp.ex = pt::RayQ{ss->qbuf + 6 * n, ss->qbuf + 7 * n, nullptr};
+    wp.ex = pt::RayQ{ss->qbuf + 6 * n, ss->qbuf + 7 * n, nullptr, nullptr};
     wp.cq[0] = ss->carry;
     wp.cq[1] = ss->carry + (size_t)ss->carry_cap * ss->carry_words;
     wp.carry_cap = ss->carry_cap;
