@@ -350,12 +350,17 @@ int finish_pending(pt_session* ss) {
         (void)hipEventDestroy(e.second);
     }
     ss->pending.clear();
+    const char* rlog = getenv("PT_ROUNDLOG");   // diagnostics: per-launch ms of the rounds, one line per sync
+    const bool log = rlog && *rlog == '1' && !ss->pending_isect.empty();
+    if (log) fprintf(stderr, "rounds_ms");
     for (auto& e : ss->pending_isect) {
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) ss->isect_ms += ms;
+        if (log) fprintf(stderr, " %.3f", ms);
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
     }
+    if (log) fprintf(stderr, "\n");
     ss->pending_isect.clear();
     return PT_OK;
 }
@@ -724,6 +729,19 @@ int trace_wave(pt_session* ss, uint32_t spp) {
         }
         HIP_TRY(hipMemcpyAsync(ss->ctl_host, ss->ctl + PT_CTL_SET * p, 8, hipMemcpyDeviceToHost, ss->stream));
         HIP_TRY(hipStreamSynchronize(ss->stream));
+        if (const char* rl = getenv("PT_ROUNDLOG"); rl && *rl == '2') {
+            // diagnostics: how far behind the pass target the unfinished pixels are
+            std::vector<uint32_t> ns(ss->n_slots);
+            HIP_TRY(hipMemcpy(ns.data(), ss->nsamp, ns.size() * 4, hipMemcpyDeviceToHost));
+            std::vector<uint32_t> lag;
+            for (uint32_t v : ns)
+                if (v < wp.target) lag.push_back(wp.target - v);
+            std::sort(lag.begin(), lag.end());
+            const size_t m = lag.size();
+            fprintf(stderr, "round %u chains %u+%u unfinished %zu lag p50 %u p90 %u p99 %u max %u\n", ss->rounds,
+                    ss->ctl_host[pt::C_FRESH], ss->ctl_host[pt::C_CARRY], m, m ? lag[m / 2] : 0u,
+                    m ? lag[m * 9 / 10] : 0u, m ? lag[m * 99 / 100] : 0u, m ? lag[m - 1] : 0u);
+        }
         if (ss->ctl_host[pt::C_FRESH] == 0u && ss->ctl_host[pt::C_CARRY] == 0u) break;
         if (guard > 100000u) return fail(PT_E_HIP, "wavefront rounds did not drain");
         batch = ss->ctl_host[pt::C_FRESH] + ss->ctl_host[pt::C_CARRY] > 4096u ? 4u : 2u;
