@@ -54,6 +54,13 @@ int pt_scene_load_mem(const char* text, size_t len, pt_scene** out);
  * list, and the device-side layouts.  Host-only; no GPU needed. */
 int pt_scene_prepare(pt_scene* s);
 
+/* Optional start-up of the HIP runtime on `device`: context creation and the
+ * kernels' code objects (no launch).  No reference counterpart: a caller may run
+ * it on a second thread while Scene::Load / InitScene parse and build on the
+ * CPU, so the runtime's start-up does not add to the wall-clock (cli/main.cpp).
+ * pt_render does the same work itself when it has not been done. */
+int pt_device_init(int device);
+
 typedef struct pt_scene_info {
     uint32_t width, height, samples, ray_depth;
     uint32_t n_prims, n_bvh_prims, n_planes, n_emitters;

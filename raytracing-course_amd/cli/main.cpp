@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <thread>
 #include <vector>
 
 #include "pt.h"
@@ -23,8 +24,16 @@ int main(int argc, char** argv) {
         fprintf(stderr, "usage: %s <scene.txt> <out.ppm>\n", argv[0]);
         return 2;
     }
+    const int ngpu = env_int("PT_NGPU", 1), dev0 = env_int("PT_DEVICE", 0);
+    // the HIP runtime starts on a second thread while the scene is parsed and its
+    // BVH built (errors surface again, from pt_render)
+    std::thread warm([=] {
+        for (int g = 0; g < ngpu; ++g) (void)pt_device_init(dev0 + g);
+    });
     pt_scene* s = nullptr;
-    if (pt_scene_load(argv[1], &s) != PT_OK || pt_scene_prepare(s) != PT_OK) {
+    const bool ok = pt_scene_load(argv[1], &s) == PT_OK && pt_scene_prepare(s) == PT_OK;
+    warm.join();
+    if (!ok) {
         fprintf(stderr, "pt_render: %s\n", pt_last_error());
         pt_scene_free(s);
         return 1;
@@ -33,8 +42,8 @@ int main(int argc, char** argv) {
     pt_scene_get_info(s, &info);
     pt_render_opts o;
     pt_render_opts_default(&o);
-    o.ngpu = env_int("PT_NGPU", 1);
-    o.device = env_int("PT_DEVICE", 0);
+    o.ngpu = ngpu;
+    o.device = dev0;
     o.spp_per_launch = (uint32_t)env_int("PT_SPP_LAUNCH", 0);
     o.progress = env_int("PT_QUIET", 0) ? 0 : 1;
     std::vector<uint8_t> rgb((size_t)info.width * info.height * 3);

@@ -124,6 +124,8 @@ struct ResolveParams {
 
 }  // namespace pt
 
+hipError_t pt_preload_kernels_base();
+hipError_t pt_preload_kernels_wave();
 hipError_t pt_launch_init(const pt::InitParams& p, uint32_t n_tiles, hipStream_t s);
 // variant: bit 0 = filtered node tests + flat replay, bit 1 = XCD-banded tile order
 hipError_t pt_launch_trace(const pt::TraceParams& p, int variant, uint32_t lds_bytes, hipStream_t s);

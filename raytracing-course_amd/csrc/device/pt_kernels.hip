@@ -116,6 +116,10 @@ __global__ void __launch_bounds__(256) k_resolve(ResolveParams P) {
 
 // ---------------------------------------------------------------- launchers
 extern "C++" {
+hipError_t pt_preload_kernels_base() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(pt::k_init));
+}
 hipError_t pt_launch_init(const pt::InitParams& p, uint32_t n_tiles, hipStream_t s) {
     hipLaunchKernelGGL(pt::k_init, dim3(n_tiles), dim3(256), 0, s, p);
     return hipGetLastError();

@@ -988,6 +988,12 @@ __global__ void __launch_bounds__(256) k_wshade(WaveParams P) {
 }  // namespace pt
 
 extern "C++" {
+// load this file's code object onto the current device (no launch)
+hipError_t pt_preload_kernels_wave() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(pt::k_wpath<false>));
+}
+
 hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s) {
     hipError_t e = hipMemsetAsync(p.ctl, 0, 4u * 2u * PT_CTL_SET, s);
     if (e != hipSuccess) return e;

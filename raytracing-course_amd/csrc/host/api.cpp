@@ -385,6 +385,16 @@ void progress_bar(uint64_t done, uint64_t total, int& last) {
 extern "C" {
 
 const char* pt_last_error(void) { return g_err.c_str(); }
+
+int pt_device_init(int device) {
+    int rc = check_device(device);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipFree(nullptr));                // creates the device context
+    HIP_TRY(pt_preload_kernels_base());       // loads both code objects (no launch)
+    HIP_TRY(pt_preload_kernels_wave());
+    return PT_OK;
+}
 int pt_abi_version(void) { return PT_ABI_VERSION; }
 
 int pt_scene_load_mem(const char* text, size_t len, pt_scene** out) {
@@ -686,7 +696,9 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     // rounds until no fresh ray and no suspended query is left; counts are
     // checked every few rounds (empty rounds are cheap, syncs are not free)
     uint32_t p = 0, batch = 4;
-    bool sparse = false;   // the chains of the last counted round are few: end-of-pass kernel
+    // end-of-pass kernel when the chains of the last counted round are few; before
+    // the first count, the pass's pixels (at most one chain each) decide
+    bool sparse = ss->n_slots < ss->path_sparse;
     for (uint32_t guard = 0;; ++guard) {
         for (uint32_t r = 0; r < batch; ++r) {
             wp.parity = p;

@@ -77,6 +77,7 @@ _sig = {
     "pt_scene_load": (C.c_int, [C.c_char_p, C.POINTER(_P)]),
     "pt_scene_load_mem": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(_P)]),
     "pt_scene_prepare": (C.c_int, [_P]),
+    "pt_device_init": (C.c_int, [C.c_int]),
     "pt_scene_get_info": (C.c_int, [_P, C.POINTER(SceneInfo)]),
     "pt_scene_override": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "pt_scene_dump_bvh": (C.c_int, [_P, _P, C.c_size_t, _P, C.c_size_t]),

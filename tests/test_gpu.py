@@ -135,6 +135,14 @@ def test_cli_drop_in_config1(pt, tmp_path):
     assert U.md5(out.read_bytes()) == M["full"]["c1"]["md5"]
 
 
+def test_device_init(pt):
+    # optional runtime start-up (the CLI runs it beside the scene parse): idempotent,
+    # and a bad index fails loudly
+    assert pt._lib.pt_device_init(0) == pt.PT_OK
+    assert pt._lib.pt_device_init(0) == pt.PT_OK
+    assert pt._lib.pt_device_init(4096) == pt.PT_E_NO_GPU
+
+
 @pytest.mark.parametrize("engine", ["path", "path_dense", "round"])
 @pytest.mark.parametrize("straggler", ["1", "3"])
 @pytest.mark.parametrize("name", ["c3s4_win_944_520_16x16", "c4glass_s4_win_900_560_16x16", "dragon_64x64x16",

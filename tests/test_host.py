@@ -181,3 +181,9 @@ def test_render_without_gpu_fails_loudly():
         with pytest.raises(pt.PTError) as e:
             s.render()
         assert e.value.code in (pt.PT_E_NO_GPU, pt.PT_E_HIP)
+
+
+def test_device_init_without_gpu_fails_loudly():
+    if U.gpu_available():
+        pytest.skip("GPU present")
+    assert pt._lib.pt_device_init(0) in (pt.PT_E_NO_GPU, pt.PT_E_HIP)
