@@ -14,6 +14,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <thread>
 #include <stdexcept>
 #include <vector>
 
@@ -50,10 +52,7 @@ struct Builder {
     std::vector<Box> box;        // per item (reference leaf)
     std::vector<float> cen[3];
     std::vector<uint32_t> item;  // reference leaf node index per item
-    std::vector<pt::AuxNode>& out;
-    uint32_t max_depth = 0;
-
-    explicit Builder(std::vector<pt::AuxNode>& o) : out(o) {}
+    std::atomic<uint32_t> max_depth{0};
 
     static void set_child(pt::AuxNode& n, int k, const Box& b, uint32_t code) {
         float* f = reinterpret_cast<float*>(&n);
@@ -67,12 +66,16 @@ struct Builder {
         u[12 + k] = code;
     }
 
-    // returns the child code of the subtree over items [b, e) and its bounds
-    uint32_t build(uint32_t b, uint32_t e, Box& bounds, uint32_t depth) {
+    // returns the child code of the subtree over items [b, e) and its bounds; its
+    // nodes go to `out` in preorder (codes local to `out`).  Subtrees work on
+    // disjoint item ranges: a large one's first half is built on another thread
+    // into its own vector and spliced in front of the second (same preorder).
+    uint32_t build(uint32_t b, uint32_t e, Box& bounds, uint32_t depth, std::vector<pt::AuxNode>& out, int spawn) {
         bounds = empty_box();
         for (uint32_t i = b; i < e; ++i) grow(bounds, box[i]);
         if (e - b == 1) return 0x80000000u | item[b];
-        max_depth = std::max(max_depth, depth + 1);
+        for (uint32_t m = max_depth.load(); m < depth + 1 && !max_depth.compare_exchange_weak(m, depth + 1);) {
+        }
         // centroid bounds
         float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (uint32_t i = b; i < e; ++i)
@@ -130,8 +133,28 @@ struct Builder {
         const uint32_t self = (uint32_t)out.size();
         out.emplace_back();
         Box b0, b1;
-        const uint32_t c0 = build(b, mid, b0, depth + 1);
-        const uint32_t c1 = build(mid, e, b1, depth + 1);
+        uint32_t c0, c1;
+        if (spawn > 0 && e - b >= 8192u) {
+            std::vector<pt::AuxNode> v0, v1;
+            std::thread t([&] { c0 = build(b, mid, b0, depth + 1, v0, spawn - 1); });
+            c1 = build(mid, e, b1, depth + 1, v1, spawn - 1);
+            t.join();
+            const auto splice = [&out](const std::vector<pt::AuxNode>& v, uint32_t code) {
+                const uint32_t off = (uint32_t)out.size();
+                for (pt::AuxNode n : v) {
+                    uint32_t* u = reinterpret_cast<uint32_t*>(&n);
+                    for (int k = 12; k < 14; ++k)
+                        if (!(u[k] & 0x80000000u)) u[k] += off;   // internal child (0xFFFFFFFF has the bit)
+                    out.push_back(n);
+                }
+                return (code & 0x80000000u) ? code : code + off;
+            };
+            c0 = splice(v0, c0);
+            c1 = splice(v1, c1);
+        } else {
+            c0 = build(b, mid, b0, depth + 1, out, 0);
+            c1 = build(mid, e, b1, depth + 1, out, 0);
+        }
         set_child(out[self], 0, b0, c0);
         set_child(out[self], 1, b1, c1);
         return self;
@@ -142,7 +165,7 @@ struct Builder {
 
 void build_aux_bvh(const std::vector<HNode>& nodes, std::vector<pt::AuxNode>& out, uint32_t& max_depth) {
     out.clear();
-    Builder B(out);
+    Builder B;
     for (uint32_t i = 0; i < (uint32_t)nodes.size(); ++i) {
         const HNode& n = nodes[i];
         if (n.left != 0xFFFFFFFFu) continue;
@@ -163,7 +186,8 @@ void build_aux_bvh(const std::vector<HNode>& nodes, std::vector<pt::AuxNode>& ou
         max_depth = 1;
         return;
     }
-    B.build(0, (uint32_t)B.item.size(), root, 0);
+    // subtrees of >= 8192 items fork down to depth 4 (at most 16 threads)
+    B.build(0, (uint32_t)B.item.size(), root, 0, out, 4);
     max_depth = B.max_depth;
 }
 

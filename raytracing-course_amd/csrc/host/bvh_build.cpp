@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
+#include <thread>
 #include <vector>
 
 #include "pt_scene.h"
@@ -80,9 +81,12 @@ struct Builder {
     std::vector<BB> box;          // per original primitive
     std::vector<uint32_t> perm;   // position -> original primitive
     std::vector<float> cutq;
-    std::vector<HNode>& nodes;
+    std::vector<float> key;       // pos.xyz per original primitive (the sort keys)
 
-    Builder(const std::vector<HPrim>& p, uint32_t n, std::vector<HNode>& out) : P(p), nodes(out) {
+    Builder(const std::vector<HPrim>& p, uint32_t n) : P(p) {
+        key.resize(3 * (size_t)n);
+        for (uint32_t i = 0; i < n; ++i)
+            for (int a = 0; a < 3; ++a) key[3 * (size_t)i + a] = P[i].pos[a];
         box.resize(n);
         for (uint32_t i = 0; i < n; ++i) box[i] = prim_box(P[i]);
         perm.resize(n);
@@ -90,14 +94,27 @@ struct Builder {
         cutq.resize(n);
     }
 
-    void sort_axis(uint32_t first, uint32_t last, int axis) {
-        const std::vector<HPrim>& prims = P;
-        std::sort(perm.begin() + first, perm.begin() + last,
-                  [&prims, axis](uint32_t u, uint32_t v) { return prims[u].pos[axis] < prims[v].pos[axis]; });
+    // std::sort with the comparator of bvh.cpp:129-131 (and :168).  It runs on
+    // (key, primitive) pairs compared by key only: introsort's moves depend on the
+    // comparison results alone, so the permutation (ties included) is the one of
+    // sorting the Primitive objects, without an indirection per comparison.
+    struct KI {
+        float k;
+        uint32_t i;
+    };
+    void sort_axis(uint32_t first, uint32_t last, int axis, std::vector<KI>& tmp) {
+        tmp.resize(last - first);
+        for (uint32_t j = first; j < last; ++j) tmp[j - first] = KI{key[3 * (size_t)perm[j] + axis], perm[j]};
+        std::sort(tmp.begin(), tmp.end(), [](const KI& u, const KI& v) { return u.k < v.k; });
+        for (uint32_t j = first; j < last; ++j) perm[j] = tmp[j - first].i;
     }
 
-    // BVH_t::InitTree, bvh.cpp:105-179
-    uint32_t build(uint32_t first, uint32_t last) {
+    // BVH_t::InitTree, bvh.cpp:105-179, into `nodes` (preorder, indices local to it).
+    // The two subtrees of a large node work on disjoint ranges of perm / cutq, so
+    // the left one is built on another thread into its own vector and spliced in
+    // front of the right one: the same preorder as the sequential recursion.
+    uint32_t build(uint32_t first, uint32_t last, std::vector<HNode>& nodes, int spawn) {
+        thread_local std::vector<KI> tmp;
         BB bb;
         for (uint32_t i = first; i < last; ++i) extend_bb(bb, box[perm[i]]);
         HNode cur;
@@ -112,7 +129,7 @@ struct Builder {
         float opt[3] = {kInf, kInf, kInf};
         uint32_t cuts[3] = {0, 0, 0};
         for (int axis = 0; axis < 3; ++axis) {
-            sort_axis(first, last, axis);
+            sort_axis(first, last, axis, tmp);
             BB pref = box[perm[first]];
             for (uint32_t cut = first + 1; cut < last; ++cut) {
                 cutq[cut] = calc_s(pref) * (float)(cut - first);
@@ -134,14 +151,34 @@ struct Builder {
         uint32_t cut = 0;
         for (int axis = 0; axis < 3; ++axis) {
             if (optimum == opt[axis]) {
-                sort_axis(first, last, axis);  // the reference re-sorts (and may permute again)
+                sort_axis(first, last, axis, tmp);  // the reference re-sorts (and may permute again)
                 cut = cuts[axis];
                 break;
             }
         }
-        const uint32_t l = build(first, cut);
+        if (spawn > 0 && last - first >= 4096u) {
+            std::vector<HNode> ln, rn;
+            ln.reserve(2 * (size_t)(cut - first));
+            rn.reserve(2 * (size_t)(last - cut));
+            std::thread t([&] { build(first, cut, ln, spawn - 1); });
+            build(cut, last, rn, spawn - 1);
+            t.join();
+            const auto splice = [&nodes](const std::vector<HNode>& v) {
+                const uint32_t off = (uint32_t)nodes.size();
+                for (HNode n : v) {
+                    if (n.left != 0xFFFFFFFFu) n.left += off;
+                    if (n.right != 0xFFFFFFFFu) n.right += off;
+                    nodes.push_back(n);
+                }
+                return off;
+            };
+            nodes[pos].left = splice(ln);
+            nodes[pos].right = splice(rn);
+            return pos;
+        }
+        const uint32_t l = build(first, cut, nodes, 0);
         nodes[pos].left = l;
-        const uint32_t r = build(cut, last);
+        const uint32_t r = build(cut, last, nodes, 0);
         nodes[pos].right = r;
         return pos;
     }
@@ -153,8 +190,9 @@ void build_reference_bvh(std::vector<HPrim>& prims, uint32_t n, std::vector<HNod
     nodes.clear();
     if (n == 0) throw std::runtime_error("scene has no non-plane primitive (the reference aborts in BVH_t)");
     nodes.reserve(2 * (size_t)n);
-    Builder B(prims, n, nodes);
-    B.build(0, n);
+    Builder B(prims, n);
+    // subtrees of >= 4096 primitives fork down to depth 4 (at most 16 threads)
+    B.build(0, n, nodes, 4);
     std::vector<HPrim> reordered(n);
     for (uint32_t i = 0; i < n; ++i) reordered[i] = prims[B.perm[i]];
     std::copy(reordered.begin(), reordered.end(), prims.begin());
