@@ -74,7 +74,8 @@ __device__ __forceinline__ Ray camera_sample(const CamView& cam, Rng& R, uint32_
 // path end, the backward fold into the pixel sum.  Returns true with `ray` set
 // to the chain's next ray (the child, or the next sample's camera ray); false
 // when the pixel has reached this pass's target.  `ray` enters as the query ray.
-__device__ __forceinline__ bool shade_item(const WaveParams& P, uint32_t slot, Ray& ray, uint32_t hid) {
+// `sdone` returns whether a sample of the pixel ended here.
+__device__ __forceinline__ bool shade_item(const WaveParams& P, uint32_t slot, Ray& ray, uint32_t hid, bool& sdone) {
     bool emit = false;
     uint32_t nv = P.pstate[slot] & 0xffu;
     uint32_t end = PE_LIVE;
@@ -96,6 +97,7 @@ __device__ __forceinline__ bool shade_item(const WaveParams& P, uint32_t slot, R
         else if (nv >= P.depth) end = PE_CUT;   // RayTrace(.., 0) = 0
         else emit = true;
     }
+    sdone = end != PE_LIVE;
     if (end != PE_LIVE) {
         // path over: backward fold (deepest vertex first), src/scene.cpp:198 sum += ...
         f3 L = end == PE_MISS ? P.S.bg : mk3(0.f, 0.f, 0.f);
@@ -774,6 +776,7 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
 #ifdef PT_WPROF
     uint64_t pf_batches = 0, pf_items = 0, pf_spin = 0, pf_cyc = 0;
 #endif
+    uint32_t prog = 0u;               // finished samples not yet added to P.progress
     bool waiting = false;             // holding back a small batch (since wait_t0)
     uint64_t wait_t0 = 0;
     for (;;) {
@@ -840,13 +843,19 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
         const bool have = lane < n;
         Ray ray;
         uint32_t slot = 0u;
-        bool emit = false;
+        bool emit = false, sdone = false;
         if (have) {
             const F4 o = G.dq_ro[j], d = G.dq_rd[j];
             slot = f2u(o.w);
             ray.o = mk3(o.x, o.y, o.z);
             ray.d = mk3(d.x, d.y, d.z);
-            emit = shade_item(P, slot, ray, f2u(d.w));
+            emit = shade_item(P, slot, ray, f2u(d.w), sdone);
+        }
+        // finished samples for the host's progress bar: a system-scope add per ~4 k
+        prog += (uint32_t)__popcll(__ballot(sdone));
+        if (P.progress && prog >= 4096u) {
+            if (lane == 0u) __hip_atomic_fetch_add(P.progress, (unsigned long long)prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            prog = 0u;
         }
 #ifdef PT_WPROF
         if (lane < PT_NQ) lds_write(L.dq_head[lane], head[lane]);
@@ -881,6 +890,8 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
         w[1] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
+    if (P.progress && prog && lane == 0u)
+        __hip_atomic_fetch_add(P.progress, (unsigned long long)prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // the ray ring's leftovers (no query wave takes from it any more) -> next round
     const uint32_t h = lds_read(L.rq_head);
     for (uint32_t b = h; b < tail; b += 64u) {
@@ -969,7 +980,7 @@ __global__ void __launch_bounds__(256) k_wshade(WaveParams P) {
     // grid-stride with a block-uniform trip count (the block-aggregated append needs every thread)
     for (uint32_t base = blockIdx.x * 256u; base < n; base += stride) {
         const uint32_t i = base + threadIdx.x;
-        bool emit = false;
+        bool emit = false, sdone = false;
         Ray ray;
         uint32_t slot = 0u;
         const uint32_t hid = i < n ? P.done.id[i] : PT_SUSPENDED;
@@ -978,7 +989,12 @@ __global__ void __launch_bounds__(256) k_wshade(WaveParams P) {
             slot = f2u(o.w);
             ray.o = mk3(o.x, o.y, o.z);
             ray.d = mk3(d.x, d.y, d.z);
-            emit = shade_item(P, slot, ray, hid);
+            emit = shade_item(P, slot, ray, hid, sdone);
+        }
+        if (P.progress) {
+            const uint32_t nd = (uint32_t)__popcll(__ballot(sdone));
+            if (nd && (threadIdx.x & 63u) == 0u)
+                __hip_atomic_fetch_add(P.progress, (unsigned long long)nd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         const uint32_t qn = block_append<4u>(out + C_FRESH, emit, agg);
         if (emit) push_ray(P, N, qn, ray, slot);

@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <array>
 #include <chrono>
+#include <functional>
 #include <fstream>
 #include <map>
 #include <mutex>
@@ -115,6 +116,11 @@ struct pt_session {
     uint64_t isect_launches = 0;
     uint64_t samples_done = 0;
     uint32_t deferred_spp = 0;    // wavefront engine: trace() calls not yet run (one pass at the next sync point)
+    // optional progress report during a pass (pt_render's bar): finished samples,
+    // counted by the kernels into host-mapped memory and polled at the round syncs
+    std::function<void(uint64_t)> on_progress;
+    unsigned long long* prog_host = nullptr;
+    unsigned long long* prog_dev = nullptr;
     pt::CamView cam{};
     int traversal = PT_TRAVERSAL_REPLAY;
 };
@@ -363,6 +369,17 @@ int finish_pending(pt_session* ss) {
     if (log) fprintf(stderr, "\n");
     ss->pending_isect.clear();
     return PT_OK;
+}
+
+uint64_t owned_pixels(const pt_session* ss) {
+    uint64_t px = 0;
+    for (uint32_t t = 0; t < ss->n_tiles_local; ++t) {
+        const uint32_t gt = t * ss->tm.world + ss->tm.rank;
+        const uint32_t tx = gt % ss->tm.tiles_x, ty = gt / ss->tm.tiles_x;
+        const uint32_t w = std::min(16u, ss->tm.ww - tx * 16u), h = std::min(16u, ss->tm.wh - ty * 16u);
+        px += (uint64_t)w * h;
+    }
+    return px;
 }
 
 void progress_bar(uint64_t done, uint64_t total, int& last) {
@@ -688,6 +705,12 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.path_runend = ss->path_runend;
     wp.sparse_steps = ss->sparse_steps;
     wp.ring = ss->ring;
+    if (ss->on_progress && !ss->prog_host) {
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ss->prog_host), 8, hipHostMallocMapped | hipHostMallocCoherent));
+        *ss->prog_host = 0ull;
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&ss->prog_dev), ss->prog_host, 0));
+    }
+    wp.progress = ss->on_progress ? ss->prog_dev : nullptr;
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
@@ -740,6 +763,15 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             p ^= 1u;
         }
         HIP_TRY(hipMemcpyAsync(ss->ctl_host, ss->ctl + PT_CTL_SET * p, 8, hipMemcpyDeviceToHost, ss->stream));
+        if (wp.progress) {
+            // report the finished samples while the rounds run
+            hipError_t e;
+            while ((e = hipStreamQuery(ss->stream)) == hipErrorNotReady) {
+                ss->on_progress(__atomic_load_n(ss->prog_host, __ATOMIC_RELAXED));
+                std::this_thread::sleep_for(std::chrono::milliseconds(2));
+            }
+            HIP_TRY(e);
+        }
         HIP_TRY(hipStreamSynchronize(ss->stream));
         if (const char* rl = getenv("PT_ROUNDLOG"); rl && *rl == '2') {
             // diagnostics: how far behind the pass target the unfinished pixels are
@@ -909,14 +941,7 @@ int pt_session_stats(pt_session* ss, pt_stats* st) {
     st->aux_visits = c[5];
     st->fallbacks = c[6];
     st->fallbacks_ray = c[7];
-    uint64_t px = 0;
-    for (uint32_t t = 0; t < ss->n_tiles_local; ++t) {
-        const uint32_t gt = t * ss->tm.world + ss->tm.rank;
-        const uint32_t tx = gt % ss->tm.tiles_x, ty = gt / ss->tm.tiles_x;
-        const uint32_t w = std::min(16u, ss->tm.ww - tx * 16u), h = std::min(16u, ss->tm.wh - ty * 16u);
-        px += (uint64_t)w * h;
-    }
-    st->samples = px * ss->samples_done;
+    st->samples = owned_pixels(ss) * ss->samples_done;
     st->kernel_ms = ss->kernel_ms;
     st->resolve_ms = ss->resolve_ms;
     st->node_bytes = sizeof(pt::Node);
@@ -948,6 +973,7 @@ void pt_session_free(pt_session* ss) {
     (void)hipFree(ss->pstate); (void)hipFree(ss->qbuf); (void)hipFree(ss->hid); (void)hipFree(ss->nsamp); (void)hipFree(ss->pidbuf);
     (void)hipFree(ss->carry); (void)hipFree(ss->ctl); (void)hipFree(ss->ring);
     if (ss->ctl_host) (void)hipHostFree(ss->ctl_host);
+    if (ss->prog_host) (void)hipHostFree(ss->prog_host);
     if (ss->stream) (void)hipStreamDestroy(ss->stream);
     delete ss;
 }
@@ -1075,10 +1101,17 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
         so.win_h = o.win_h;
         if ((rc = pt_session_create(s, &so, &sess[(size_t)g]))) return cleanup(rc);
     }
-    // samples per trace call: one pass for all of them unless a progress bar wants
-    // about 20 updates (every sync ends a pass, and a pass ends with its slowest pixel)
-    const uint32_t chunk = o.spp_per_launch ? o.spp_per_launch : o.progress ? std::max(1u, (S + 19u) / 20u) : std::max(S, 1u);
+    // samples per trace call: one pass for all of them (a pass ends with its slowest
+    // pixel, so every extra sync costs a tail).  The wavefront engine reports the
+    // bar from inside the pass; the exact-traversal renderer takes ~20 passes.
     int last = 0;
+    const bool in_pass = o.progress && sess[0]->wave;
+    const uint32_t chunk = o.spp_per_launch ? o.spp_per_launch
+                           : o.progress && !in_pass ? std::max(1u, (S + 19u) / 20u) : std::max(S, 1u);
+    if (in_pass) {
+        const uint64_t total = owned_pixels(sess[0]) * S;
+        sess[0]->on_progress = [&last, total](uint64_t n) { progress_bar(std::min(n, total), total, last); };
+    }
     // one host thread per GPU drives its session (the wavefront rounds sync on
     // their own stream); thread 0 reports progress
     std::vector<int> trc((size_t)ngpu, PT_OK);
