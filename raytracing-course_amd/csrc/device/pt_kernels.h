@@ -63,7 +63,7 @@ enum : uint32_t { PE_LIVE = 0u, PE_MISS = 1u, PE_CUT = 2u, PE_TERM = 3u };
 
 // round counters: set p = ctl + PT_CTL_SET * p; the work-batch heads are one per
 // XCD, each on its own 128-B line (C_HEADS + 32 x)
-enum : uint32_t { C_FRESH = 0u, C_CARRY = 1u, C_DONE = 3u, C_EXACT = 4u, C_HEADS = 32u };
+enum : uint32_t { C_FRESH = 0u, C_CARRY = 1u, C_DONE = 3u, C_EXACT = 4u, C_FRONT = 5u, C_BACK = 6u, C_HEADS = 32u };
 #define PT_CTL_SET 288u          // words per counter set (C_HEADS + 8 x 32)
 // statistics counters: one copy per XCD (PT_CTR_COPIES x PT_CTR_STRIDE u64), summed by the host
 #define PT_CTR_COPIES 8u

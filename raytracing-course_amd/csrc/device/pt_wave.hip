@@ -154,10 +154,36 @@ __global__ void __launch_bounds__(256) k_wcamera(WaveParams P) {
         }
         store_rng(P.st, slot, R);
     }
+    // Pull order of the pass: pixels whose camera ray enters the BVH's box first
+    // (the costly ones -- a pass ends with its slowest pixel, and pixels are pulled
+    // as capacity frees up), the others after them (k_wcamera_merge).
+    bool front = false;
+    if (want) {
+        const Node nd = P.S.nodes[0];
+        const f3 rinv = mk3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
+        float t1, t2;
+        slab_approx(nd.a, nd.b, ray, rinv, t1, t2);
+        front = t1 <= t2 && t2 > 0.f;
+    }
     __shared__ uint32_t agg[5];
     uint32_t* ctl = P.ctl + PT_CTL_SET * P.parity;
-    const uint32_t qi = block_append<4u>(ctl + C_FRESH, want, agg);
-    if (want) push_ray(P, P.fq[P.parity], qi, ray, slot);
+    const uint32_t qf = block_append<4u>(ctl + C_FRONT, want && front, agg);
+    const uint32_t qb = block_append<4u>(ctl + C_BACK, want && !front, agg);
+    if (want) push_ray(P, front ? P.fq[P.parity] : P.fq[1u - P.parity], front ? qf : qb, ray, slot);
+}
+
+// the back class after the front one: fq[1-p][0, n_back) -> fq[p][n_front + i]
+__global__ void __launch_bounds__(256) k_wcamera_merge(WaveParams P) {
+    uint32_t* ctl = P.ctl + PT_CTL_SET * P.parity;
+    const uint32_t nf = ctl[C_FRONT], nb = ctl[C_BACK];
+    const RayQ A = P.fq[P.parity], B = P.fq[1u - P.parity];
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nb; i += gridDim.x * 256u) {
+        A.ro[nf + i] = B.ro[i];
+        A.rd[nf + i] = B.rd[i];
+        A.pid[nf + i] = B.pid[i];
+        A.ri[nf + i] = B.ri[i];
+    }
+    if (blockIdx.x == 0u && threadIdx.x == 0u) ctl[C_FRESH] = nf + nb;
 }
 
 #ifndef PT_VOTE
@@ -1015,6 +1041,7 @@ hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s) {
     if (e != hipSuccess) return e;
     p.parity = 0u;
     hipLaunchKernelGGL(pt::k_wcamera, dim3(p.n_tiles_local), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(pt::k_wcamera_merge, dim3(p.n_tiles_local < 1024u ? p.n_tiles_local : 1024u), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
