@@ -575,7 +575,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
             while (given < nidle && !exhausted) {
                 uint32_t v = PT_NOWORK, cnt = 0u;
                 if (lane_id() == 0u) {
-                    if (atomicAdd(&L.resident, bsz) + bsz > PT_CMAX) {
+                    if (atomicAdd(&L.resident, bsz) + bsz > P.path_cap) {
                         atomicSub(&L.resident, bsz);   // workgroup full: its chains first
                         v = PT_CAPPED;
                     } else {

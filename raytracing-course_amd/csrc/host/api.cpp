@@ -703,6 +703,15 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.path = ss->path ? 1u : 0u;
     wp.path_budget = ss->path_budget;
     wp.path_runend = ss->path_runend;
+    // Chains a workgroup may hold: PT_CMAX when the pixels outnumber that, else a
+    // little below the pixels' fair share, so the workgroups do not fill up to
+    // uneven depths and a few chains wait, costly-first, in the queue (a rank of
+    // a large N: 261 k pixels on 768 workgroups -> 320 each, +7 %).
+    {
+        const uint64_t share = ((uint64_t)ss->n_slots + ss->path_grid - 1) / std::max(1u, ss->path_grid);
+        wp.path_cap = (uint32_t)std::min<uint64_t>(PT_CMAX, std::max<uint64_t>(256u, share * 15u / 16u));
+    }
+    if (const char* c = getenv("PT_PATH_CAP")) wp.path_cap = std::min<uint32_t>(PT_CMAX, (uint32_t)std::max(64, atoi(c)));
     wp.sparse_steps = ss->sparse_steps;
     wp.ring = ss->ring;
     if (ss->on_progress && !ss->prog_host) {
