@@ -100,6 +100,7 @@ struct WaveParams {
     uint32_t path_runend;         // a round with at most this many chains runs them to the end of the pass
     unsigned long long* progress; // optional host-mapped count of finished samples (progress bar), or null
     uint32_t path_cap;            // chains a workgroup may hold (<= PT_CMAX)
+    const uint32_t* tile_order;   // k_wcamera: block b seeds local tile tile_order[b] (null: tile b)
     uint32_t sparse_steps;        // steps per loop trip of the end-of-pass (sparse) kernel
     F4* ring;                     // per-workgroup ray/done rings, PT_RING_F4 F4 per workgroup
 };

@@ -128,9 +128,12 @@ __device__ __forceinline__ bool shade_item(const WaveParams& P, uint32_t slot, R
 }
 
 __global__ void __launch_bounds__(256) k_wcamera(WaveParams P) {
-    const uint32_t slot = blockIdx.x * 256u + threadIdx.x;
+    // blocks append in about block order: the queue follows tile_order (Z-order of
+    // the tiles, so the pixels resident together form compact image regions)
+    const uint32_t t = P.tile_order ? P.tile_order[blockIdx.x] : blockIdx.x;
+    const uint32_t slot = t * 256u + threadIdx.x;
     uint32_t x, y;
-    const bool ok = slot_pixel(P.tm, blockIdx.x, threadIdx.x, x, y);
+    const bool ok = slot_pixel(P.tm, t, threadIdx.x, x, y);
     bool want = false;
     Ray ray;
     if (ok) {

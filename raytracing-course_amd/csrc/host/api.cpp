@@ -116,6 +116,7 @@ struct pt_session {
     uint64_t isect_launches = 0;
     uint64_t samples_done = 0;
     uint32_t deferred_spp = 0;    // wavefront engine: trace() calls not yet run (one pass at the next sync point)
+    uint32_t* tile_order = nullptr;   // local tiles in Z-order of their image position (k_wcamera)
     // optional progress report during a pass (pt_render's bar): finished samples,
     // counted by the kernels into host-mapped memory and polled at the round syncs
     std::function<void(uint64_t)> on_progress;
@@ -636,6 +637,25 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         if (const char* b = getenv("PT_SPARSE_STEPS")) ss->sparse_steps = (uint32_t)std::max(1, atoi(b));
         if (ss->path && hipMalloc(&ss->ring, (size_t)ss->path_grid * PT_RING_F4 * sizeof(pt::F4)) != hipSuccess)
             return cleanup(fail(PT_E_OOM, "device allocation failed (path rings)"));
+        if (ss->n_tiles_local) {
+            // seeding order of the pass: the local tiles sorted by the Z-order (Morton)
+            // code of their tile coordinates
+            std::vector<std::pair<uint64_t, uint32_t>> key(ss->n_tiles_local);
+            for (uint32_t t = 0; t < ss->n_tiles_local; ++t) {
+                const uint32_t gt = t * ss->tm.world + ss->tm.rank;
+                const uint32_t tx = gt % ss->tm.tiles_x, ty = gt / ss->tm.tiles_x;
+                uint64_t m = 0;
+                for (int b = 0; b < 16; ++b)
+                    m |= (uint64_t)((tx >> b) & 1u) << (2 * b) | (uint64_t)((ty >> b) & 1u) << (2 * b + 1);
+                key[t] = {m, t};
+            }
+            std::sort(key.begin(), key.end());
+            std::vector<uint32_t> ord(ss->n_tiles_local);
+            for (uint32_t t = 0; t < ss->n_tiles_local; ++t) ord[t] = key[t].second;
+            if (hipMalloc(&ss->tile_order, ord.size() * 4) != hipSuccess ||
+                hipMemcpy(ss->tile_order, ord.data(), ord.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+                return cleanup(fail(PT_E_OOM, "device allocation failed (tile order)"));
+        }
     }
     if (hipMemsetAsync(ss->counters, 0, 8 * PT_CTR_COPIES * PT_CTR_STRIDE, ss->stream) != hipSuccess) return cleanup(fail(PT_E_HIP, "memset failed"));
     if (ss->n_tiles_local) {
@@ -712,6 +732,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
         wp.path_cap = (uint32_t)std::min<uint64_t>(PT_CMAX, std::max<uint64_t>(256u, share * 15u / 16u));
     }
     if (const char* c = getenv("PT_PATH_CAP")) wp.path_cap = std::min<uint32_t>(PT_CMAX, (uint32_t)std::max(64, atoi(c)));
+    wp.tile_order = getenv("PT_ROWMAJOR") ? nullptr : ss->tile_order;
     wp.sparse_steps = ss->sparse_steps;
     wp.ring = ss->ring;
     if (ss->on_progress && !ss->prog_host) {
@@ -979,6 +1000,7 @@ void pt_session_free(pt_session* ss) {
     (void)hipFree(ss->st.rng_x); (void)hipFree(ss->st.rng_saved); (void)hipFree(ss->st.rng_flag);
     (void)hipFree(ss->st.sum); (void)hipFree(ss->vscratch); (void)hipFree(ss->counters);
     (void)hipFree(ss->out); (void)hipFree(ss->rad); (void)hipFree(ss->wg_prof);
+    (void)hipFree(ss->tile_order);
     (void)hipFree(ss->pstate); (void)hipFree(ss->qbuf); (void)hipFree(ss->hid); (void)hipFree(ss->nsamp); (void)hipFree(ss->pidbuf);
     (void)hipFree(ss->carry); (void)hipFree(ss->ctl); (void)hipFree(ss->ring);
     if (ss->ctl_host) (void)hipHostFree(ss->ctl_host);
