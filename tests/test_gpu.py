@@ -131,8 +131,16 @@ def test_cli_drop_in_config1(pt, tmp_path):
     exe = U.os.path.join(U.PKG, "build", "pt_render")
     r = subprocess.run([exe, U.scene_path("c1"), str(out)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
-    assert "Loading: [ ########## 100% ]" in r.stdout
+    # the bar is reported from inside one pass (finished-sample counter): all ten steps, in order
+    bars = [l for l in r.stdout.splitlines() if l.startswith("Loading: [")]
+    assert [b.split()[-2] for b in bars] == ["%d%%" % (10 * k) for k in range(1, 11)], bars
     assert U.md5(out.read_bytes()) == M["full"]["c1"]["md5"]
+    # quiet: same bytes, no bar
+    out2 = tmp_path / "c1q.ppm"
+    r = subprocess.run([exe, U.scene_path("c1"), str(out2)], capture_output=True, text=True, timeout=300,
+                       env=dict(U.os.environ, PT_QUIET="1"))
+    assert r.returncode == 0 and "Loading" not in r.stdout, r.stderr
+    assert out2.read_bytes() == out.read_bytes()
 
 
 def test_device_init(pt):
