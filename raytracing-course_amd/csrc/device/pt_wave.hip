@@ -157,16 +157,19 @@ __global__ void __launch_bounds__(256) k_wcamera(WaveParams P) {
         }
         store_rng(P.st, slot, R);
     }
-    // Pull order of the pass: pixels whose camera ray enters the BVH's box first
+    // Pull order of the pass: pixels whose camera ray enters the BVH's boxes first
     // (the costly ones -- a pass ends with its slowest pixel, and pixels are pulled
     // as capacity frees up), the others after them (k_wcamera_merge).
     bool front = false;
     if (want) {
-        const Node nd = P.S.nodes[0];
+        // the (conservative) boxes of the aux BVH's root entries: tighter than the
+        // reference root box (+2.6 % over it)
         const f3 rinv = mk3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
-        float t1, t2;
-        slab_approx(nd.a, nd.b, ray, rinv, t1, t2);
-        front = t1 <= t2 && t2 > 0.f;
+        const f3 oinv = mk3(ray.o.x * rinv.x, ray.o.y * rinv.y, ray.o.z * rinv.z);
+        for (uint32_t k = 0; k < PT_AUXW && k < P.n_aux; ++k) {
+            const AuxSL e = P.aux[k];
+            front = front || aux_box(e.a.x, e.a.y, e.a.z, e.a.w, e.b.x, e.b.y, rinv, oinv);
+        }
     }
     __shared__ uint32_t agg[5];
     uint32_t* ctl = P.ctl + PT_CTL_SET * P.parity;
