@@ -10,21 +10,27 @@ so K steps are exactly the first K*spp of the 256 spp).  `value` = Mray/s =
 closest-hit queries (Scene::RayIntersection calls, counted on the GPU) over
 the timed region.
 
-Multi-GPU (torchrun, one process per GPU): the frame's 16x16 tiles are dealt
+Multi-GPU: one process per GPU.  `python bench.py --gpus N` (no WORLD_SIZE in
+the environment) starts the N ranks itself under torch.distributed.run before
+anything touches a GPU; under torchrun it runs as the rank it is given and
+exits non-zero if WORLD_SIZE != --gpus.  The frame's 16x16 tiles are dealt
 round-robin to ranks (no data-path collective) and every rank advances its
 pixels by spp-per-step x N samples per step, so the per-GPU work is fixed as N
 grows ("weak" scaling); the timed region ends with the framebuffer resolve
 (tonemap on device) and an RCCL gather of the packed 8-bit tiles to rank 0.
 
-Also reported: roofline of the dominant kernel (k_wpath, the persistent path
-engine: closest-hit queries + shading) from in-kernel counters and HIP-event
-launch times, and the reference CPU renderer timed on this host on a bounded
-sample of the same scene.
+Also reported: the roofline of the dominant kernel (k_wpath, the persistent
+path engine: closest-hit queries + shading) from in-kernel counters and
+HIP-event launch times, per rank; the reference CPU renderer timed on this
+host (per-config bounded samples, render only); and the wall-clock to PPM of
+the drop-in CLI on the whole config, on N GPUs in one process (PT_NGPU=N).
 """
 import argparse
 import hashlib
 import json
 import os
+import re
+import socket
 import subprocess
 import sys
 import time
@@ -33,9 +39,11 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "scenes"))
+sys.path.insert(0, os.path.join(REPO, "tools"))
 import make_scene  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+REF_MD5 = {"c1": "99f1bc9386a22892970f058bfa8114c7", "c2": "a16f6cf46a6443244ecbd0c9d856c295"}
 
 
 def log(*a):
@@ -61,6 +69,47 @@ def scene_file(config):
     return p
 
 
+# ------------------------------------------------------------------ launch --
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(args, argv):
+    """--gpus N > 1 without a torchrun environment: start N ranks (one process
+    per GPU) under torch.distributed.run as CHILD processes and return their
+    exit code.  Nothing in this process has touched a GPU (device_count does not
+    initialise the runtime on this image)."""
+    if not args.same_device and not args.probe_ranks:
+        import torch
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            log("bench: --gpus %d but only %d GPU(s) visible" % (args.gpus, have))
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + argv
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0", PT_BENCH_SPAWNED="1")
+    return subprocess.call(cmd, env=env)
+
+
+def probe_ranks(args, rank, world):
+    """CPU check of the launch path (tests/test_dist.py): every rank joins a gloo
+    group and rank 0 prints the ranks it sees.  No GPU is touched."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    got = [None] * world
+    dist.all_gather_object(got, {"rank": rank, "pid": os.getpid(), "local_rank": int(os.environ.get("LOCAL_RANK", 0))})
+    if rank == 0:
+        print(json.dumps({"probe": True, "n_gpus": world, "gpus_arg": args.gpus, "ranks": got}))
+    dist.destroy_process_group()
+    del torch
+
+
+# ------------------------------------------------------------------ tiles --
 def gather_tiles(dist, packed, rank, world, width, height, device):
     """RCCL/gloo gather of every rank's packed 8-bit tiles to rank 0 and the
     host un-interleave into the W*H*3 framebuffer (rank 0 returns it)."""
@@ -87,60 +136,199 @@ def gather_tiles(dist, packed, rank, world, width, height, device):
     return img
 
 
-def cpu_baseline(pt, args):
-    """The reference hw5 renderer (oracle/_ref, built from /root/reference by
-    oracle/build_ref.sh) on a bounded sample of the same scene; rays of the
-    sample counted by the GPU renderer (identical path decisions)."""
-    W, H = args.cpu_sample
-    src = os.path.join(REPO, "scenes", "gen", "cpu_sample_%dx%d.txt" % (W, H))
-    make_scene.make_custom(os.path.join(REPO, "scenes", "practice5_dragon_10k.txt"), W, H, 1, True, "diffuse", src)
-    ref = os.path.join(REPO, "oracle", "_ref", "raytracing_hw5")
-    port = os.path.join(REPO, "oracle", "_build", "pt_oracle")
-    out = os.path.join("/tmp", "pt_cpu_sample_%d.ppm" % os.getpid())
-    cores = os.cpu_count()
-    if os.path.exists(ref):
-        kind, cmd = "reference", [ref, src, out]
-    elif os.path.exists(port):
-        kind, cmd = "port", [port, src, out, str(cores)]
-    else:
-        return None
-    t0 = time.perf_counter()
-    subprocess.check_call(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
-    dt = time.perf_counter() - t0
-    with pt.Scene.load(src) as s:
-        gimg, _, st = s.render(device=0)
-    with open(out, "rb") as f:
-        same = f.read() == b"P6\n%d %d\n255\n" % (W, H) + gimg.tobytes()
-    os.unlink(out)
+# ------------------------------------------------------------ CPU baseline --
+def host_cpus():
+    """(usable CPUs, description): the affinity mask capped by the cgroup CPU quota."""
     try:
         aff = len(os.sched_getaffinity(0))
     except Exception:
-        aff = cores
-    return {"value": st["rays"] / dt / 1e6, "unit": "Mray/s", "cores": cores, "kind": kind,
-            "sample": "stand-in dragon %dx%d x 1 spp (%d rays, %.1f s wall, load+BVH included; "
-                      "threads = hardware_concurrency = %d, affinity %d CPUs; GPU image of the sample %s)"
-                      % (W, H, st["rays"], dt, cores, aff, "byte-identical" if same else "DIFFERS")}
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except Exception:
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return usable, {"cpu_model": model, "affinity_cpus": aff, "cgroup_quota_cpus": quota, "OMP_NUM_THREADS": omp,
+                    "os_cpu_count": os.cpu_count()}
 
 
-def wall_to_ppm(config):
+# bounded samples of every BASELINE config (render only, load + BVH timed apart):
+#   name -> (scene config, spp override, x0, y0, w, rows, row stride)
+# Rows are spread over the frame (stride) so the sample's per-ray cost is the
+# frame's, not one band's.  c1 is the full image at full spp.
+CPU_SAMPLES = {
+    "c1": ("c1", 0, 0, 0, 256, 256, 1),
+    "c2": ("c2", 0, 0, 4, 512, 8, 64),
+    "c3": ("c3", 1, 0, 9, 1920, 12, 90),
+    "c4_metal": ("c4_metal", 1, 0, 9, 1920, 6, 180),
+    "c4_glass": ("c4_glass", 1, 0, 9, 1920, 6, 180),
+    "c5": ("c5", 1, 0, 18, 3840, 4, 540),
+}
+FULL_SPP = {"c1": 16, "c2": 64, "c3": 256, "c4_metal": 1024, "c4_glass": 1024, "c5": 4096}
+
+
+def cpu_baseline(pt, args):
+    """The reference hw5 renderer on this host's CPUs: oracle/_ref/ref_harness =
+    the UNMODIFIED reference sources (Scene::Load/InitScene/Sample) around a
+    restatement of Scene::Render's pixel loop that can render a row sample and
+    times load+InitScene and the render separately.  Rays of each sample are
+    counted by the GPU renderer on the same pixels (identical path decisions;
+    the GPU image of the sample is checked byte-identical)."""
+    harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(harness):
+        return None
+    usable, cpu = host_cpus()
+    rows = {}
+    for name in args.cpu_configs:
+        cfg, spp, x0, y0, w, nrow, stride = CPU_SAMPLES[name]
+        src = scene_file(cfg)
+        if spp:
+            # the same scene text with only the SAMPLES line changed (per-sample work is i.i.d.)
+            text = open(src).read()
+            text = re.sub(r"(?m)^SAMPLES\s+\d+", "SAMPLES %d" % spp, text, count=1)
+            src = os.path.join(REPO, "scenes", "gen", "%s_spp%d.txt" % (cfg, spp))
+            if not os.path.exists(src) or open(src).read() != text:
+                open(src, "w").write(text)
+        out_ppm = "/tmp/pt_cpu_%s_%d.ppm" % (name, os.getpid())
+        out_rad = out_ppm + ".f32"
+        env = dict(os.environ, REF_THREADS=str(usable))
+        r = subprocess.run([harness, "render", src, out_ppm, out_rad, str(x0), str(y0), str(w), str(nrow), str(stride)],
+                           env=env, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("ref_harness %s: %s" % (name, r.stderr[-300:]))
+        m = dict(re.findall(r"(\w+)=([\d.]+)", r.stderr.splitlines()[-1]))
+        ref_img = open(out_ppm, "rb").read()
+        os.unlink(out_ppm)
+        os.unlink(out_rad)
+        # the GPU renders the same rows (one window per row: global-index seeds)
+        rays = 0
+        gpu_rows = []
+        with pt.Scene.load(src) as s:
+            if nrow * stride == s.info["height"] and stride == 1 and w == s.info["width"]:
+                img, _, st = s.render(device=0)
+                gpu_rows.append(img)
+                rays = st["rays"]
+            else:
+                for k in range(nrow):
+                    img, _, st = s.render(device=0, window=(x0, y0 + k * stride, w, 1))
+                    gpu_rows.append(img)
+                    rays += st["rays"]
+        gimg = np.concatenate(gpu_rows, axis=0)
+        same = ref_img == b"P6\n%d %d\n255\n" % (w, nrow) + gimg.tobytes()
+        render_s = float(m["render_s"])
+        spp_eff = spp or FULL_SPP[name]
+        row = {"render_s": render_s, "load_init_s": float(m["load_init_s"]), "rays": rays,
+               "mray_s": rays / render_s / 1e6, "msample_s": w * nrow * spp_eff / render_s / 1e6,
+               "pixels": w * nrow, "spp": spp_eff, "threads": int(m["threads"]),
+               "sample": "%d rows x %d px from row %d, stride %d, %d spp" % (nrow, w, y0, stride, spp_eff),
+               "gpu_image_identical": same}
+        if spp:
+            # config time scaled to the full spp and frame (per-sample work is i.i.d. per pixel)
+            W, H = {"c5": (3840, 2160), "c2": (512, 512)}.get(cfg, (1920, 1080))
+            row["projected_full_render_s"] = render_s * (W * H) / (w * nrow) * FULL_SPP[name] / spp
+        elif (w * nrow, stride) != (256 * 256, 1):
+            W, H = (512, 512) if cfg == "c2" else (1920, 1080)
+            row["projected_full_render_s"] = render_s * (W * H) / (w * nrow)
+        if name in REF_MD5 and nrow * stride == 256 and w == 256:
+            row["md5_matches_reference"] = hashlib.md5(ref_img).hexdigest() == REF_MD5[name]
+        rows[name] = row
+        log("cpu baseline %s: %.2f Mray/s (%d rays, %.2f s render, %d threads), GPU image %s"
+            % (name, row["mray_s"], rays, render_s, row["threads"], "identical" if same else "DIFFERS"))
+    main_row = rows.get(args.config) or next(iter(rows.values()))
+    return {"value": main_row["mray_s"], "unit": "Mray/s", "cores": main_row["threads"], "kind": "reference",
+            "sample": "config %s: %s, render only (load + InitScene %.2f s timed apart); unmodified reference "
+                      "sources (oracle/_ref/ref_harness), OpenMP threads = usable CPUs of this host"
+                      % (args.config, main_row["sample"], main_row["load_init_s"]),
+            "host": cpu, "configs": rows}
+
+
+# ------------------------------------------------------------- wall clock --
+def wall_to_ppm(config, ngpu):
     """The drop-in CLI (run.sh <scene.txt> <out.ppm>) on the whole config: process
     start -> PPM closed (parse, reference BVH, aux BVH, upload, full render,
-    tonemap, P6 write), as the reference's `run.sh` is timed."""
-    import re
+    tonemap, gather, P6 write), as the reference's `run.sh` is timed.  ngpu > 1:
+    one process drives ngpu GPUs (PT_NGPU) and gathers with RCCL."""
     src = scene_file(config)
     out = os.path.join("/tmp", "pt_bench_%s_%d.ppm" % (config, os.getpid()))
-    env = dict(os.environ, PT_STATS="1", PT_QUIET="1")
+    env = dict(os.environ, PT_STATS="1", PT_QUIET="1", PT_NGPU=str(ngpu))
+    if ngpu > 1:
+        env["PT_GATHER"] = "rccl"
     t0 = time.perf_counter()
     r = subprocess.run([os.path.join(REPO, "run.sh"), src, out], env=env, capture_output=True, text=True)
     dt = time.perf_counter() - t0
     if r.returncode != 0:
         raise RuntimeError(r.stderr.strip()[-300:])
+    md5 = hashlib.md5(open(out, "rb").read()).hexdigest()
     os.unlink(out)
-    rays = int(re.search(r"rays=(\d+)", r.stderr).group(1))
-    return {"config": config, "seconds": dt, "rays": rays, "mray_s": rays / dt / 1e6,
-            "what": "run.sh <scene> <out.ppm> on one GPU, process start to PPM closed (all spp of the config)"}
+    m = dict(re.findall(r"(\w+(?:/\w+)?)=([\d.]+)", r.stderr))
+    rays = int(m["rays"])
+    return {"config": config, "ngpu": ngpu, "seconds": dt, "rays": rays, "mray_s": rays / dt / 1e6,
+            "render_ms": float(m["wall_ms"]), "gather_rccl": int(m.get("gather_rccl", 0)), "ppm_md5": md5,
+            "what": "PT_NGPU=%d run.sh <scene> <out.ppm>: one process, process start to PPM closed "
+                    "(all spp of the config)" % ngpu}
 
 
+# -------------------------------------------------------------- roofline --
+def roofline(st0, st1, traffic_json, key):
+    """k_wpath roofline record of this rank: algorithmic bytes per launch (in-kernel
+    visit counters x record sizes) / mean launch time (HIP events on the session's
+    stream).  `traffic` = this run's algorithmic bytes x the profiled ratio of
+    memory-side bytes to algorithmic bytes (rocprofv3 FETCH/WRITE passes of the
+    same workload, profiles/traffic.json), so it scales with this run's launches."""
+    launches = max(st1["isect_launches"] - st0["isect_launches"], 1)
+    isect_ms = st1["isect_ms"] - st0["isect_ms"]
+    nodes = st1["node_visits"] - st0["node_visits"]
+    ptests = st1["prim_tests"] - st0["prim_tests"]
+    auxv = st1["aux_visits"] - st0["aux_visits"]
+    alg_bytes = (nodes * st1["node_bytes"] + ptests * st1["prim_bytes"] + auxv * st1["aux_bytes"]) / launches
+    launch_s = (isect_ms / 1e3) / launches
+    achieved = alg_bytes / launch_s / 1e9 if launch_s > 0 else 0.0
+    rec = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_wpath",
+           "alg_bytes_per_launch": alg_bytes, "launch_ms": launch_s * 1e3, "launches": launches}
+    prof = None
+    try:
+        prof = json.load(open(traffic_json)).get(key)
+    except Exception:
+        pass
+    if prof and "traffic_per_alg_byte" in prof:
+        rec["traffic"] = prof["traffic_per_alg_byte"] * alg_bytes
+        rec["traffic_per_alg_byte"] = prof["traffic_per_alg_byte"]
+        rec["traffic_source"] = ("profiles/%s: rocprofv3 --pmc FETCH_SIZE (KiB, x2 gfx950) + WRITE_SIZE (KiB) over the "
+                                 "same workload's timed launches, as a ratio to that run's algorithmic bytes, times "
+                                 "this run's algorithmic bytes per launch" % prof.get("profile", "?"))
+        for k in ("l2_hit_rate", "write_bytes_per_ray", "fetch_bytes_per_ray", "limiter", "valu_issue_frac",
+                  "wait_frac", "vgpr", "waves_per_simd"):
+            if k in prof:
+                rec[k] = prof[k]
+    rec["note"] = ("algorithmic = 4-wide aux BVH nodes (128 B) + reference node records (32 B) + compact primitive "
+                   "records (48 B) per visit; the ~25 MB working set is L2/Infinity-Cache resident; what limits the "
+                   "kernel is in `limiter` (rocprofv3 SQ counters, DESIGN.md §4)")
+    return rec
+
+
+def kernel_resources():
+    try:
+        import kernel_resources as KR
+        ks = KR.kernel("k_wpath")
+        return {("end_of_pass" if "ILb1" in k else "main"): v for k, v in ks.items()}
+    except Exception:
+        return None
+
+
+# ------------------------------------------------------------------ main --
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -150,17 +338,31 @@ def main():
     ap.add_argument("--spp-per-step", type=int, default=16, help="samples per pixel per step, per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-wallclock", action="store_true", help="skip the full-config CLI run (wall_to_ppm)")
-    ap.add_argument("--cpu-sample", type=int, nargs=2, default=[480, 270])
+    ap.add_argument("--cpu-configs", nargs="+", default=list(CPU_SAMPLES), choices=list(CPU_SAMPLES))
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     ap.add_argument("--traversal", default="replay", choices=["replay", "exact"])
     # testing the multi-process path on a one-GPU box: every rank on cuda:0, gloo collectives
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"], help=argparse.SUPPRESS)
     ap.add_argument("--same-device", action="store_true", help=argparse.SUPPRESS)
-    args = ap.parse_args()
+    ap.add_argument("--probe-ranks", action="store_true", help=argparse.SUPPRESS)
+    argv = sys.argv[1:]
+    args = ap.parse_args(argv)
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", str(args.gpus if args.gpus == 1 else 1)))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(spawn_ranks(args, argv))
+        world, rank, local = 1, 0, 0
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if world != args.gpus:
+            log("bench: WORLD_SIZE=%d but --gpus %d: refusing to report a different GPU count" % (world, args.gpus))
+            sys.exit(2)
+    if args.probe_ranks:
+        probe_ranks(args, rank, world)
+        return
+
     import torch
     import torch.distributed as dist
     if args.same_device:
@@ -224,39 +426,23 @@ def main():
     errs = st1["errors"]
     t = torch.tensor([elapsed, float(rays), float(nodes), float(ptests), kms, float(errs), float(auxv), float(fb)],
                      dtype=torch.float64, device=coll_device)
+    roof = roofline(st0, st1, args.traffic_json, "%s_n1" % args.config)
     if world > 1:
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t.clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, {"rank": rank, "mray_s": rays / elapsed / 1e6, "frac": roof["frac"],
+                                          "achieved": roof["achieved"], "launch_ms": roof["launch_ms"],
+                                          "launches": roof["launches"], "tiles": ss.n_tiles})
     else:
         tmax = tsum = t
+        per_rank = None
+    res = None
     if rank == 0:
         T = float(tmax[0])
         total_rays = float(tsum[1])
-        # roofline of the dominant kernel (k_wpath: the path engine's persistent
-        # query + shade kernel, >99% of GPU time, both instantiations -- main and
-        # end-of-pass): algorithmic bytes per launch / mean launch time, both from
-        # rank 0; launch times are HIP events recorded around each k_wpath launch on
-        # the session's stream
-        launches = max(st1["isect_launches"] - st0["isect_launches"], 1)
-        isect_ms = st1["isect_ms"] - st0["isect_ms"]
-        alg_bytes = (nodes * st1["node_bytes"] + ptests * st1["prim_bytes"] + auxv * st1["aux_bytes"]) / launches
-        launch_s = (isect_ms / 1e3) / launches
-        achieved = alg_bytes / launch_s / 1e9 if launch_s > 0 else 0.0
-        traffic = None
-        traffic_src = None
-        if os.path.exists(args.traffic_json):
-            try:
-                tj = json.load(open(args.traffic_json))
-                key = "%s_spp%d_n%d" % (args.config, spp, world)
-                if key in tj:
-                    # profiled per-launch fabric bytes x (this run's launches / the profile's):
-                    # kept per launch like `achieved`
-                    traffic = tj[key]["hbm_bytes_per_launch"]
-                    traffic_src = tj[key].get("source")
-            except Exception:
-                pass
         res = {
             "metric": "Mray/s (closest-hit queries/s), dragon stand-in 1080p, RAY_DEPTH 6",
             "value": total_rays / T / 1e6,
@@ -270,19 +456,12 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: md5-pinned 89,928-triangle dragon stand-in (SURVEY §8d), per-pixel reference seeds",
-            "config": {"workload": "config 3: %s %dx%d, %d spp per step (of 256), RAY_DEPTH %d; %s traversal of the "
-                                   "reference tree (bit-exact)" % (args.config, W, H, spp,
-                                                                   info["ray_depth"], args.traversal),
+            "config": {"workload": "config 3: %s %dx%d, %d spp per step per rank (of 256), RAY_DEPTH %d; %s "
+                                   "traversal of the reference tree (bit-exact)" % (args.config, W, H, spp,
+                                                                                     info["ray_depth"], args.traversal),
                        "pixels": W * H, "samples_per_step": W * H * spp,
                        "parallelism": "pixel tiles x%d" % world},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_wpath", "alg_bytes_per_launch": alg_bytes, "launch_ms": launch_s * 1e3,
-                         "launches": launches, "traffic_source": traffic_src,
-                         "note": "algorithmic = 4-wide aux BVH nodes (128 B) + reference node records (32 B) + "
-                                 "compact primitive records (48 B) per visit; the ~25 MB working set is "
-                                 "L2/Infinity-Cache resident, and the kernel is bound by VALU issue (divergent "
-                                 "per-lane state machines), not bandwidth (DESIGN.md §4)"},
+            "roofline": roof,
             "wavefront_rounds": int(st1["rounds"] - st0["rounds"]),
             "kernel_ms_per_step": kms / args.steps,
             "rays": total_rays,
@@ -295,8 +474,20 @@ def main():
             "wall": {"load_s": t_prep - t_load, "prepare_bvh_s": t_sess - t_prep, "session_upload_s": t_ready - t_sess},
             "framebuffer_gathered": img is not None and img.shape == (H, W, 3),
             "framebuffer_md5": hashlib.md5(img.tobytes()).hexdigest() if img is not None else None,
+            "distributed": {"world_size": world, "backend": args.dist_backend if world > 1 else None,
+                            "collective_ranks": dist.get_world_size() if world > 1 else 1,
+                            "launched_by": "bench.py --gpus" if os.environ.get("PT_BENCH_SPAWNED") else
+                                           ("torch.distributed.run" if world > 1 else "single process")},
+            "kernel_resources": kernel_resources(),
         }
+        if per_rank:
+            res["per_rank"] = per_rank
         res["projected_c3_render_s"] = (256.0 / (spp * args.steps)) * T
+    ss.close()
+    scene.close()
+    # the host-side legs run after the timed region, on rank 0 only; the other
+    # ranks wait at the final barrier (their GPUs are free for the N-GPU CLI run)
+    if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             try:
                 res["cpu_baseline"] = cpu_baseline(pt, args)
@@ -305,16 +496,16 @@ def main():
                 res["cpu_baseline"] = None
         else:
             res["cpu_baseline"] = None
-        if world == 1 and not args.no_wallclock:
+        if not args.no_wallclock:
+            ngpu = world if not args.same_device else 1
             try:
-                res["wall_to_ppm"] = wall_to_ppm(args.config)
+                res["wall_to_ppm"] = wall_to_ppm(args.config, ngpu)
             except Exception as e:
                 log("wall-clock run failed:", e)
                 res["wall_to_ppm"] = None
-        print(json.dumps(res))
-    ss.close()
-    scene.close()
+        print(json.dumps(res), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

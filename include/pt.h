@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 1
+#define PT_ABI_VERSION 2   /* 2: pt_render_opts.gather */
 
 enum {
     PT_OK = 0,
@@ -100,7 +100,13 @@ typedef struct pt_render_opts {
     int32_t progress;        /* 1 = print the reference's "Loading: [...]" bar to stdout */
     uint32_t win_x0, win_y0; /* optional window: render only [x0,x0+w) x [y0,y0+h) of the */
     uint32_t win_w, win_h;   /* image, keeping global-index seeds (win_w = 0: full image) */
+    int32_t gather;          /* PT_GATHER_*: how the framebuffer tiles reach the caller */
 } pt_render_opts;
+enum {
+    PT_GATHER_AUTO = 0,      /* default: RCCL (ncclGather over xGMI) when ngpu > 1, host copy if RCCL fails */
+    PT_GATHER_RCCL = 1,      /* RCCL at any ngpu (also ngpu = 1: a one-rank communicator); failure is an error */
+    PT_GATHER_HOST = 2       /* per-device copies through the host, never RCCL */
+};
 void pt_render_opts_default(pt_render_opts* o);
 
 typedef struct pt_stats {

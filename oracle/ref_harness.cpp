@@ -12,12 +12,13 @@
 //          4 u32 (left,right,first,count); primitive order: per primitive
 //          u32 type + 9 f32 (dop_data, dop_data1, dop_data2 -- the latter two
 //          zero unless TRIANGLE) + 3 f32 pos.
-//   render <scene> <out.ppm> <radiance.f32> [x0 y0 w h]
+//   render <scene> <out.ppm> <radiance.f32> [x0 y0 w h [ystride]]
 //          restates Scene::Render's per-pixel loop (hw5/src/scene.cpp:205-252)
 //          around the reference's own Scene::Sample, additionally saving the
 //          pre-tonemap fp32 mean radiance.  With a window, only those pixels
 //          are rendered (seeds stay the global index y*W+x), the PPM is the
-//          window crop.
+//          window crop; with ystride, the window's h rows are y0, y0+ystride, ...
+//          Load+InitScene and render times go to stderr (bench.py cpu_baseline).
 //   rng    <seed> <n> <out.bin>
 //          libstdc++ minstd_rand + uniform_real<float> + normal<float> streams
 //          exactly as hw5/src/scene.cpp:216-223 builds them: n uniforms, then
@@ -29,6 +30,7 @@
 // see the access override below.
 #include <algorithm>
 #include <cassert>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -44,6 +46,7 @@
 #include <thread>
 #include <variant>
 #include <vector>
+#include <omp.h>
 #define GLM_ENABLE_EXPERIMENTAL
 #include <glm/vec3.hpp>
 #include <glm/gtc/quaternion.hpp>
@@ -93,21 +96,33 @@ static int mode_bvh(int argc, char** argv) {
     return 0;
 }
 
+static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 static int mode_render(int argc, char** argv) {
     if (argc < 5) return 2;
     Scene s;
+    const double t0 = now_s();
     load(s, argv[2]);
+    const double t1 = now_s();
+    // threads as the reference sets them (hw5/src/scene.cpp:212), unless REF_THREADS
+    // names the host's usable CPU share (bench.py cpu_baseline)
+    const char* rt = std::getenv("REF_THREADS");
+    const int threads = rt && *rt ? std::atoi(rt) : (int)std::thread::hardware_concurrency();
+    omp_set_num_threads(threads);
     const unsigned W = s.cam.width, H = s.cam.height;
-    unsigned x0 = 0, y0 = 0, w = W, h = H;
+    unsigned x0 = 0, y0 = 0, w = W, h = H, ystride = 1;
     if (argc >= 9) {
         x0 = (unsigned)std::atoi(argv[5]); y0 = (unsigned)std::atoi(argv[6]);
         w = (unsigned)std::atoi(argv[7]); h = (unsigned)std::atoi(argv[8]);
     }
+    if (argc >= 10) ystride = (unsigned)std::max(1, std::atoi(argv[9]));   // rows y0, y0+ystride, ...
     std::vector<float> rad((size_t)w * h * 3);
     std::vector<unsigned char> rgb((size_t)w * h * 3);
     #pragma omp parallel for schedule(dynamic)
     for (long long k = 0; k < (long long)w * h; ++k) {
-        const unsigned x = x0 + (unsigned)(k % w), y = y0 + (unsigned)(k / w);
+        const unsigned x = x0 + (unsigned)(k % w), y = y0 + (unsigned)(k / w) * ystride;
         const unsigned i = y * W + x;
         std::minstd_rand rnd(i);
         std::uniform_real_distribution<float> uniform01{0.f, 1.f};
@@ -120,6 +135,9 @@ static int mode_render(int argc, char** argv) {
         rgb[k * 3 + 0] = u[0]; rgb[k * 3 + 1] = u[1]; rgb[k * 3 + 2] = u[2];
         delete[] u;
     }
+    const double t2 = now_s();
+    std::fprintf(stderr, "ref_harness: load_init_s=%.6f render_s=%.6f threads=%d hardware_concurrency=%u\n", t1 - t0,
+                 t2 - t1, threads, std::thread::hardware_concurrency());
     std::ofstream out(argv[3], std::ios::binary);
     out << "P6\n" << w << " " << h << "\n" << 255 << "\n";
     out.write(reinterpret_cast<const char*>(rgb.data()), (std::streamsize)rgb.size());

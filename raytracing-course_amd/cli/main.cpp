@@ -4,10 +4,12 @@
 //     PT_NGPU=<n>     GPUs driven by this process (pixel tiles, default 1)
 //     PT_DEVICE=<i>   first device (default 0)
 //     PT_SPP_LAUNCH=<k> samples per kernel launch (default auto)
+//     PT_GATHER=rccl|host  framebuffer gather (default: RCCL when PT_NGPU > 1)
 //     PT_QUIET=1      no progress bar
 //     PT_STATS=1      print rays / Mray/s / timings to stderr
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <thread>
 #include <vector>
@@ -46,6 +48,10 @@ int main(int argc, char** argv) {
     o.device = dev0;
     o.spp_per_launch = (uint32_t)env_int("PT_SPP_LAUNCH", 0);
     o.progress = env_int("PT_QUIET", 0) ? 0 : 1;
+    if (const char* g = getenv("PT_GATHER")) {
+        if (!strcmp(g, "rccl")) o.gather = PT_GATHER_RCCL;
+        else if (!strcmp(g, "host")) o.gather = PT_GATHER_HOST;
+    }
     std::vector<uint8_t> rgb((size_t)info.width * info.height * 3);
     pt_stats st;
     if (pt_render(s, &o, rgb.data(), nullptr, &st) != PT_OK) {
@@ -59,9 +65,9 @@ int main(int argc, char** argv) {
         return 1;
     }
     if (env_int("PT_STATS", 0)) {
-        fprintf(stderr, "rays=%llu samples=%llu kernel_ms=%.3f wall_ms=%.3f Mray/s=%.3f\n",
+        fprintf(stderr, "rays=%llu samples=%llu kernel_ms=%.3f wall_ms=%.3f Mray/s=%.3f ngpu=%d gather_rccl=%llu\n",
                 (unsigned long long)st.rays, (unsigned long long)st.samples, st.kernel_ms, st.wall_ms,
-                st.kernel_ms > 0 ? st.rays / (st.kernel_ms * 1e3) : 0.0);
+                st.kernel_ms > 0 ? st.rays / (st.kernel_ms * 1e3) : 0.0, ngpu, (unsigned long long)st.gather_rccl);
     }
     pt_scene_free(s);
     return 0;

@@ -117,6 +117,7 @@ struct Query {
     int res_id;                 // the normal is recomputed from the prim by the consumer
 };
 static_assert(PT_REPLAY_HITS < 8, "nh is a 3-bit field");
+#define PT_QUERY_SP_MAX 127u    // Query::sp is a 7-bit field: pt_scene_prepare rejects deeper aux stacks
 
 struct QCounts {
     uint32_t nodes, aux, ptests, planes;

@@ -479,6 +479,9 @@ int pt_scene_prepare(pt_scene* s) {
         if (!std::isfinite(s->box_extent)) s->box_extent = INFINITY;   // certification then never succeeds
         pth::build_aux_bvh(s->nodes, s->aux, s->aux_depth);
         pth::build_aux_wide(s->aux, s->dnodes, PT_AUXW, s->auxsl, s->auxsl_depth, s->auxw_stack);
+        // Query::sp (pt_query.h) counts pending aux nodes in a 7-bit field
+        if (s->auxw_stack > PT_QUERY_SP_MAX)
+            throw std::runtime_error("auxiliary BVH too deep for the query's stack counter");
         build_query_blob(s);
         pth::build_gamma_thresholds(s->thr);
     } catch (const std::exception& e) {
@@ -1063,34 +1066,39 @@ int gather_rccl(const std::vector<pt_session*>& sess, int dev0, uint32_t W, uint
     size_t cap = 0;
     for (auto* x : sess) cap = std::max<size_t>(cap, 3ull * x->n_slots);
     cap = std::max<size_t>(cap, 16);
-    std::vector<uint8_t*> send(n, nullptr);
-    uint8_t* recv = nullptr;
-    auto release = [&]() {
-        for (int g = 0; g < n; ++g) { (void)hipSetDevice(dev0 + g); (void)hipFree(send[g]); }
-        (void)hipSetDevice(dev0);
-        (void)hipFree(recv);
-    };
+    // per-device staging buffers, released on every exit path (scope guard)
+    struct Buffers {
+        int dev0, n;
+        std::vector<uint8_t*> send;
+        uint8_t* recv = nullptr;
+        Buffers(int d, int k) : dev0(d), n(k), send((size_t)k, nullptr) {}
+        ~Buffers() {
+            for (int g = 0; g < n; ++g)
+                if (send[(size_t)g]) { (void)hipSetDevice(dev0 + g); (void)hipFree(send[(size_t)g]); }
+            (void)hipSetDevice(dev0);
+            if (recv) (void)hipFree(recv);
+        }
+    } buf(dev0, n);
     for (int g = 0; g < n; ++g) {
         HIP_TRY(hipSetDevice(dev0 + g));
-        if (hipMalloc(&send[g], cap) != hipSuccess) { release(); return fail(PT_E_OOM, "gather buffer"); }
+        if (hipMalloc(&buf.send[(size_t)g], cap) != hipSuccess) return fail(PT_E_OOM, "gather buffer");
         if (sess[g]->n_slots)
-            HIP_TRY(hipMemcpyAsync(send[g], sess[g]->out, 3ull * sess[g]->n_slots, hipMemcpyDeviceToDevice,
+            HIP_TRY(hipMemcpyAsync(buf.send[(size_t)g], sess[g]->out, 3ull * sess[g]->n_slots, hipMemcpyDeviceToDevice,
                                    sess[g]->stream));
-        if (g == 0 && hipMalloc(&recv, cap * n) != hipSuccess) { release(); return fail(PT_E_OOM, "gather buffer"); }
+        if (g == 0 && hipMalloc(&buf.recv, cap * n) != hipSuccess) return fail(PT_E_OOM, "gather buffer");
     }
     ncclResult_t r = ncclGroupStart();
     for (int g = 0; g < n && r == ncclSuccess; ++g)
-        r = ncclGather(send[g], g == 0 ? recv : nullptr, cap, ncclUint8, 0, c[g], sess[g]->stream);
+        r = ncclGather(buf.send[(size_t)g], g == 0 ? buf.recv : nullptr, cap, ncclUint8, 0, c[g], sess[g]->stream);
     if (r == ncclSuccess) r = ncclGroupEnd();
-    if (r != ncclSuccess) { release(); return fail(PT_E_RCCL, std::string("ncclGather: ") + ncclGetErrorString(r)); }
+    if (r != ncclSuccess) return fail(PT_E_RCCL, std::string("ncclGather: ") + ncclGetErrorString(r));
     std::vector<uint8_t> host(cap * n);
     HIP_TRY(hipSetDevice(dev0));
-    HIP_TRY(hipMemcpyAsync(host.data(), recv, cap * n, hipMemcpyDeviceToHost, sess[0]->stream));
+    HIP_TRY(hipMemcpyAsync(host.data(), buf.recv, cap * n, hipMemcpyDeviceToHost, sess[0]->stream));
     for (int g = 0; g < n; ++g) {
         HIP_TRY(hipSetDevice(dev0 + g));
         HIP_TRY(hipStreamSynchronize(sess[g]->stream));
     }
-    release();
     for (int g = 0; g < n; ++g) pt_unpack_tiles(W, H, (uint32_t)g, (uint32_t)n, host.data() + cap * g, rgb);
     return PT_OK;
 }
@@ -1182,10 +1190,14 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
         if ((rc = pt_session_resolve(x, nullptr, drads[(size_t)g]))) return cleanup(rc);
     }
     if (rgb) {
-        if (ngpu > 1 && gather_rccl(sess, o.device, W, H, rgb) == PT_OK) {
+        // PT_GATHER_AUTO: RCCL when ngpu > 1 (host fallback with a warning);
+        // PT_GATHER_RCCL: RCCL at any ngpu, an error if it fails; PT_GATHER_HOST: never RCCL
+        const bool try_rccl = o.gather == PT_GATHER_RCCL || (o.gather == PT_GATHER_AUTO && ngpu > 1);
+        if (try_rccl && (rc = gather_rccl(sess, o.device, W, H, rgb)) == PT_OK) {
             agg.gather_rccl = 1;
         } else {
-            if (ngpu > 1) fprintf(stderr, "pt_render: RCCL gather unavailable (%s); gathering through the host\n",
+            if (o.gather == PT_GATHER_RCCL) return cleanup(rc);
+            if (try_rccl) fprintf(stderr, "pt_render: RCCL gather unavailable (%s); gathering through the host\n",
                                   pt_last_error());
             for (int g = 0; g < ngpu; ++g) {
                 pt_session* x = sess[(size_t)g];

@@ -156,6 +156,9 @@ struct Builder {
                 break;
             }
         }
+        // every SAH cost overflowed to >= kInf while the unsplit cost is larger still
+        // (huge extents): the reference then recurses on an empty range (UB, it crashes)
+        if (cut <= first || cut >= last) throw std::runtime_error("degenerate SAH split (the reference crashes here)");
         if (spawn > 0 && last - first >= 4096u) {
             std::vector<HNode> ln, rn;
             ln.reserve(2 * (size_t)(cut - first));

@@ -25,6 +25,8 @@ PT_E_INVALID, PT_E_IO, PT_E_SCENE, PT_E_NO_GPU, PT_E_HIP, PT_E_RCCL, PT_E_OOM = 
 TRAVERSAL_REPLAY = 0
 TRAVERSAL_EXACT = 1
 TRAVERSAL_REPLAY_DIV = 2
+GATHER_AUTO, GATHER_RCCL, GATHER_HOST = 0, 1, 2
+ABI_VERSION = 2
 
 # One HIP runtime per process: PyTorch bundles its own libamdhip64 (soname
 # libamdhip64.so.7, but its users link the unversioned name), so loading
@@ -51,7 +53,8 @@ class SceneInfo(C.Structure):
 class RenderOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("ngpu", C.c_int32), ("spp_per_launch", C.c_uint32),
                 ("samples", C.c_uint32), ("traversal", C.c_int32), ("progress", C.c_int32),
-                ("win_x0", C.c_uint32), ("win_y0", C.c_uint32), ("win_w", C.c_uint32), ("win_h", C.c_uint32)]
+                ("win_x0", C.c_uint32), ("win_y0", C.c_uint32), ("win_w", C.c_uint32), ("win_h", C.c_uint32),
+                ("gather", C.c_int32)]
 
 
 class Stats(C.Structure):
@@ -182,10 +185,12 @@ class Scene:
         return nb.tobytes(), pb.tobytes()
 
     def render(self, device=0, ngpu=1, samples=0, spp_per_launch=0, radiance=False, progress=False, window=None,
-               traversal=TRAVERSAL_REPLAY):
+               traversal=TRAVERSAL_REPLAY, gather=GATHER_AUTO):
         """Render on the GPU(s): returns (rgb u8 HxWx3, radiance f32 HxWx3 | None, stats).
 
-        window=(x0, y0, w, h) renders only those pixels (global-index seeds kept)."""
+        window=(x0, y0, w, h) renders only those pixels (global-index seeds kept).
+        gather: GATHER_AUTO (RCCL when ngpu > 1), GATHER_RCCL (RCCL at any ngpu, an
+        error if it fails), GATHER_HOST (never RCCL)."""
         inf = self.info
         w, h = (window[2], window[3]) if window else (inf["width"], inf["height"])
         rgb = np.zeros((h, w, 3), np.uint8)
@@ -194,6 +199,7 @@ class Scene:
         _lib.pt_render_opts_default(C.byref(o))
         o.device, o.ngpu, o.samples, o.spp_per_launch, o.progress = device, ngpu, samples, spp_per_launch, int(progress)
         o.traversal = traversal
+        o.gather = gather
         if window:
             o.win_x0, o.win_y0, o.win_w, o.win_h = window
         st = Stats()
@@ -270,6 +276,13 @@ def unpack_tiles(packed, width, height, rank, world, out=None):
     out = np.zeros((height, width, 3), np.uint8) if out is None else out
     packed = np.ascontiguousarray(packed, np.uint8)
     _check(_lib.pt_unpack_tiles(width, height, rank, world, _ptr(packed), _ptr(out)))
+    return out
+
+
+def unpack_tiles_f32(packed, width, height, rank, world, out=None):
+    out = np.zeros((height, width, 3), np.float32) if out is None else out
+    packed = np.ascontiguousarray(packed, np.float32)
+    _check(_lib.pt_unpack_tiles_f32(width, height, rank, world, _ptr(packed), _ptr(out)))
     return out
 
 

@@ -51,6 +51,12 @@ IMAGES = {
     "c3s4_win_944_520_16x16": ("c3", (1920, 1080, 4, True, "diffuse"), (944, 520, 16, 16)),
     "c4glass_s4_win_900_560_16x16": ("c4_glass", (1920, 1080, 4, True, "glass"), (900, 560, 16, 16)),
     "c4metal_s4_win_900_560_16x16": ("c4_metal", (1920, 1080, 4, True, "metal"), (900, 560, 16, 16)),
+    # config 5 (3840x2160, pixel-tiled over 8 GPUs): windows whose 16x16 tiles belong to
+    # ranks 0, 2+3, 6 and 7 of 8 (global tile ty*240+tx, rank = tile % 8); seeds y*3840+x
+    "c5s4_win_1920_1072_16x16": ("c5", (3840, 2160, 4, True, "diffuse"), (1920, 1072, 16, 16)),
+    "c5s4_win_1952_1072_32x16": ("c5", (3840, 2160, 4, True, "diffuse"), (1952, 1072, 32, 16)),
+    "c5s4_win_1760_1200_16x16": ("c5", (3840, 2160, 4, True, "diffuse"), (1760, 1200, 16, 16)),
+    "c5s4_win_3824_2144_16x16": ("c5", (3840, 2160, 4, True, "diffuse"), (3824, 2144, 16, 16)),
 }
 
 RNG_SEEDS = [0, 1, 2, 12345, 262143, 2073599, 2147483646, 4294967295]
@@ -89,32 +95,47 @@ def scene_file(tmp, src, gen):
     return out
 
 
+def render_image(harness, tmp, name):
+    src, gen, win = IMAGES[name]
+    sc = scene_file(tmp, src, gen)
+    ppm = os.path.join(HERE, "img_%s.ppm" % name)
+    rad = os.path.join(HERE, "rad_%s.f32" % name)
+    cmd = [harness, "render", sc, ppm, rad]
+    if win:
+        cmd += [str(v) for v in win]
+    subprocess.check_call(cmd)
+    entry = {"scene": src, "gen": list(gen) if gen else None, "window": list(win) if win else None,
+             "ppm_md5": md5f(ppm), "rad_md5": md5f(rad)}
+    if not win:
+        # the windowless harness render must equal the real CLI byte-for-byte
+        cli_ppm = os.path.join(tmp, name + "_cli.ppm")
+        subprocess.check_call([os.path.join(REF, "raytracing_hw5"), sc, cli_ppm], stdout=subprocess.DEVNULL)
+        assert md5f(cli_ppm) == entry["ppm_md5"], name
+    print("image", name, entry["ppm_md5"])
+    return entry
+
+
 def main():
     if not os.path.isdir("/root/reference/hw5"):
         print("reference not present; cannot regenerate fixtures", file=sys.stderr)
         return 1
     subprocess.check_call(["sh", os.path.join(REPO, "oracle", "build_ref.sh")])
     harness = os.path.join(REF, "ref_harness")
+    if len(sys.argv) > 2 and sys.argv[1] == "--images":
+        # add / refresh only the named image fixtures in the existing manifest
+        with open(os.path.join(HERE, "manifest.json")) as f:
+            manifest = json.load(f)
+        with tempfile.TemporaryDirectory() as tmp:
+            for name in sys.argv[2:]:
+                manifest["images"][name] = render_image(harness, tmp, name)
+        with open(os.path.join(HERE, "manifest.json"), "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+        return 0
     manifest = {"images": {}, "rng": {}, "trav": {}, "bvh": {}, "full": {},
                 "generator": "tests/golden/make_golden.py", "reference": "FeggieBoss/raytracing-course hw5"}
     with tempfile.TemporaryDirectory() as tmp:
-        for name, (src, gen, win) in IMAGES.items():
-            sc = scene_file(tmp, src, gen)
-            ppm = os.path.join(HERE, "img_%s.ppm" % name)
-            rad = os.path.join(HERE, "rad_%s.f32" % name)
-            cmd = [harness, "render", sc, ppm, rad]
-            if win:
-                cmd += [str(v) for v in win]
-            subprocess.check_call(cmd)
-            entry = {"scene": src, "gen": list(gen) if gen else None, "window": list(win) if win else None,
-                     "ppm_md5": md5f(ppm), "rad_md5": md5f(rad)}
-            if not win:
-                # the windowless harness render must equal the real CLI byte-for-byte
-                cli_ppm = os.path.join(tmp, name + "_cli.ppm")
-                subprocess.check_call([os.path.join(REF, "raytracing_hw5"), sc, cli_ppm], stdout=subprocess.DEVNULL)
-                assert md5f(cli_ppm) == entry["ppm_md5"], name
-            manifest["images"][name] = entry
-            print("image", name, entry["ppm_md5"])
+        for name in IMAGES:
+            manifest["images"][name] = render_image(harness, tmp, name)
         for seed in RNG_SEEDS:
             p = os.path.join(HERE, "rng_%d.f32" % seed)
             subprocess.check_call([harness, "rng", str(seed), str(RNG_N), p])

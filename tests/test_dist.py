@@ -90,3 +90,37 @@ def test_unpack_tiles_abi_matches_deal(world):
     for r in range(world):
         pt.unpack_tiles(_packed_for_rank(img, r, world), W, H, r, world, out=out)
     assert np.array_equal(out, img)
+
+
+def _bench(args, env_extra=None):
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, env=env, capture_output=True,
+                       text=True, timeout=300)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r.stderr
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_gpus_n_starts_n_ranks(n):
+    """`bench.py --gpus N` (as the driver calls it, no torchrun environment)
+    starts N ranks itself: rank 0 sees exactly N distinct rank processes."""
+    rc, out, err = _bench(["--gpus", str(n), "--probe-ranks"])
+    assert rc == 0, err[-2000:]
+    assert out["probe"] and out["n_gpus"] == n and out["gpus_arg"] == n
+    assert sorted(r["rank"] for r in out["ranks"]) == list(range(n))
+    assert len({r["pid"] for r in out["ranks"]}) == n
+    assert sorted(r["local_rank"] for r in out["ranks"]) == list(range(n))
+
+
+def test_bench_refuses_mismatched_world():
+    """under torchrun, a WORLD_SIZE that differs from --gpus is an error, not a
+    silently relabelled run"""
+    rc, out, err = _bench(["--gpus", "2", "--probe-ranks"], {"WORLD_SIZE": "1", "RANK": "0"})
+    assert rc == 2 and out is None
+    assert "refusing" in err

@@ -191,3 +191,80 @@ def test_round_engine_bit_exact(pt, name, monkeypatch):
     assert st["errors"] == 0
     assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
     assert np.array_equal(rgb, img)
+
+
+C5_WINDOWS = ["c5s4_win_1920_1072_16x16", "c5s4_win_1952_1072_32x16", "c5s4_win_1760_1200_16x16",
+              "c5s4_win_3824_2144_16x16"]
+
+
+def test_config5_rank_of_8_sessions_vs_reference_windows(pt):
+    """Config 5 (3840x2160, the BASELINE's 8-GPU config) as the 8-rank run renders it:
+    a session per rank owning every 8th 16x16 tile of the 4K frame (seeds y*3840+x),
+    4 spp.  The pixels of the reference's golden windows must come out of the
+    ranks that own them bit-exactly (8-bit and fp32 radiance)."""
+    import torch
+    world, W, H = 8, 3840, 2160
+    wins = {n: U.golden_image(n) for n in C5_WINDOWS}
+    m0 = wins[C5_WINDOWS[0]][0]
+    tiles_x = W // 16
+    owners = {}
+    for n, (m, _, _) in wins.items():
+        x0, y0, w, h = m["window"]
+        for ty in range(y0 // 16, (y0 + h + 15) // 16):
+            for tx in range(x0 // 16, (x0 + w + 15) // 16):
+                owners.setdefault((ty * tiles_x + tx) % world, set()).add(n)
+    assert len(owners) >= 4   # the windows span several ranks (0, 2, 3, 6, 7)
+    rgb = np.zeros((H, W, 3), np.uint8)
+    rad = np.zeros((H, W, 3), np.float32)
+    covered = np.zeros((H, W), bool)
+    with pt.Scene.load(U.golden_scene_path(C5_WINDOWS[0])) as s:
+        s.prepare()
+        assert (s.info["width"], s.info["height"], s.info["samples"]) == (W, H, 4)
+        for r in sorted(owners):
+            ss = pt.Session(s, rank=r, world=world)
+            ss.trace(4)
+            drad = torch.empty(ss.n_tiles * 256 * 3, dtype=torch.float32, device="cuda")
+            ss.resolve(dev_rad=drad.data_ptr())
+            ss.sync()
+            assert ss.stats()["errors"] == 0
+            pt.unpack_tiles(ss.read_packed(), W, H, r, world, out=rgb)
+            pt.unpack_tiles_f32(drad.cpu().numpy(), W, H, r, world, out=rad)
+            mine = np.zeros(((H + 15) // 16, tiles_x), bool)
+            mine.reshape(-1)[r::world] = True
+            covered |= np.repeat(np.repeat(mine, 16, 0), 16, 1)[:H, :W]
+            ss.close()
+    assert m0["gen"][:3] == [W, H, 4]
+    for n, (m, img, wrad) in wins.items():
+        x0, y0, w, h = m["window"]
+        assert covered[y0:y0 + h, x0:x0 + w].all(), n
+        assert rad[y0:y0 + h, x0:x0 + w].view(np.uint32).tolist() == wrad.view(np.uint32).tolist(), n
+        assert np.array_equal(rgb[y0:y0 + h, x0:x0 + w], img), n
+
+
+@pytest.mark.parametrize("ngpu_gather", ["rccl", "host", "auto"])
+def test_render_gather_paths(pt, ngpu_gather):
+    """pt_render's framebuffer gather: PT_GATHER_RCCL runs the ncclGather path
+    (ncclCommInitAll + grouped ncclGather, a one-rank communicator on one GPU) and
+    must give the same bytes as the host gather; gather_rccl records which ran."""
+    mode = {"rccl": pt.GATHER_RCCL, "host": pt.GATHER_HOST, "auto": pt.GATHER_AUTO}[ngpu_gather]
+    m, img, rad = U.golden_image("dragon_64x64x16")
+    with pt.Scene.load(U.golden_scene_path("dragon_64x64x16")) as s:
+        rgb, r, st = s.render(radiance=True, gather=mode)
+        rgb2, _, st2 = s.render(gather=mode)   # the cached communicator is reused
+    assert st["gather_rccl"] == (1 if ngpu_gather == "rccl" else 0)
+    assert st2["gather_rccl"] == st["gather_rccl"]
+    assert np.array_equal(rgb, img) and np.array_equal(rgb2, img)
+    assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
+
+
+def test_cli_rccl_gather_config1(pt, tmp_path):
+    """The drop-in CLI's multi-GPU gather (PT_GATHER=rccl; PT_NGPU=n uses the
+    same code with n ranks) on config 1: same bytes as the reference."""
+    import subprocess
+    out = tmp_path / "c1.ppm"
+    exe = U.os.path.join(U.PKG, "build", "pt_render")
+    r = subprocess.run([exe, U.scene_path("c1"), str(out)], capture_output=True, text=True, timeout=300,
+                       env=dict(U.os.environ, PT_QUIET="1", PT_STATS="1", PT_GATHER="rccl"))
+    assert r.returncode == 0, r.stderr
+    assert "gather_rccl=1" in r.stderr, r.stderr
+    assert U.md5(out.read_bytes()) == M["full"]["c1"]["md5"]

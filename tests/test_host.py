@@ -35,7 +35,7 @@ def test_abi_exports_every_declared_symbol():
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
     assert set(names) == set(pt.EXPORTED)
-    assert pt.abi_version() == 1
+    assert pt.abi_version() == pt.ABI_VERSION == 2
 
 
 @pytest.mark.parametrize("name", sorted(M["bvh"]))
@@ -108,6 +108,21 @@ def test_scene_errors():
         with pytest.raises(pt.PTError) as e:
             s.prepare()
         assert e.value.code == pt.PT_E_SCENE
+
+
+
+def test_degenerate_sah_split_is_an_error_not_a_crash():
+    # 200 boxes at x = 1.3^i: every SAH cut cost overflows (the reference's
+    # bvh.cpp recursion then runs on an empty range and crashes); the library
+    # reports PT_E_SCENE instead of taking the calling process down
+    lines = ["DIMENSIONS 4 4", "SAMPLES 1", "RAY_DEPTH 1"]
+    for i in range(200):
+        lines += ["NEW_PRIMITIVE", "BOX 1 1 1", "POSITION %.6g 0 0" % (1.3 ** i)]
+    with pt.Scene.loads("\n".join(lines) + "\n") as s:
+        with pytest.raises(pt.PTError) as e:
+            s.prepare()
+        assert e.value.code == pt.PT_E_SCENE
+        assert "degenerate SAH split" in str(e.value)
 
 
 TRAVERSALS = {"replay": 0, "exact": 1, "replay_div": 2}

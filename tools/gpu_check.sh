@@ -2,6 +2,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
+{ nproc; cat /sys/fs/cgroup/cpu.max 2>/dev/null; grep -m1 "model name" /proc/cpuinfo; python3 -c "import os; print(len(os.sched_getaffinity(0)))"; } > gpurun_out/host.txt 2>&1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && echo SMOKE_OK || { echo SMOKE_FAIL; tail -20 gpurun_out/smoke.log; exit 1; }
 timeout -k 10 900 python -u -m pytest tests/test_gpu.py -x -v --timeout 300 --timeout-method thread --durations=30 > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo PYTEST_RC=$rc
 tail -5 gpurun_out/pytest_gpu.log

@@ -13,10 +13,14 @@ Counter conventions (MI355X_MICROARCH.md, HBM/rocprofv3 section):
 """
 import argparse
 import collections
+import sys
 import csv
 import json
 import os
 import shutil
+
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
 def per_kernel(path, kernel=None, last=0):
@@ -87,25 +91,43 @@ def main():
         avg_ns = sum(d) / len(d)
         lines += ["`%s` over the bench's timed region (last %d launches, kernel trace): mean %.3f ms"
                   % (a.kernel, len(d), avg_ns / 1e6)]
-    # resources of the kernel from the trace
+    # resources of the kernel: registers from the compiler's report (the trace's
+    # VGPR_Count column is in allocation granules, not registers); grid from the trace
+    import kernel_resources
+    res_k = kernel_resources.kernel(a.kernel)
+    for name, v in sorted(res_k.items()):
+        lines += ["", "`%s` (compiler): %d VGPRs + %d AGPRs, %d SGPRs, %d VGPR / %d SGPR spills, scratch %d B/lane, "
+                  "%d waves/SIMD" % (name, v.get("vgpr", 0), v.get("agpr", 0), v.get("sgpr", 0), v.get("vgpr_spill", 0),
+                                     v.get("sgpr_spill", 0), v.get("scratch_bytes", 0), v.get("waves_per_simd", 0))]
     for r in csv.DictReader(open(os.path.join(kt, "run_kernel_trace.csv"))):
         if a.kernel in r["Kernel_Name"]:
-            lines += ["", "`%s`: VGPR %s, SGPR %s, scratch %s B, LDS (static) %s B, grid %s x wg %s" % (
-                a.kernel, r["VGPR_Count"], r["SGPR_Count"], r["Scratch_Size"], r["LDS_Block_Size"],
-                r["Grid_Size_X"], r["Workgroup_Size_X"])]
+            lines += ["`%s` (trace): LDS %s B, grid %s x wg %s" % (
+                a.kernel, r["LDS_Block_Size"], r["Grid_Size_X"], r["Workgroup_Size_X"])]
             break
     pmc = {}
+    per_alg, per_ray = {}, {}   # counter totals over the timed launches / that pass's algorithmic bytes, rays
     for sub in sorted(os.listdir(a.prof)):
         p = os.path.join(a.prof, sub, "run_counter_collection.csv")
         if sub.startswith("pmc") and os.path.exists(p):
+            bj = None
+            bjp = os.path.join(a.prof, "bench_%s.json" % sub[4:])
+            if os.path.exists(bjp):
+                try:
+                    bj = json.load(open(bjp))
+                except Exception:
+                    bj = None
+            timed = int(bj["roofline"]["launches"]) if bj else a.timed
             tot, nd = collections.defaultdict(float), 0
-            for k, (d, n) in per_kernel(p, a.kernel, a.timed).items():
+            for k, (d, n) in per_kernel(p, a.kernel, timed).items():
                 if a.kernel in k:
                     nd += n
                     for c, v in d.items():
                         tot[c] += v
             for c, v in tot.items():
                 pmc[c] = v / nd
+                if bj:
+                    per_alg[c] = v / (bj["roofline"]["alg_bytes_per_launch"] * nd)
+                    per_ray[c] = v / bj["rays"]
     lines += ["", "## PMC, per %s launch (separate --pmc passes%s)"
               % (a.kernel, ", last %d launches" % a.timed if a.timed else ""), ""]
     for c, v in sorted(pmc.items()):
@@ -126,8 +148,37 @@ def main():
         lines += ["", "## derived", ""]
         for k, v in res.items():
             lines.append("* %s = %s" % (k, v if isinstance(v, str) else "%.6g" % v))
+    if "FETCH_SIZE" in per_alg:
+        res["traffic_per_alg_byte"] = per_alg["FETCH_SIZE"] * 2048.0 + per_alg.get("WRITE_SIZE", 0.0) * 1024.0
+        res["fetch_bytes_per_ray"] = per_ray["FETCH_SIZE"] * 2048.0
+        if "WRITE_SIZE" in per_ray:
+            res["write_bytes_per_ray"] = per_ray["WRITE_SIZE"] * 1024.0
+        lines.append("* traffic / algorithmic bytes (per pass, same launches) = %.4g" % res["traffic_per_alg_byte"])
+        lines.append("* fetch bytes per ray = %.4g, write bytes per ray = %.4g"
+                     % (res["fetch_bytes_per_ray"], res.get("write_bytes_per_ray", 0.0)))
     if "SQ_INSTS_VALU" in pmc and "SQ_WAVES" in pmc:
         lines.append("* VALU instructions per wave = %.6g" % (pmc["SQ_INSTS_VALU"] / pmc["SQ_WAVES"]))
+    if "SQ_INSTS_VALU" in per_ray:
+        lines.append("* VALU wave-instructions per ray = %.4g" % per_ray["SQ_INSTS_VALU"])
+    # what limits the kernel (SQ_* cycle counters are per wave, in quad-cycles; a
+    # SIMD issues one wave64 VALU instruction per 2 cycles)
+    if "SQ_WAVE_CYCLES" in pmc and "SQ_ACTIVE_INST_VALU" in pmc:
+        wc = pmc["SQ_WAVE_CYCLES"]
+        busy = pmc.get("SQ_BUSY_CYCLES")
+        lim = {"active_valu_frac": pmc["SQ_ACTIVE_INST_VALU"] / wc}
+        for c in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_SCA",
+                  "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_MISC"):
+            if c in pmc:
+                lim[c.lower().replace("sq_", "") + "_frac"] = pmc[c] / wc
+        if "SQ_INSTS_VALU" in pmc and res.get("avg_launch_ms"):
+            # VALU issue share of the chip: 2 cycles per wave64 instruction, 1024 SIMDs, the clock from GRBM
+            clk = pmc["GRBM_GUI_ACTIVE"] / 8.0 / (res["avg_launch_ms"] * 1e-3) if "GRBM_GUI_ACTIVE" in pmc else 2.4e9
+            lim["valu_issue_frac"] = pmc["SQ_INSTS_VALU"] * 2.0 / (1024 * clk * res["avg_launch_ms"] * 1e-3)
+            lim["clock_ghz"] = clk / 1e9
+        res.update(lim)
+        lines += ["", "## what limits k_wpath (fractions of wave cycles)", ""]
+        for k, v in sorted(lim.items()):
+            lines.append("* %s = %.4g" % (k, v))
     open(os.path.join(a.out, "SUMMARY.md"), "w").write("\n".join(lines) + "\n")
     for f in os.listdir(a.prof):
         if f.endswith(".json"):
