@@ -33,20 +33,49 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool want) {
     return base + lanes_below(m);
 }
 
+// a slot's fold records: one 16-B store per vertex, contiguous per slot
 struct HbmVStore {
-    uint32_t* base;   // + slot
-    uint32_t stride;  // n_slots
+    uint4* base;      // fold + slot * depth
     __device__ __forceinline__ void put(uint32_t k, uint32_t idm, float s1, float s2) {
-        base[(3u * k) * stride] = idm;
-        base[(3u * k + 1u) * stride] = f2u(s1);
-        base[(3u * k + 2u) * stride] = f2u(s2);
+        base[k] = make_uint4(idm, f2u(s1), f2u(s2), 0u);
     }
     __device__ __forceinline__ void get(uint32_t k, uint32_t& idm, float& s1, float& s2) const {
-        idm = base[(3u * k) * stride];
-        s1 = u2f(base[(3u * k + 1u) * stride]);
-        s2 = u2f(base[(3u * k + 2u) * stride]);
+        const uint4 v = base[k];
+        idm = v.x;
+        s1 = u2f(v.y);
+        s2 = u2f(v.z);
     }
 };
+__device__ __forceinline__ HbmVStore fold_store(const PixelState& st, uint32_t slot) {
+    return HbmVStore{st.fold + (size_t)slot * st.depth};
+}
+
+// the RNG / progress piece of a slot's record
+struct PixelHot {
+    Rng R;
+    uint32_t nv;      // vertices of the current path (fold records written)
+    uint32_t done;    // samples completed in this session
+};
+__device__ __forceinline__ PixelHot load_hot(const PixelState& st, uint32_t slot) {
+    const uint4 v = st.rec[2u * slot];
+    PixelHot h;
+    h.R.x = v.x;
+    h.R.saved = u2f(v.y);
+    h.R.saved_ok = v.z & 1u;
+    h.nv = (v.z >> 8) & 0xffu;
+    h.done = v.w;
+    return h;
+}
+__device__ __forceinline__ void store_hot(const PixelState& st, uint32_t slot, const PixelHot& h) {
+    st.rec[2u * slot] = make_uint4(h.R.x, f2u(h.R.saved), (h.R.saved_ok & 1u) | (h.nv << 8), h.done);
+}
+__device__ __forceinline__ f3 load_sum(const PixelState& st, uint32_t slot) {
+    const uint4 v = st.rec[2u * slot + 1u];
+    return mk3(u2f(v.x), u2f(v.y), u2f(v.z));
+}
+__device__ __forceinline__ void store_sum(const PixelState& st, uint32_t slot, f3 s) {
+    st.rec[2u * slot + 1u] = make_uint4(f2u(s.x), f2u(s.y), f2u(s.z), 0u);
+}
 
 // owned slot -> global pixel (16x16 tiles of the window dealt round-robin to ranks)
 __device__ __forceinline__ bool slot_pixel(const TileMap& tm, uint32_t tile_local, uint32_t lane, uint32_t& x,

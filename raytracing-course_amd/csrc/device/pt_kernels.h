@@ -19,12 +19,18 @@ struct TileMap {
     uint32_t rank, world; // window tile t belongs to rank t % world
 };
 
-struct PixelState {       // SoA over owned slots (256 per owned tile)
-    uint32_t* rng_x;
-    float* rng_saved;
-    uint32_t* rng_flag;
-    float* sum;           // 3 * n_slots (r plane, g plane, b plane)
+// Per owned slot (256 per owned tile) one 32-B record, read and written as two
+// 16-B pieces: a shade touches ONE piece (one vector load + one store instead of
+// five scattered dwords), the path end the second one as well.
+//   rec[2 slot]     = {rng x, rng saved (f32 bits), rng flag | vertices << 8, samples done}
+//   rec[2 slot + 1] = {sum.r, sum.g, sum.b, -}
+// Fold records (one 16-B record per path vertex: {idm, s1, s2, -}) are slot-major,
+// fold[slot * depth + k], so a path's records share lines.
+struct PixelState {
+    uint4* rec;           // 2 * n_slots
+    uint4* fold;          // depth * n_slots
     uint32_t n_slots;
+    uint32_t depth;       // fold records per slot (>= 1)
 };
 
 struct InitParams {
@@ -37,7 +43,6 @@ struct TraceParams {
     CamView cam;
     TileMap tm;
     PixelState st;
-    uint32_t* vscratch;          // 3 * depth * n_slots
     unsigned long long* counters; // rays, nodes, prim tests, plane tests, errors, aux visits, fallbacks
     ReplayCfg cfg;
     uint32_t depth;
@@ -58,7 +63,7 @@ struct DoneQ {                    // finished queries, input of the shade kernel
     F4* rd;                       // {d.xyz, -}
     uint32_t* id;                 // closest prim (the shade kernel recomputes t, n, side from it), 0xffffffff = miss
 };
-// per-slot path state (pstate = nv | end << 8)
+// how a path ended (shade_item)
 enum : uint32_t { PE_LIVE = 0u, PE_MISS = 1u, PE_CUT = 2u, PE_TERM = 3u };
 
 // round counters: set p = ctl + PT_CTL_SET * p; the work-batch heads are one per
@@ -75,10 +80,7 @@ struct WaveParams {
     uint32_t n_aux;
     CamView cam;
     TileMap tm;
-    PixelState st;
-    uint32_t* vscratch;           // 3 * depth * n_slots fold records
-    uint32_t* pstate;             // n_slots
-    uint32_t* nsamp;              // samples completed per slot (this session)
+    PixelState st;                // per-slot records (RNG, vertices, samples done, sum) + fold records
     RayQ fq[2];                   // fresh rays: round with parity p reads fq[p], appends to fq[1-p]
     uint32_t* cq[2];              // suspended queries (carry_words each): read cq[p], append to cq[1-p]
     uint32_t carry_cap, carry_words;

@@ -23,13 +23,12 @@ __global__ void __launch_bounds__(256) k_init(InitParams P) {
     const uint32_t slot = blockIdx.x * 256u + threadIdx.x;
     uint32_t x, y;
     const bool ok = slot_pixel(P.tm, blockIdx.x, threadIdx.x, x, y);
-    const Rng r = rng_seed(ok ? y * P.tm.W + x : 0u);
-    P.st.rng_x[slot] = r.x;
-    P.st.rng_saved[slot] = r.saved;
-    P.st.rng_flag[slot] = r.saved_ok;
-    P.st.sum[slot] = 0.f;
-    P.st.sum[P.st.n_slots + slot] = 0.f;
-    P.st.sum[2u * P.st.n_slots + slot] = 0.f;
+    PixelHot h;
+    h.R = rng_seed(ok ? y * P.tm.W + x : 0u);
+    h.nv = 0u;
+    h.done = 0u;
+    store_hot(P.st, slot, h);
+    store_sum(P.st, slot, mk3(0.f, 0.f, 0.f));
 }
 
 // V bit 0: filtered node tests + flat replay loop (FAST); bit 1: XCD-banded
@@ -53,13 +52,11 @@ __global__ void __launch_bounds__(256) k_trace(TraceParams P) {
     C.rays = C.nodes = C.ptests = C.planes = C.aux = C.fallbacks = 0ull;
     C.errs = 0u;
     if (ok) {
-        Rng R;
-        R.x = P.st.rng_x[slot];
-        R.saved = P.st.rng_saved[slot];
-        R.saved_ok = P.st.rng_flag[slot];
-        f3 sum = mk3(P.st.sum[slot], P.st.sum[P.st.n_slots + slot], P.st.sum[2u * P.st.n_slots + slot]);
+        PixelHot hot = load_hot(P.st, slot);
+        Rng R = hot.R;
+        f3 sum = load_sum(P.st, slot);
         LdsMem stk{lds_stack + threadIdx.x};
-        HbmVStore vs{P.vscratch + slot, P.st.n_slots};
+        HbmVStore vs = fold_store(P.st, slot);
         const float fxb = (float)x, fyb = (float)y;
         for (uint32_t s = 0; s < P.spp; ++s) {
             const float fx = fxb + rng_uniform(R);
@@ -67,12 +64,10 @@ __global__ void __launch_bounds__(256) k_trace(TraceParams P) {
             const Ray ray = camera_ray(P.cam, fx, fy);
             sum = sum + trace_path<(V & 1) != 0>(P.S, P.cfg, ray, P.depth, R, stk, vs, C);
         }
-        P.st.rng_x[slot] = R.x;
-        P.st.rng_saved[slot] = R.saved;
-        P.st.rng_flag[slot] = R.saved_ok;
-        P.st.sum[slot] = sum.x;
-        P.st.sum[P.st.n_slots + slot] = sum.y;
-        P.st.sum[2u * P.st.n_slots + slot] = sum.z;
+        hot.R = R;
+        hot.done += P.spp;
+        store_hot(P.st, slot, hot);
+        store_sum(P.st, slot, sum);
     }
     unsigned long long* ctr = ctr_copy(P.counters);
     wave_add_u64(ctr + 0, C.rays);
@@ -101,8 +96,8 @@ __global__ void __launch_bounds__(256) k_resolve(ResolveParams P) {
     __syncthreads();
     const uint32_t slot = blockIdx.x * 256u + threadIdx.x;
     const float inv = 1.f / (float)P.samples;    // src/scene.cpp:201: (1.f / SAMPLES) * sum
-    const float m[3] = {inv * P.st.sum[slot], inv * P.st.sum[P.st.n_slots + slot],
-                        inv * P.st.sum[2u * P.st.n_slots + slot]};
+    const f3 s = load_sum(P.st, slot);
+    const float m[3] = {inv * s.x, inv * s.y, inv * s.z};
     uint8_t* o = P.out + (size_t)slot * 3u;
 #pragma unroll
     for (int c = 0; c < 3; ++c) o[c] = (uint8_t)quantize_gamma(aces1(m[c]), thr);

@@ -32,19 +32,6 @@
 
 namespace pt {
 
-__device__ __forceinline__ Rng load_rng(const PixelState& st, uint32_t slot) {
-    Rng R;
-    R.x = st.rng_x[slot];
-    R.saved = st.rng_saved[slot];
-    R.saved_ok = st.rng_flag[slot];
-    return R;
-}
-__device__ __forceinline__ void store_rng(const PixelState& st, uint32_t slot, const Rng& R) {
-    st.rng_x[slot] = R.x;
-    st.rng_saved[slot] = R.saved;
-    st.rng_flag[slot] = R.saved_ok;
-}
-
 // the pixel of an owned slot (slot = local tile * 256 + lane)
 __device__ __forceinline__ void slot_xy(const TileMap& tm, uint32_t slot, uint32_t& x, uint32_t& y) {
     slot_pixel(tm, slot >> 8, slot & 255u, x, y);
@@ -77,9 +64,10 @@ __device__ __forceinline__ Ray camera_sample(const CamView& cam, Rng& R, uint32_
 // `sdone` returns whether a sample of the pixel ended here.
 __device__ __forceinline__ bool shade_item(const WaveParams& P, uint32_t slot, Ray& ray, uint32_t hid, bool& sdone) {
     bool emit = false;
-    uint32_t nv = P.pstate[slot] & 0xffu;
+    PixelHot hot = load_hot(P.st, slot);     // one 16-B load: RNG, vertex count, samples done
+    uint32_t nv = hot.nv;
     uint32_t end = PE_LIVE;
-    Rng R = load_rng(P.st, slot);
+    Rng R = hot.R;
     if (hid == 0xffffffffu) {
         end = PE_MISS;
     } else {
@@ -90,7 +78,7 @@ __device__ __forceinline__ bool shade_item(const WaveParams& P, uint32_t slot, R
         uint32_t idm;
         float s1, s2;
         const bool cont = shade_vertex(P.S, R, ray, h, (int)hid, idm, s1, s2);
-        HbmVStore vs{P.vscratch + slot, P.st.n_slots};
+        HbmVStore vs = fold_store(P.st, slot);
         vs.put(nv, idm, s1, s2);
         ++nv;
         if (!cont) end = PE_TERM;
@@ -101,18 +89,16 @@ __device__ __forceinline__ bool shade_item(const WaveParams& P, uint32_t slot, R
     if (end != PE_LIVE) {
         // path over: backward fold (deepest vertex first), src/scene.cpp:198 sum += ...
         f3 L = end == PE_MISS ? P.S.bg : mk3(0.f, 0.f, 0.f);
-        HbmVStore vs{P.vscratch + slot, P.st.n_slots};
+        HbmVStore vs = fold_store(P.st, slot);
         for (uint32_t k = nv; k > 0u; --k) {
             uint32_t idm;
             float s1, s2;
             vs.get(k - 1u, idm, s1, s2);
             L = fold_vertex(P.S, L, idm, s1, s2);
         }
-        P.st.sum[slot] = P.st.sum[slot] + L.x;
-        P.st.sum[P.st.n_slots + slot] = P.st.sum[P.st.n_slots + slot] + L.y;
-        P.st.sum[2u * P.st.n_slots + slot] = P.st.sum[2u * P.st.n_slots + slot] + L.z;
-        const uint32_t done = P.nsamp[slot] + 1u;
-        P.nsamp[slot] = done;
+        store_sum(P.st, slot, load_sum(P.st, slot) + L);   // src/scene.cpp:198 sum += RayTrace(...)
+        const uint32_t done = hot.done + 1u;
+        hot.done = done;
         nv = 0u;
         if (done < P.target) {
             // the pixel's next sample: jitter draws + camera ray
@@ -122,8 +108,9 @@ __device__ __forceinline__ bool shade_item(const WaveParams& P, uint32_t slot, R
             emit = true;
         }
     }
-    P.pstate[slot] = nv;
-    store_rng(P.st, slot, R);
+    hot.nv = nv;
+    hot.R = R;
+    store_hot(P.st, slot, hot);               // one 16-B store
     return emit;
 }
 
@@ -140,25 +127,25 @@ __global__ void __launch_bounds__(256) k_wcamera(WaveParams P) {
     bool want = false;
     Ray ray;
     if (ok) {
-        Rng R = load_rng(P.st, slot);
-        uint32_t done = P.nsamp[slot];
+        PixelHot hot = load_hot(P.st, slot);
+        Rng R = hot.R;
+        uint32_t done = hot.done;
         if (P.depth == 0u) {
             // RayTrace(.., 0) = 0: only the jitter draws and sum += 0 per sample
-            f3 sum = mk3(P.st.sum[slot], P.st.sum[P.st.n_slots + slot], P.st.sum[2u * P.st.n_slots + slot]);
+            f3 sum = load_sum(P.st, slot);
             for (; done < P.target; ++done) {
                 (void)camera_sample(P.cam, R, x, y);
                 sum = sum + mk3(0.f, 0.f, 0.f);
             }
-            P.st.sum[slot] = sum.x;
-            P.st.sum[P.st.n_slots + slot] = sum.y;
-            P.st.sum[2u * P.st.n_slots + slot] = sum.z;
-            P.nsamp[slot] = done;
+            store_sum(P.st, slot, sum);
         } else if (done < P.target) {
             ray = camera_sample(P.cam, R, x, y);
-            P.pstate[slot] = PE_LIVE << 8;
             want = true;
         }
-        store_rng(P.st, slot, R);
+        hot.R = R;
+        hot.done = done;
+        hot.nv = 0u;
+        store_hot(P.st, slot, hot);
     }
     // Pull order of the pass: pixels whose camera ray enters the BVH's boxes first
     // (the costly ones -- a pass ends with its slowest pixel, and pixels are pulled

@@ -89,8 +89,7 @@ struct pt_session {
     int dev = 0;
     pt::TileMap tm{};
     uint32_t n_tiles_local = 0, n_slots = 0, depth = 0;
-    pt::PixelState st{};
-    uint32_t* vscratch = nullptr;
+    pt::PixelState st{};          // per-slot records + fold records (device)
     unsigned long long* counters = nullptr;
     uint8_t* out = nullptr;
     float* rad = nullptr;
@@ -100,8 +99,6 @@ struct pt_session {
     bool path = false;            // path engine (k_wpath) rounds instead of {k_wisect, k_wshade}
     pt::F4* ring = nullptr;       // path engine: path_grid * PT_RING_F4
     uint32_t path_grid = 0, path_budget = 1024, path_runend = 0, path_sparse = 0, sparse_steps = 8;
-    uint32_t* pstate = nullptr;
-    uint32_t* nsamp = nullptr;    // samples completed per slot
     pt::F4* qbuf = nullptr;       // 10 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd, fq0.ri, fq1.ri
     uint32_t* hid = nullptr;      // n_slots (done.id)
     uint32_t* pidbuf = nullptr;   // 2 * n_slots (fresh queues' plane prims)
@@ -587,11 +584,11 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
     };
     if (hipSetDevice(ss->dev) != hipSuccess) return cleanup(fail(PT_E_HIP, "hipSetDevice failed"));
     const size_t n = std::max<size_t>(ss->n_slots, 1);
-    const size_t vwords = 3ull * std::max<uint32_t>(ss->depth, 1u) * n;
+    ss->st.depth = std::max<uint32_t>(ss->depth, 1u);
     if (hipStreamCreateWithFlags(&ss->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&ss->st.rng_x, n * 4) != hipSuccess || hipMalloc(&ss->st.rng_saved, n * 4) != hipSuccess ||
-        hipMalloc(&ss->st.rng_flag, n * 4) != hipSuccess || hipMalloc(&ss->st.sum, 3 * n * 4) != hipSuccess ||
-        hipMalloc(&ss->vscratch, vwords * 4) != hipSuccess || hipMalloc(&ss->counters, 8 * PT_CTR_COPIES * PT_CTR_STRIDE) != hipSuccess ||
+        hipMalloc(&ss->st.rec, 2 * n * sizeof(uint4)) != hipSuccess ||
+        hipMalloc(&ss->st.fold, (size_t)ss->st.depth * n * sizeof(uint4)) != hipSuccess ||
+        hipMalloc(&ss->counters, 8 * PT_CTR_COPIES * PT_CTR_STRIDE) != hipSuccess ||
         hipMalloc(&ss->out, 3 * n) != hipSuccess)
         return cleanup(fail(PT_E_OOM, "device allocation failed"));
     ss->st.n_slots = ss->n_slots;
@@ -607,15 +604,11 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // queue would make its queries run to the end inside the round)
         ss->carry_cap = (uint32_t)n;
         if (const char* g = getenv("PT_STRAGGLER")) ss->straggler_steps = (uint32_t)std::max(1, atoi(g));
-        if (hipMalloc(&ss->pstate, n * 4) != hipSuccess || hipMalloc(&ss->qbuf, 10 * n * 16) != hipSuccess ||
-            hipMalloc(&ss->hid, n * 4) != hipSuccess || hipMalloc(&ss->nsamp, n * 4) != hipSuccess ||
+        if (hipMalloc(&ss->qbuf, 10 * n * 16) != hipSuccess || hipMalloc(&ss->hid, n * 4) != hipSuccess ||
             hipMalloc(&ss->pidbuf, 2 * n * 4) != hipSuccess ||
             hipMalloc(&ss->carry, 2ull * ss->carry_cap * ss->carry_words * 4) != hipSuccess ||
             hipMalloc(&ss->ctl, 8 * PT_CTL_SET) != hipSuccess || hipHostMalloc(&ss->ctl_host, 64) != hipSuccess)
             return cleanup(fail(PT_E_OOM, "device allocation failed (wavefront buffers)"));
-        if (hipMemsetAsync(ss->nsamp, 0, n * 4, ss->stream) != hipSuccess ||
-            hipMemsetAsync(ss->pstate, 0, n * 4, ss->stream) != hipSuccess)
-            return cleanup(fail(PT_E_HIP, "memset failed"));
         hipDeviceProp_t pr;
         if (hipGetDeviceProperties(&pr, ss->dev) != hipSuccess) return cleanup(fail(PT_E_HIP, "device query failed"));
         ss->shade_grid = std::min<uint32_t>((uint32_t)std::max(1, pr.multiProcessorCount) * 8u,
@@ -703,9 +696,6 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.cam = ss->cam;
     wp.tm = ss->tm;
     wp.st = ss->st;
-    wp.vscratch = ss->vscratch;
-    wp.pstate = ss->pstate;
-    wp.nsamp = ss->nsamp;
     const size_t n = std::max<size_t>(ss->n_slots, 1);
     wp.fq[0] = pt::RayQ{ss->qbuf, ss->qbuf + n, reinterpret_cast<int*>(ss->pidbuf), ss->qbuf + 8 * n};
     wp.fq[1] = pt::RayQ{ss->qbuf + 2 * n, ss->qbuf + 3 * n, reinterpret_cast<int*>(ss->pidbuf) + n, ss->qbuf + 9 * n};
@@ -808,11 +798,11 @@ int trace_wave(pt_session* ss, uint32_t spp) {
         HIP_TRY(hipStreamSynchronize(ss->stream));
         if (const char* rl = getenv("PT_ROUNDLOG"); rl && *rl == '2') {
             // diagnostics: how far behind the pass target the unfinished pixels are
-            std::vector<uint32_t> ns(ss->n_slots);
-            HIP_TRY(hipMemcpy(ns.data(), ss->nsamp, ns.size() * 4, hipMemcpyDeviceToHost));
+            std::vector<uint4> rec(2ull * ss->n_slots);
+            HIP_TRY(hipMemcpy(rec.data(), ss->st.rec, rec.size() * sizeof(uint4), hipMemcpyDeviceToHost));
             std::vector<uint32_t> lag;
-            for (uint32_t v : ns)
-                if (v < wp.target) lag.push_back(wp.target - v);
+            for (uint32_t i = 0; i < ss->n_slots; ++i)
+                if (rec[2 * i].w < wp.target) lag.push_back(wp.target - rec[2 * i].w);
             std::sort(lag.begin(), lag.end());
             const size_t m = lag.size();
             fprintf(stderr, "round %u chains %u+%u unfinished %zu lag p50 %u p90 %u p99 %u max %u\n", ss->rounds,
@@ -874,7 +864,6 @@ int pt_session_trace(pt_session* ss, uint32_t spp) {
     tp.cam = ss->cam;
     tp.tm = ss->tm;
     tp.st = ss->st;
-    tp.vscratch = ss->vscratch;
     tp.counters = ss->counters;
     tp.depth = ss->depth;
     tp.spp = spp;
@@ -1000,11 +989,10 @@ void pt_session_free(pt_session* ss) {
     (void)hipSetDevice(ss->dev);
     if (ss->stream) (void)hipStreamSynchronize(ss->stream);
     finish_pending(ss);
-    (void)hipFree(ss->st.rng_x); (void)hipFree(ss->st.rng_saved); (void)hipFree(ss->st.rng_flag);
-    (void)hipFree(ss->st.sum); (void)hipFree(ss->vscratch); (void)hipFree(ss->counters);
+    (void)hipFree(ss->st.rec); (void)hipFree(ss->st.fold); (void)hipFree(ss->counters);
     (void)hipFree(ss->out); (void)hipFree(ss->rad); (void)hipFree(ss->wg_prof);
     (void)hipFree(ss->tile_order);
-    (void)hipFree(ss->pstate); (void)hipFree(ss->qbuf); (void)hipFree(ss->hid); (void)hipFree(ss->nsamp); (void)hipFree(ss->pidbuf);
+    (void)hipFree(ss->qbuf); (void)hipFree(ss->hid); (void)hipFree(ss->pidbuf);
     (void)hipFree(ss->carry); (void)hipFree(ss->ctl); (void)hipFree(ss->ring);
     if (ss->ctl_host) (void)hipHostFree(ss->ctl_host);
     if (ss->prog_host) (void)hipHostFree(ss->prog_host);
