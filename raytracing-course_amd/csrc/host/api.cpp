@@ -4,6 +4,7 @@
 // ../device/pt_kernels.hip.
 #include "pt.h"
 
+#include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 #include <math.h>
@@ -35,6 +36,50 @@ thread_local std::string g_err;
 int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
+}
+
+// RCCL is loaded on first use (the multi-GPU gather only): librccl is a ~570 MB
+// library, and mapping it at process start costs the one-GPU CLI its start-up.
+struct Rccl {
+    decltype(&ncclCommInitAll) CommInitAll = nullptr;
+    decltype(&ncclGather) Gather = nullptr;
+    decltype(&ncclGroupStart) GroupStart = nullptr;
+    decltype(&ncclGroupEnd) GroupEnd = nullptr;
+    decltype(&ncclGetErrorString) GetErrorString = nullptr;
+    bool ok = false;
+};
+const Rccl& rccl() {
+    static const Rccl r = [] {
+        Rccl x;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return x;
+        x.CommInitAll = reinterpret_cast<decltype(&ncclCommInitAll)>(dlsym(h, "ncclCommInitAll"));
+        x.Gather = reinterpret_cast<decltype(&ncclGather)>(dlsym(h, "ncclGather"));
+        x.GroupStart = reinterpret_cast<decltype(&ncclGroupStart)>(dlsym(h, "ncclGroupStart"));
+        x.GroupEnd = reinterpret_cast<decltype(&ncclGroupEnd)>(dlsym(h, "ncclGroupEnd"));
+        x.GetErrorString = reinterpret_cast<decltype(&ncclGetErrorString)>(dlsym(h, "ncclGetErrorString"));
+        x.ok = x.CommInitAll && x.Gather && x.GroupStart && x.GroupEnd && x.GetErrorString;
+        return x;
+    }();
+    return r;
+}
+
+// streams made ahead of time by pt_device_init (stream creation costs ~8 ms of
+// the runtime's first use), adopted by the next session on that device
+std::mutex g_spare_mu;
+std::map<int, std::vector<hipStream_t>> g_spare_streams;
+hipError_t take_stream(int dev, hipStream_t* s) {
+    {
+        std::lock_guard<std::mutex> lk(g_spare_mu);
+        auto& v = g_spare_streams[dev];
+        if (!v.empty()) {
+            *s = v.back();
+            v.pop_back();
+            return hipSuccess;
+        }
+    }
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
 }
 
 #define HIP_TRY(expr)                                                                                 \
@@ -408,6 +453,26 @@ int pt_device_init(int device) {
     HIP_TRY(hipFree(nullptr));                // creates the device context
     HIP_TRY(pt_preload_kernels_base());       // loads both code objects (no launch)
     HIP_TRY(pt_preload_kernels_wave());
+    {
+        // the runtime's copy path starts on its first transfer (tens of ms): do one
+        // now, and make the first session's stream
+        static std::mutex mu;
+        static std::map<int, bool> warmed;
+        std::lock_guard<std::mutex> lk(mu);
+        if (!warmed[device]) {
+            void* d = nullptr;
+            uint32_t h = 0;
+            hipStream_t s = nullptr;
+            HIP_TRY(hipMalloc(&d, 64));
+            HIP_TRY(hipMemcpy(d, &h, 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost));
+            HIP_TRY(hipFree(d));
+            HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+            std::lock_guard<std::mutex> lk2(g_spare_mu);
+            g_spare_streams[device].push_back(s);
+            warmed[device] = true;
+        }
+    }
     return PT_OK;
 }
 int pt_abi_version(void) { return PT_ABI_VERSION; }
@@ -585,7 +650,7 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
     if (hipSetDevice(ss->dev) != hipSuccess) return cleanup(fail(PT_E_HIP, "hipSetDevice failed"));
     const size_t n = std::max<size_t>(ss->n_slots, 1);
     ss->st.depth = std::max<uint32_t>(ss->depth, 1u);
-    if (hipStreamCreateWithFlags(&ss->stream, hipStreamNonBlocking) != hipSuccess ||
+    if (take_stream(ss->dev, &ss->stream) != hipSuccess ||
         hipMalloc(&ss->st.rec, 2 * n * sizeof(uint4)) != hipSuccess ||
         hipMalloc(&ss->st.fold, (size_t)ss->st.depth * n * sizeof(uint4)) != hipSuccess ||
         hipMalloc(&ss->counters, 8 * PT_CTR_COPIES * PT_CTR_STRIDE) != hipSuccess ||
@@ -791,7 +856,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             hipError_t e;
             while ((e = hipStreamQuery(ss->stream)) == hipErrorNotReady) {
                 ss->on_progress(__atomic_load_n(ss->prog_host, __ATOMIC_RELAXED));
-                std::this_thread::sleep_for(std::chrono::milliseconds(2));
+                std::this_thread::sleep_for(std::chrono::microseconds(500));
             }
             HIP_TRY(e);
         }
@@ -996,7 +1061,11 @@ void pt_session_free(pt_session* ss) {
     (void)hipFree(ss->carry); (void)hipFree(ss->ctl); (void)hipFree(ss->ring);
     if (ss->ctl_host) (void)hipHostFree(ss->ctl_host);
     if (ss->prog_host) (void)hipHostFree(ss->prog_host);
-    if (ss->stream) (void)hipStreamDestroy(ss->stream);
+    if (ss->stream) {
+        // back to the device's pool for the next session (no destroy/create per render)
+        std::lock_guard<std::mutex> lk(g_spare_mu);
+        g_spare_streams[ss->dev].push_back(ss->stream);
+    }
     delete ss;
 }
 
@@ -1047,7 +1116,8 @@ int gather_rccl(const std::vector<pt_session*>& sess, int dev0, uint32_t W, uint
         std::vector<int> devs(n);
         for (int g = 0; g < n; ++g) devs[g] = dev0 + g;
         std::vector<ncclComm_t> c(n);
-        if (ncclCommInitAll(c.data(), n, devs.data()) != ncclSuccess) return fail(PT_E_RCCL, "ncclCommInitAll failed");
+        if (!rccl().ok) return fail(PT_E_RCCL, "librccl.so.1 not loadable");
+        if (rccl().CommInitAll(c.data(), n, devs.data()) != ncclSuccess) return fail(PT_E_RCCL, "ncclCommInitAll failed");
         comms[key] = c;
     }
     auto& c = comms[key];
@@ -1075,11 +1145,12 @@ int gather_rccl(const std::vector<pt_session*>& sess, int dev0, uint32_t W, uint
                                    sess[g]->stream));
         if (g == 0 && hipMalloc(&buf.recv, cap * n) != hipSuccess) return fail(PT_E_OOM, "gather buffer");
     }
-    ncclResult_t r = ncclGroupStart();
+    const Rccl& R = rccl();
+    ncclResult_t r = R.GroupStart();
     for (int g = 0; g < n && r == ncclSuccess; ++g)
-        r = ncclGather(buf.send[(size_t)g], g == 0 ? buf.recv : nullptr, cap, ncclUint8, 0, c[g], sess[g]->stream);
-    if (r == ncclSuccess) r = ncclGroupEnd();
-    if (r != ncclSuccess) return fail(PT_E_RCCL, std::string("ncclGather: ") + ncclGetErrorString(r));
+        r = R.Gather(buf.send[(size_t)g], g == 0 ? buf.recv : nullptr, cap, ncclUint8, 0, c[g], sess[g]->stream);
+    if (r == ncclSuccess) r = R.GroupEnd();
+    if (r != ncclSuccess) return fail(PT_E_RCCL, std::string("ncclGather: ") + R.GetErrorString(r));
     std::vector<uint8_t> host(cap * n);
     HIP_TRY(hipSetDevice(dev0));
     HIP_TRY(hipMemcpyAsync(host.data(), buf.recv, cap * n, hipMemcpyDeviceToHost, sess[0]->stream));

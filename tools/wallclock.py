@@ -35,7 +35,7 @@ def main():
     for c in configs:
         src = scene(c)
         out = os.path.join(out_dir, "pt_%s.ppm" % c)
-        env = dict(os.environ, PT_STATS="1", PT_QUIET="1")
+        env = dict(os.environ, PT_STATS="2", PT_QUIET="1")
         t0 = time.perf_counter()
         r = subprocess.run([os.path.join(REPO, "run.sh"), src, out], env=env, capture_output=True, text=True)
         wall = time.perf_counter() - t0
@@ -48,9 +48,22 @@ def main():
         rays = int(m.get("rays", 0))
         rec = {"config": c, "wall_to_ppm_s": wall, "rays": rays, "render_ms": float(m.get("wall_ms", 0)),
                "kernel_ms": float(m.get("kernel_ms", 0)), "mray_s_wall": rays / wall / 1e6,
-               "mray_s_render": rays / (float(m.get("wall_ms", 1)) * 1e3), "ppm_md5": md5}
+               "mray_s_render": rays / (float(m.get("wall_ms", 1)) * 1e3), "ppm_md5": md5,
+               "fallbacks": int(m.get("fallbacks", 0)), "rounds": int(m.get("rounds", 0))}
+        ph = re.search(r"phases_ms: (.*)", r.stderr)
+        if ph:
+            rec["phases_ms"] = {k: float(v) for k, v in re.findall(r"(\w+)=([\d.]+)", ph.group(1))}
         if c in GOLDEN_MD5:
             rec["md5_matches_reference"] = md5 == GOLDEN_MD5[c]
+        ref = os.path.join(REPO, "oracle", "_ref", "raytracing_hw5")
+        if c in ("c1",) and os.path.exists(ref):
+            # the reference CLI on the same scene and host (hw5/run.sh), for the same wall-clock
+            t0 = time.perf_counter()
+            rr = subprocess.run([ref, src, out], capture_output=True)
+            rec["reference_wall_s"] = time.perf_counter() - t0
+            if rr.returncode == 0:
+                rec["reference_md5_same"] = hashlib.md5(open(out, "rb").read()).hexdigest() == md5
+                os.unlink(out)
         print(json.dumps(rec), flush=True)
 
 
