@@ -38,6 +38,9 @@ namespace pt {
 #define PT_AUXW 4               // auxiliary BVH width (nodes = PT_AUXW AuxSL entries)
 #endif
 
+// wide aux entry (AuxSL, 32 B): a = {lo.xyz, hi.x}, b = {hi.y, hi.z, leaf range, code}
+//   leaf range = (max reference leaf of the subtree >> S, rounded up) << 16 | (min >> S)
+//   (S = SceneView::aux_rshift; annotate_aux_ranges in host/aux_bvh.cpp)
 // stackless auxiliary node (32 B):
 //   internal: a = {lo.x, lo.y, lo.z, hi.x}, b = {hi.y, hi.z, u32 skip, 0xffffffff}
 //   leaf:     a = {c.x, c.y, c.z, s.x},     b = {s.y, s.z, u32 skip (= own index + 1), u32 reference leaf}
@@ -388,6 +391,8 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
             }
         }
         uint32_t next = 0xffffffffu;
+        // the largest kept candidate when the list is full (else none)
+        const uint32_t cmax = q.c[PT_QK - 1];
 #pragma unroll
         for (int k = 0; k < PT_AUXW; ++k) {
             // every entry's box is conservative: a reference leaf passing it is a
@@ -396,7 +401,13 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
             const uint32_t code = f2u(r[2 * k + 1].w);
             const bool h = hit[k] && code != 0xffffffffu;
             const bool leaf = h && (code & 0x80000000u) != 0u && (code & 0x7fffffffu) >= q.lb;
-            const bool inner = h && (code & 0x80000000u) == 0u;
+            // a subtree is skipped when all its leaves lie below lb (processed in an
+            // earlier pass), or above the largest kept candidate of a full list: it
+            // could only add candidates the list would drop, so another pass follows
+            const uint32_t rng = f2u(r[2 * k + 1].z);
+            const bool above = cmax != 0xffffffffu && ((rng & 0xffffu) << S.aux_rshift) > cmax;
+            const bool inner = h && (code & 0x80000000u) == 0u && ((rng >> 16) << S.aux_rshift) >= q.lb && !above;
+            if (h && (code & 0x80000000u) == 0u && above) q.overflow = 1u;
             if (pt_any(leaf)) {
 #ifdef PT_QDIAG
                 if (leaf) C.cands++;

@@ -124,6 +124,7 @@ struct pt_scene {
     std::vector<pt::F4> blob;   // the wavefront query's fetch space (pt_core.h SceneView::blob)
     uint32_t o_nodes = 0, o_aux = 0, o_ainfo = 0, o_anc = 0, o_qprim = 0, o_prim = 0;
     uint32_t auxw_stack = 0;    // per-lane stack words of the wide aux traversal
+    uint32_t aux_rshift = 0;    // leaf-range packing of the wide aux entries (annotate_aux_ranges)
     float thr[256];
     std::map<int, DevScene> dev;
     std::mutex mu;
@@ -356,6 +357,7 @@ void set_blob(pt::SceneView& v, const pt_scene* s, const pt::F4* blob) {
     v.blob = blob;
     v.o_nodes = s->o_nodes; v.o_aux = s->o_aux; v.o_ainfo = s->o_ainfo;
     v.o_anc = s->o_anc; v.o_qprim = s->o_qprim; v.o_prim = s->o_prim;
+    v.aux_rshift = s->aux_rshift;
 }
 
 pt::SceneView host_view(const pt_scene* s, int traversal) {
@@ -541,6 +543,7 @@ int pt_scene_prepare(pt_scene* s) {
         if (!std::isfinite(s->box_extent)) s->box_extent = INFINITY;   // certification then never succeeds
         pth::build_aux_bvh(s->nodes, s->aux, s->aux_depth);
         pth::build_aux_wide(s->aux, s->dnodes, PT_AUXW, s->auxsl, s->auxsl_depth, s->auxw_stack);
+        pth::annotate_aux_ranges(s->auxsl, PT_AUXW, (uint32_t)s->dnodes.size(), s->aux_rshift);
         // Query::sp (pt_query.h) counts pending aux nodes in a 7-bit field
         if (s->auxw_stack > PT_QUERY_SP_MAX)
             throw std::runtime_error("auxiliary BVH too deep for the query's stack counter");

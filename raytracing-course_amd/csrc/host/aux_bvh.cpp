@@ -348,4 +348,37 @@ void build_aux_wide(const std::vector<pt::AuxNode>& pairs, const std::vector<pt:
     max_stack = (W - 1) * max_depth + 1;
 }
 
+// Reference-leaf index range of every entry's subtree, packed into the entry's
+// spare word (AuxSL b.z): (max >> shift, rounded up) << 16 | (min >> shift).
+// The query skips a subtree whose leaves all lie below the pass's lower bound
+// (already processed in an earlier pass), or -- with its candidate list full --
+// all lie above the list's largest kept candidate (flagging another pass), so a
+// ray with many candidates does not re-walk the whole aux tree in every pass.
+void annotate_aux_ranges(std::vector<pt::AuxSL>& out, uint32_t W, uint32_t n_ref_nodes, uint32_t& shift) {
+    shift = 0;
+    const uint64_t top = n_ref_nodes ? n_ref_nodes - 1u : 0u;
+    while (((top + (1ull << shift) - 1) >> shift) > 0xffffull) ++shift;
+    const size_t nn = out.size() / W;
+    std::vector<uint32_t> lo(nn, 0xFFFFFFFFu), hi(nn, 0u);
+    for (size_t n = nn; n-- > 0;) {
+        for (uint32_t k = 0; k < W; ++k) {
+            uint32_t* u = reinterpret_cast<uint32_t*>(&out[n * W + k]);
+            const uint32_t code = u[7];
+            if (code == 0xFFFFFFFFu) continue;
+            uint32_t mn, mx;
+            if (code & 0x80000000u) {
+                mn = mx = code & 0x7FFFFFFFu;
+            } else {
+                if (code <= n || code >= nn) throw std::runtime_error("aux wide tree: child before its parent");
+                mn = lo[code];
+                mx = hi[code];
+            }
+            lo[n] = std::min(lo[n], mn);
+            hi[n] = std::max(hi[n], mx);
+            const uint32_t mxq = (uint32_t)(((uint64_t)mx + (1ull << shift) - 1) >> shift);
+            u[6] = (mxq << 16) | (mn >> shift);
+        }
+    }
+}
+
 }  // namespace pth

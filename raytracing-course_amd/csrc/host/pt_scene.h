@@ -57,6 +57,9 @@ void build_aux_stackless(const std::vector<pt::AuxNode>& pairs, const std::vecto
 void build_aux_wide(const std::vector<pt::AuxNode>& pairs, const std::vector<pt::Node>& dnodes, uint32_t W,
                     std::vector<pt::AuxSL>& out, uint32_t& max_depth, uint32_t& max_stack);
 
+// per-entry reference-leaf ranges of the wide aux BVH (aux_bvh.cpp)
+void annotate_aux_ranges(std::vector<pt::AuxSL>& out, uint32_t W, uint32_t n_ref_nodes, uint32_t& shift);
+
 // Gamma/quantise threshold table (tonemap.cpp)
 void build_gamma_thresholds(float thr[256]);
 
