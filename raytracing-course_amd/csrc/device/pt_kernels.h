@@ -94,10 +94,9 @@ struct WaveParams {
     uint32_t n_tiles_local;
     uint32_t max_stack;           // exact DFS stack words per lane
     uint32_t aux_stack;           // wide aux traversal stack words per lane (LDS)
-    uint32_t straggler_steps;     // steps a query may run after its wave ran out of work, before suspending
     unsigned long long* wg_prof;  // optional (diagnostics): per isect workgroup {start, end, HW_ID, XCC_ID, steps}
     // path engine (k_wpath): chains continue inside the kernel
-    uint32_t path;                // 1 = path engine rounds (k_wshade then shades the exact-DFS results only)
+    uint32_t path;                // 1 (k_wshade shades the exact-DFS results only)
     uint32_t path_budget;         // loop trips a query wave keeps its chains going after the round's work ran out
     uint32_t path_runend;         // a round with at most this many chains runs them to the end of the pass
     unsigned long long* progress; // optional host-mapped count of finished samples (progress bar), or null
@@ -135,11 +134,8 @@ hipError_t pt_launch_init(const pt::InitParams& p, uint32_t n_tiles, hipStream_t
 // variant: bit 0 = filtered node tests + flat replay, bit 1 = XCD-banded tile order
 hipError_t pt_launch_trace(const pt::TraceParams& p, int variant, uint32_t lds_bytes, hipStream_t s);
 // wavefront pipeline (pt_wave.hip): start a pass (first camera ray of every
-// owned pixel), then rounds of {closest-hit, exact, shade}
+// owned pixel), then path-engine rounds
 hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s);
-// e0/e1 (optional): events recorded around the k_wisect launch (its time for the roofline)
-hipError_t pt_launch_wave_round(pt::WaveParams p, uint32_t isect_grid, uint32_t shade_grid, hipStream_t s,
-                                hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 // path engine round: {k_wpath, k_wexact, k_wshade (exact results)}
 // sparse: the end-of-pass kernel (few chains: every step kind and several steps per trip)
 hipError_t pt_launch_path_round(pt::WaveParams p, uint32_t path_grid, uint32_t shade_grid, hipStream_t s, bool sparse,

@@ -1,23 +1,21 @@
 // pt_wave.hip -- wavefront form of the hw5 render loop on gfx950.
 //
 // A pass advances every owned pixel by `target` samples (src/scene.cpp:
-// 189-203) through rounds of three launches on one stream:
+// 189-203) through rounds of launches on one stream:
 //
 //   k_wcamera   (pass start) the first sample's 2 jitter draws and camera
 //               ray (src/scene.cpp:180-199) of every pixel -> fresh queue
 //   round r (parity p):
-//     k_wisect  persistent, per-lane refilling closest-hit query
-//               (pt_query.h): lanes pull fresh rays and suspended queries in
-//               wave batches and advance one node step per loop trip.  Once
-//               its wave has no more work to pull, a query may run
-//               `straggler_steps` more steps; then it is suspended (state +
-//               LDS stack to the carry queue) and resumes next round, so no
-//               round waits for the slowest ray of the frame
+//     k_wpath   the path engine (below): persistent query waves + a shade
+//               wave per workgroup; a pixel's chain (its one ray in flight)
+//               keeps going inside the kernel; once the round's work is used
+//               up, running queries are suspended (state + LDS stack to the
+//               carry queue) and resume next round
 //     k_wexact  the rare rays handed to the exact stack DFS
-//     k_wshade  per finished query: the vertex (shade_vertex: material logic
-//               and random draws) and its fold record, then either the child
-//               ray, or -- path over -- the backward fold into the pixel sum
-//               and the next sample's camera ray
+//     k_wshade  shades k_wexact's results: the vertex (shade_vertex: material
+//               logic and random draws) and its fold record, then either the
+//               child ray, or -- path over -- the backward fold into the pixel
+//               sum and the next sample's camera ray
 //
 // Every pixel has at most one ray in flight and consumes its random stream
 // in the reference order (jitter, then vertex by vertex), so results are
@@ -205,185 +203,6 @@ __global__ void __launch_bounds__(256) k_wcamera_merge(WaveParams P) {
 #ifndef PT_REFILL_MIN
 #define PT_REFILL_MIN 4u    // idle lanes before a wave refills
 #endif
-
-__global__ void __launch_bounds__(256) k_wisect(WaveParams P) {
-    extern __shared__ uint32_t lds_stack[];
-    LdsMem stk{lds_stack + threadIdx.x};
-    const uint32_t p = P.parity;
-    const uint32_t* in = P.ctl + PT_CTL_SET * p;
-    uint32_t* out = P.ctl + PT_CTL_SET * (1u - p);
-    const uint32_t n_carry = in[C_CARRY], n_total = in[C_FRESH] + n_carry;
-    // Sparse rounds (the end of a pass: only the slowest pixels' rays are left)
-    // are latency-bound: spread the rays over all waves (small batches) and let
-    // each query run longer before it is suspended (a suspension costs a round).
-    const uint32_t n_waves = gridDim.x * (blockDim.x / 64u);
-    uint32_t bsz = n_total / n_waves;
-    bsz = bsz < 1u ? 1u : (bsz > PT_BATCH ? PT_BATCH : bsz);
-    const uint32_t budget = P.straggler_steps * (PT_BATCH / bsz);
-    const RayQ FQ = P.fq[p];
-    const uint32_t* CQ = P.cq[p];
-    uint32_t* CQout = P.cq[1u - p];
-    // wave-uniform batch of work indices: [0, n_carry) suspended queries first (they
-    // are the slow pixels' rays: fetched early they get the whole round), then fresh rays
-    // Batches are handed out by one counter per XCD: batch b = 8k + x is the k-th
-    // of XCD x's counter and covers [b*bsz, (b+1)*bsz) -- the XCDs advance together,
-    // so the global order (carried first) holds approximately; a wave whose XCD's
-    // share is used up steals from the next XCD's counter (xs = counters found empty).
-    const uint32_t xcc = xcc_id();
-    uint32_t xs = 0u;
-    uint32_t bbase = 0u, bleft = 0u;
-    bool exhausted = false;
-    bool active = false;
-    uint32_t slot = 0u, post = 0u, wi = 0u;
-    Query q;
-    QCounts C{0u, 0u, 0u, 0u};
-    uint32_t rays = 0u, fallbacks = 0u, init_exact = 0u;
-    uint64_t t_start = 0, iters = 0;
-#ifdef PT_WPROF
-    uint64_t cyc_refill = 0, cyc_step = 0, nact = 0, naux = 0;
-#endif
-    if (P.wg_prof && threadIdx.x == 0) t_start = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        iters++;
-#ifdef PT_WPROF
-        const uint64_t c0 = __builtin_amdgcn_s_memtime();
-#endif
-        const unsigned long long idle = __ballot(!active);
-        uint32_t nidle = (uint32_t)__popcll(idle);
-        if (!exhausted && (nidle >= PT_REFILL_MIN || nidle == 64u)) {
-            uint32_t rank = lanes_below(idle);
-            bool got = false;
-            while (nidle > 0u) {
-                if (bleft == 0u) {
-                    uint32_t v = 0xffffffffu;
-                    if (lane_id() == 0u) {
-                        while (xs < 8u) {
-                            const uint32_t y = (xcc + xs) & 7u;
-                            const uint64_t b = 8ull * atomicAdd(out + C_HEADS + 32u * y, 1u) + y;
-                            if (b * bsz < n_total) { v = (uint32_t)(b * bsz); break; }
-                            ++xs;
-                        }
-                    }
-                    v = __builtin_amdgcn_readfirstlane(v);
-                    xs = __builtin_amdgcn_readfirstlane(xs);
-                    if (v == 0xffffffffu) { exhausted = true; break; }
-                    bbase = v;
-                    bleft = n_total - v < bsz ? n_total - v : bsz;
-                }
-                const uint32_t take = nidle < bleft ? nidle : bleft;
-                if (!active && !got) {
-                    if (rank < take) { wi = bbase + rank; got = true; }
-                    else rank -= take;
-                }
-                bbase += take;
-                bleft -= take;
-                nidle -= take;
-            }
-            if (got) {
-                post = 0u;
-                if (wi >= n_carry) {
-                    const uint32_t fi = wi - n_carry;   // fresh-queue index (wi stays the done index)
-                    const F4 o = FQ.ro[fi], d = FQ.rd[fi];
-                    Ray ray;
-                    ray.o = mk3(o.x, o.y, o.z);
-                    ray.d = mk3(d.x, d.y, d.z);
-                    slot = f2u(o.w);
-                    rays++;
-                    C.planes += P.S.n_planes;
-                    q_init_pre(ray, d.w, FQ.pid[fi], FQ.ri[fi], q);
-                    if (q.phase == Q_EXACT) init_exact++;
-                } else {
-                    // resume a suspended query: state, slot, then its aux stack into LDS
-                    const uint32_t* w = CQ + (size_t)wi * P.carry_words;
-                    q = *reinterpret_cast<const Query*>(w);
-                    const uint32_t* tail = w + sizeof(Query) / 4u;
-                    slot = tail[0];
-                    for (uint32_t k = 0; k < q.sp; ++k) stk.set(k, tail[1u + k]);
-                }
-                active = true;
-            }
-        }
-        if (__ballot(active) == 0ull) break;
-#ifdef PT_WPROF
-        const uint64_t c1 = __builtin_amdgcn_s_memtime();
-        cyc_refill += c1 - c0;
-        const uint32_t ph = active ? (q.phase == Q_AUX ? 0u : 1u + q.walk) : 5u;
-        const unsigned long long pm = __ballot(ph == 0u) ;
-        nact += (uint64_t)__popcll(__ballot(active));
-        naux += (uint64_t)__popcll(pm);
-#endif
-        // phase vote: the step code of one phase kind per trip (the kinds' code
-        // paths would otherwise all be issued every trip); lanes of other kinds wait
-        const uint32_t kind = !active ? 7u : q.phase == Q_AUX ? 0u : q.phase == Q_REPLAY ? 1u + q.walk : 6u;
-        uint32_t pick = 6u;
-#if PT_VOTE
-        {
-            uint32_t best = 0u;
-#pragma unroll
-            for (uint32_t k = 0; k < 5u; ++k) {
-                const uint32_t c = (uint32_t)__popcll(__ballot(kind == k));
-                if (c > best) { best = c; pick = k; }
-            }
-        }
-#endif
-        if (active) {
-            if ((q.phase == Q_AUX || q.phase == Q_REPLAY) && (!PT_VOTE || kind == pick)) q_step(P.S, q, C, stk);
-            if (q.phase == Q_DONE) {
-                // results stay at the work index: no compaction, no atomics
-                const uint32_t k = wi;
-                P.done.ro[k] = F4{q.ray.o.x, q.ray.o.y, q.ray.o.z, u2f(slot)};
-                P.done.rd[k] = F4{q.ray.d.x, q.ray.d.y, q.ray.d.z, 0.f};
-                P.done.id[k] = q.res_id < 0 ? 0xffffffffu : (uint32_t)q.res_id;
-                active = false;
-            } else if (q.phase == Q_EXACT) {
-                const uint32_t k = atomicAdd(out + C_EXACT, 1u);   // rare
-                P.ex.ro[k] = F4{q.ray.o.x, q.ray.o.y, q.ray.o.z, u2f(slot)};
-                P.ex.rd[k] = F4{q.ray.d.x, q.ray.d.y, q.ray.d.z, u2f(wi)};
-                fallbacks++;
-                active = false;
-            } else if (exhausted && ++post >= budget) {
-                // this wave has nothing left to pull: suspend instead of holding up the round
-                // (carry_cap = pixel slots >= rays in flight: the queue never overflows)
-                const uint32_t k = wave_append(out + C_CARRY, true);
-                uint32_t* w = CQout + (size_t)k * P.carry_words;
-                *reinterpret_cast<Query*>(w) = q;
-                uint32_t* tail = w + sizeof(Query) / 4u;
-                tail[0] = slot;
-                for (uint32_t j = 0; j < q.sp; ++j) tail[1u + j] = stk.get(j);
-                P.done.id[wi] = PT_SUSPENDED;
-                active = false;
-            }
-        }
-#ifdef PT_WPROF
-        cyc_step += __builtin_amdgcn_s_memtime() - c1;
-#endif
-    }
-    unsigned long long* ctr = ctr_copy(P.counters);
-    wave_add_u64(ctr + 0, rays);
-    wave_add_u64(ctr + 1, C.nodes);
-    wave_add_u64(ctr + 2, C.ptests);
-    wave_add_u64(ctr + 3, C.planes);
-    wave_add_u64(ctr + 5, C.aux);
-    wave_add_u64(ctr + 6, fallbacks);
-    wave_add_u64(ctr + 7, init_exact);
-    if (P.wg_prof) {
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long* w = P.wg_prof + 9ull * blockIdx.x;
-            w[0] = t_start;
-            w[1] = __builtin_amdgcn_s_memrealtime();
-            w[2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-            w[3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
-            w[4] = iters;
-#ifdef PT_WPROF
-            w[5] = cyc_refill;
-            w[6] = cyc_step;
-            w[7] = nact;
-            w[8] = naux;
-#endif
-        }
-    }
-}
 
 // ---- path engine -------------------------------------------------------------
 // k_wpath: persistent and warp-specialised.  A workgroup is PT_NQ query waves
@@ -1006,10 +825,9 @@ __global__ void __launch_bounds__(64) k_wexact(WaveParams P) {
 
 __global__ void __launch_bounds__(256) k_wshade(WaveParams P) {
     __shared__ uint32_t agg[5];
-    const uint32_t* in = P.ctl + PT_CTL_SET * P.parity;
     uint32_t* out = P.ctl + PT_CTL_SET * (1u - P.parity);
-    // round engine: every work index of the round; path engine: the exact-DFS results only
-    const uint32_t n = P.path ? out[C_EXACT] : in[C_FRESH] + in[C_CARRY];
+    // the exact-DFS results of this round (the path engine shades everything else itself)
+    const uint32_t n = out[C_EXACT];
     const RayQ N = P.fq[1u - P.parity];
     const uint32_t stride = gridDim.x * 256u;
     // grid-stride with a block-uniform trip count (the block-aggregated append needs every thread)
@@ -1071,16 +889,4 @@ hipError_t pt_launch_path_round(pt::WaveParams p, uint32_t path_grid, uint32_t s
     return hipGetLastError();
 }
 
-hipError_t pt_launch_wave_round(pt::WaveParams p, uint32_t isect_grid, uint32_t shade_grid, hipStream_t s,
-                                hipEvent_t e0, hipEvent_t e1) {
-    hipError_t e = hipMemsetAsync(p.ctl + PT_CTL_SET * (1u - p.parity), 0, 4u * PT_CTL_SET, s);
-    if (e != hipSuccess) return e;
-    if (e0 && (e = hipEventRecord(e0, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(pt::k_wisect, dim3(isect_grid), dim3(256), 1024u * p.aux_stack, s, p);
-    if (e1 && (e = hipEventRecord(e1, s)) != hipSuccess) return e;
-    const uint32_t exact_lds = 64u * 4u * (p.max_stack ? p.max_stack : 1u);
-    hipLaunchKernelGGL(pt::k_wexact, dim3(64), dim3(64), exact_lds, s, p);
-    hipLaunchKernelGGL(pt::k_wshade, dim3(shade_grid), dim3(256), 0, s, p);
-    return hipGetLastError();
-}
 }

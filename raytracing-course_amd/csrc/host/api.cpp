@@ -65,6 +65,41 @@ const Rccl& rccl() {
     return r;
 }
 
+// Tuning and diagnostics switch: ONE environment variable, read where a
+// session or pass starts, PT_TUNE="key=value,key=value".  None of it is needed
+// for a correct or a fast render; the keys exist for A/B runs and diagnostics
+// (INTEGRATION.md "Tuning and diagnostics"):
+//   engine=mega       megakernel instead of the wavefront path engine (replay traversal)
+//   budget=N          path engine: trips a query wave keeps its chains after the round's work ran out
+//   wg_per_cu=N       path engine: workgroups per CU (grid)
+//   runend=N          a round with at most N chains runs them to the end of the pass
+//   sparse=N          rounds with fewer than N chains run the end-of-pass kernel
+//   sparse_steps=N    steps per loop trip of the end-of-pass kernel
+//   cap=N             chains a workgroup may hold
+//   rowmajor=1        seed a pass in row-major tile order instead of Z-order
+//   variant=V         megakernel variant bits (1 filtered tests, 2 XCD-banded tiles)
+//   roundlog=1|2      per-round kernel times / pixels' remaining samples on stderr
+//   wgprof=FILE       per-workgroup timelines (-DPT_WPROF builds)
+//   qstats=FILE       per-query work counters of the host self-test render
+std::string tune_str(const char* key) {
+    const char* e = getenv("PT_TUNE");
+    if (!e) return {};
+    const std::string k = std::string(key) + "=";
+    for (const char* p = e; *p;) {
+        const char* q = strchr(p, ',');
+        const std::string item(p, q ? (size_t)(q - p) : strlen(p));
+        if (item.compare(0, k.size(), k) == 0) return item.substr(k.size());
+        if (!q) break;
+        p = q + 1;
+    }
+    return {};
+}
+bool tune_has(const char* key) { return !tune_str(key).empty(); }
+int tune_int(const char* key, int def) {
+    const std::string v = tune_str(key);
+    return v.empty() ? def : atoi(v.c_str());
+}
+
 // streams made ahead of time by pt_device_init (stream creation costs ~8 ms of
 // the runtime's first use), adopted by the next session on that device
 std::mutex g_spare_mu;
@@ -142,17 +177,16 @@ struct pt_session {
     unsigned long long* wg_prof = nullptr;
     // wavefront engine buffers (replay traversal)
     bool wave = false;
-    bool path = false;            // path engine (k_wpath) rounds instead of {k_wisect, k_wshade}
     pt::F4* ring = nullptr;       // path engine: path_grid * PT_RING_F4
     uint32_t path_grid = 0, path_budget = 1024, path_runend = 0, path_sparse = 0, sparse_steps = 8;
     pt::F4* qbuf = nullptr;       // 10 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd, fq0.ri, fq1.ri
     uint32_t* hid = nullptr;      // n_slots (done.id)
     uint32_t* pidbuf = nullptr;   // 2 * n_slots (fresh queues' plane prims)
     uint32_t* carry = nullptr;    // 2 * carry_cap * carry_words
-    uint32_t carry_cap = 0, carry_words = 0, straggler_steps = 64;
+    uint32_t carry_cap = 0, carry_words = 0;
     uint32_t* ctl = nullptr;      // 2 x PT_CTL_SET round counters
     uint32_t* ctl_host = nullptr; // pinned copy of one counter set
-    uint32_t isect_grid = 0, shade_grid = 0, rounds = 0;
+    uint32_t shade_grid = 0, rounds = 0;
     hipStream_t stream = nullptr;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, pending_isect;
     double kernel_ms = 0.0, resolve_ms = 0.0, isect_ms = 0.0;
@@ -401,8 +435,8 @@ int finish_pending(pt_session* ss) {
         (void)hipEventDestroy(e.second);
     }
     ss->pending.clear();
-    const char* rlog = getenv("PT_ROUNDLOG");   // diagnostics: per-launch ms of the rounds, one line per sync
-    const bool log = rlog && *rlog == '1' && !ss->pending_isect.empty();
+    // diagnostics (PT_TUNE roundlog=1): per-launch ms of the rounds, one line per sync
+    const bool log = tune_int("roundlog", 0) == 1 && !ss->pending_isect.empty();
     if (log) fprintf(stderr, "rounds_ms");
     for (auto& e : ss->pending_isect) {
         float ms = 0.f;
@@ -663,7 +697,7 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
     // engine: the wavefront pipeline for the (filtered) replay traversal; the
     // megakernel for the exact DFS and the division-form replay (PT_ENGINE=mega forces it)
     ss->wave = o->traversal == PT_TRAVERSAL_REPLAY;
-    if (const char* e = getenv("PT_ENGINE")) ss->wave = ss->wave && strcmp(e, "mega") != 0;
+    if (tune_str("engine") == "mega") ss->wave = false;
     if (ss->wave) {
         // suspended-query records: Query | slot | aux stack, rounded to 16 B
         ss->carry_words = ((uint32_t)(sizeof(pt::Query) / 4) + 1u + std::max<uint32_t>(s->auxw_stack, 1u) + 3u) & ~3u;
@@ -671,7 +705,6 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // suspended at once: the carry queue can never overflow (an over-full
         // queue would make its queries run to the end inside the round)
         ss->carry_cap = (uint32_t)n;
-        if (const char* g = getenv("PT_STRAGGLER")) ss->straggler_steps = (uint32_t)std::max(1, atoi(g));
         if (hipMalloc(&ss->qbuf, 10 * n * 16) != hipSuccess || hipMalloc(&ss->hid, n * 4) != hipSuccess ||
             hipMalloc(&ss->pidbuf, 2 * n * 4) != hipSuccess ||
             hipMalloc(&ss->carry, 2ull * ss->carry_cap * ss->carry_words * 4) != hipSuccess ||
@@ -681,25 +714,18 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         if (hipGetDeviceProperties(&pr, ss->dev) != hipSuccess) return cleanup(fail(PT_E_HIP, "device query failed"));
         ss->shade_grid = std::min<uint32_t>((uint32_t)std::max(1, pr.multiProcessorCount) * 8u,
                                             std::max(1u, ss->n_tiles_local));
-        // persistent intersection grid: 3 workgroups per CU (the resident limit), capped by the work
-        ss->isect_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * 3u;
-        if (const char* g = getenv("PT_ISECT_WG_PER_CU")) ss->isect_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * (uint32_t)std::max(1, atoi(g));
-        ss->isect_grid = std::min(ss->isect_grid, std::max(1u, ss->n_tiles_local));
         // path engine: PT_NQ query waves + 1 shade wave per workgroup, 3 workgroups per CU
-        const char* eng = getenv("PT_ENGINE");
-        ss->path = !(eng && strcmp(eng, "round") == 0);
-        if (const char* b = getenv("PT_PATH_BUDGET")) ss->path_budget = (uint32_t)std::max(1, atoi(b));
-        ss->path_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * 3u;
-        if (const char* g = getenv("PT_PATH_WG_PER_CU")) ss->path_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * (uint32_t)std::max(1, atoi(g));
+        ss->path_budget = (uint32_t)std::max(1, tune_int("budget", (int)ss->path_budget));
+        ss->path_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * (uint32_t)std::max(1, tune_int("wg_per_cu", 3));
         // a round whose chains are this few runs them to the end of the pass (a few
         // per query wave: rebalancing them costs more rounds than it saves)
         ss->path_runend = ss->path_grid * PT_NQ * 4u;
-        if (const char* b = getenv("PT_PATH_RUNEND")) ss->path_runend = (uint32_t)std::max(0, atoi(b));
+        ss->path_runend = (uint32_t)std::max(0, tune_int("runend", (int)ss->path_runend));
         // rounds with fewer chains than this run the end-of-pass (sparse) kernel
         ss->path_sparse = ss->path_grid * PT_NQ * 32u;
-        if (const char* b = getenv("PT_PATH_SPARSE")) ss->path_sparse = (uint32_t)std::max(0, atoi(b));
-        if (const char* b = getenv("PT_SPARSE_STEPS")) ss->sparse_steps = (uint32_t)std::max(1, atoi(b));
-        if (ss->path && hipMalloc(&ss->ring, (size_t)ss->path_grid * PT_RING_F4 * sizeof(pt::F4)) != hipSuccess)
+        ss->path_sparse = (uint32_t)std::max(0, tune_int("sparse", (int)ss->path_sparse));
+        ss->sparse_steps = (uint32_t)std::max(1, tune_int("sparse_steps", (int)ss->sparse_steps));
+        if (hipMalloc(&ss->ring, (size_t)ss->path_grid * PT_RING_F4 * sizeof(pt::F4)) != hipSuccess)
             return cleanup(fail(PT_E_OOM, "device allocation failed (path rings)"));
         if (ss->n_tiles_local) {
             // seeding order of the pass: the local tiles sorted by the Z-order (Morton)
@@ -780,8 +806,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.n_tiles_local = ss->n_tiles_local;
     wp.max_stack = std::max<uint32_t>(s->max_stack, 1u);
     wp.aux_stack = std::max<uint32_t>(s->auxw_stack, 1u);
-    wp.straggler_steps = ss->straggler_steps;
-    wp.path = ss->path ? 1u : 0u;
+    wp.path = 1u;
     wp.path_budget = ss->path_budget;
     wp.path_runend = ss->path_runend;
     // Chains a workgroup may hold: PT_CMAX when the pixels outnumber that, else a
@@ -792,8 +817,8 @@ int trace_wave(pt_session* ss, uint32_t spp) {
         const uint64_t share = ((uint64_t)ss->n_slots + ss->path_grid - 1) / std::max(1u, ss->path_grid);
         wp.path_cap = (uint32_t)std::min<uint64_t>(PT_CMAX, std::max<uint64_t>(256u, share * 15u / 16u));
     }
-    if (const char* c = getenv("PT_PATH_CAP")) wp.path_cap = std::min<uint32_t>(PT_CMAX, (uint32_t)std::max(64, atoi(c)));
-    wp.tile_order = getenv("PT_ROWMAJOR") ? nullptr : ss->tile_order;
+    if (tune_has("cap")) wp.path_cap = std::min<uint32_t>(PT_CMAX, (uint32_t)std::max(64, tune_int("cap", 0)));
+    wp.tile_order = tune_int("rowmajor", 0) ? nullptr : ss->tile_order;
     wp.sparse_steps = ss->sparse_steps;
     wp.ring = ss->ring;
     if (ss->on_progress && !ss->prog_host) {
@@ -816,12 +841,12 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     for (uint32_t guard = 0;; ++guard) {
         for (uint32_t r = 0; r < batch; ++r) {
             wp.parity = p;
-            const char* wgp = getenv("PT_WGPROF");
-            if (wgp && *wgp) {
-                // diagnostics: per-round isect workgroup timelines appended to $PT_WGPROF
-                // round engine: 9 u64 per isect workgroup; path engine: 16 u64 per path workgroup
-                const size_t wgb = ss->path ? 256ull * ss->path_grid : 72ull * ss->isect_grid;
-                if (!ss->wg_prof) HIP_TRY(hipMalloc(&ss->wg_prof, 256ull * std::max(ss->isect_grid, ss->path_grid)));
+            const std::string wgps = tune_str("wgprof");
+            const char* wgp = wgps.c_str();
+            if (*wgp) {
+                // diagnostics: per-round path workgroup timelines (32 u64 each) appended to the file
+                const size_t wgb = 256ull * ss->path_grid;
+                if (!ss->wg_prof) HIP_TRY(hipMalloc(&ss->wg_prof, wgb));
                 HIP_TRY(hipMemsetAsync(ss->wg_prof, 0, wgb, ss->stream));
                 wp.wg_prof = ss->wg_prof;
             }
@@ -830,10 +855,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             HIP_TRY(hipEventCreate(&i1));
             ss->pending_isect.emplace_back(i0, i1);
             ss->isect_launches++;
-            if (ss->path)
-                HIP_TRY(pt_launch_path_round(wp, ss->path_grid, 64u, ss->stream, sparse, i0, i1));
-            else
-                HIP_TRY(pt_launch_wave_round(wp, ss->isect_grid, ss->shade_grid, ss->stream, i0, i1));
+            HIP_TRY(pt_launch_path_round(wp, ss->path_grid, 64u, ss->stream, sparse, i0, i1));
             if (wp.wg_prof) {
                 uint32_t cnt[2][8];
                 HIP_TRY(hipMemcpyAsync(cnt[0], ss->ctl + PT_CTL_SET * p, 32, hipMemcpyDeviceToHost, ss->stream));
@@ -842,7 +864,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 fprintf(stderr, "round %u: in fresh %u carry %u -> out fresh %u carry %u exact %u\n", ss->rounds,
                         cnt[0][pt::C_FRESH], cnt[0][pt::C_CARRY], cnt[1][pt::C_FRESH], cnt[1][pt::C_CARRY],
                         cnt[1][pt::C_EXACT]);
-                std::vector<unsigned long long> h(ss->path ? 32ull * ss->path_grid : 9ull * ss->isect_grid);
+                std::vector<unsigned long long> h(32ull * ss->path_grid);
                 HIP_TRY(hipMemcpyAsync(h.data(), wp.wg_prof, h.size() * 8, hipMemcpyDeviceToHost, ss->stream));
                 HIP_TRY(hipStreamSynchronize(ss->stream));
                 if (FILE* f = fopen(wgp, "ab")) {
@@ -864,7 +886,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             HIP_TRY(e);
         }
         HIP_TRY(hipStreamSynchronize(ss->stream));
-        if (const char* rl = getenv("PT_ROUNDLOG"); rl && *rl == '2') {
+        if (tune_int("roundlog", 0) == 2) {
             // diagnostics: how far behind the pass target the unfinished pixels are
             std::vector<uint4> rec(2ull * ss->n_slots);
             HIP_TRY(hipMemcpy(rec.data(), ss->st.rec, rec.size() * sizeof(uint4), hipMemcpyDeviceToHost));
@@ -938,12 +960,13 @@ int pt_session_trace(pt_session* ss, uint32_t spp) {
     tp.n_tiles_local = ss->n_tiles_local;
     tp.wg_prof = nullptr;
     // kernel variant: filtered tests unless the division form was asked for;
-    // XCD-banded tile order by default (PT_VARIANT=<0..3> overrides, for A/B runs)
+    // XCD-banded tile order by default (PT_TUNE variant=<0..3> overrides, for A/B runs)
     int variant = (ss->traversal == PT_TRAVERSAL_REPLAY ? 1 : 0) | 2;
-    if (const char* v = getenv("PT_VARIANT")) variant = atoi(v) & 3;
+    if (tune_has("variant")) variant = tune_int("variant", 0) & 3;
     if (ss->traversal == PT_TRAVERSAL_EXACT) variant &= 2;
-    const char* wgp = getenv("PT_WGPROF");
-    if (wgp && *wgp) {
+    const std::string wgps = tune_str("wgprof");
+    const char* wgp = wgps.c_str();
+    if (*wgp) {
         if (!ss->wg_prof) HIP_TRY(hipMalloc(&ss->wg_prof, 32ull * std::max(ss->n_tiles_local, 1u)));
         HIP_TRY(hipMemsetAsync(ss->wg_prof, 0, 32ull * std::max(ss->n_tiles_local, 1u), ss->stream));
         tp.wg_prof = ss->wg_prof;
@@ -957,7 +980,7 @@ int pt_session_trace(pt_session* ss, uint32_t spp) {
     HIP_TRY(pt_launch_trace(tp, variant, lds, ss->stream));
     HIP_TRY(hipEventRecord(e1, ss->stream));
     if (tp.wg_prof) {
-        // diagnostics: append this launch's per-workgroup timeline to $PT_WGPROF
+        // diagnostics: append this launch's per-workgroup timeline to the wgprof file
         std::vector<unsigned long long> h(4ull * ss->n_tiles_local);
         HIP_TRY(hipMemcpyAsync(h.data(), tp.wg_prof, h.size() * 8, hipMemcpyDeviceToHost, ss->stream));
         HIP_TRY(hipStreamSynchronize(ss->stream));
@@ -1379,7 +1402,8 @@ int pt_selftest_render_host(pt_scene* s, int32_t traversal, uint32_t x0, uint32_
     std::vector<std::thread> th;
     std::vector<uint32_t> errs(nt, 0);
     // diagnostics: PT_QSTATS=<file> dumps per-query {aux visits, node tests, prim tests, exact} (u32 x4)
-    const char* qpath = getenv("PT_QSTATS");
+    const std::string qpaths = tune_str("qstats");
+    const char* qpath = qpaths.empty() ? nullptr : qpaths.c_str();
     std::vector<std::vector<std::array<uint32_t, 4>>> qlogs(nt);
     for (uint32_t t = 0; t < nt; ++t) {
         th.emplace_back([&, t]() {

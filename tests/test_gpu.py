@@ -151,21 +151,18 @@ def test_device_init(pt):
     assert pt._lib.pt_device_init(4096) == pt.PT_E_NO_GPU
 
 
-@pytest.mark.parametrize("engine", ["path", "path_dense", "round"])
-@pytest.mark.parametrize("straggler", ["1", "3"])
+@pytest.mark.parametrize("engine", ["path", "path_dense"])
+@pytest.mark.parametrize("budget", ["1", "3"])
 @pytest.mark.parametrize("name", ["c3s4_win_944_520_16x16", "c4glass_s4_win_900_560_16x16", "dragon_64x64x16",
-                                  "hw3s4_48x48x8"])
-def test_suspended_queries_resume_bit_exact(pt, name, straggler, engine, monkeypatch):
-    """Force the wavefront engine to suspend almost every query after 1-3 steps
-    past its wave's last fetch (PT_STRAGGLER, read at session creation): queries
-    then resume from the carry queue over many rounds, interleaving pixels'
-    samples arbitrarily -- results must not change.  "path" lets the path engine
-    switch to its end-of-pass (sparse) kernel once few chains are left, as it does
-    by default; "path_dense" keeps the main kernel for every round."""
-    monkeypatch.setenv("PT_ENGINE", "round" if engine == "round" else "path")
-    monkeypatch.setenv("PT_PATH_SPARSE", "0" if engine == "path_dense" else "100000000")
-    monkeypatch.setenv("PT_STRAGGLER", straggler)     # round engine
-    monkeypatch.setenv("PT_PATH_BUDGET", straggler)   # path engine: trips after the round's work ran out
+                                  "hw3s4_48x48x8", "c2_win_240_200_24x24"])
+def test_suspended_queries_resume_bit_exact(pt, name, budget, engine, monkeypatch):
+    """Force the path engine to suspend almost every query 1-3 loop trips after
+    its wave ran out of round work (PT_TUNE budget, read at session creation):
+    queries then resume from the carry queue over many rounds, interleaving
+    pixels' samples arbitrarily -- results must not change.  "path" lets the
+    engine switch to its end-of-pass (sparse) kernel once few chains are left,
+    as it does by default; "path_dense" keeps the main kernel for every round."""
+    monkeypatch.setenv("PT_TUNE", "budget=%s,sparse=%s" % (budget, "0" if engine == "path_dense" else "100000000"))
     m, img, rad = U.golden_image(name)
     with pt.Scene.load(U.golden_scene_path(name)) as s:
         s.prepare()
@@ -177,18 +174,14 @@ def test_suspended_queries_resume_bit_exact(pt, name, straggler, engine, monkeyp
     assert np.array_equal(rgb, img)
 
 
-@pytest.mark.parametrize("name", ["c3s4_win_944_520_16x16", "c4glass_s4_win_900_560_16x16", "dragon_64x64x16",
-                                  "hw3s4_48x48x8", "c2_win_240_200_24x24"])
-def test_round_engine_bit_exact(pt, name, monkeypatch):
-    """The round engine ({k_wisect, k_wshade} per round, PT_ENGINE=round) on the
-    golden fixtures (the default path engine is covered above)."""
-    monkeypatch.setenv("PT_ENGINE", "round")
-    m, img, rad = U.golden_image(name)
-    with pt.Scene.load(U.golden_scene_path(name)) as s:
-        s.prepare()
-        win = tuple(m["window"]) if m["window"] else None
-        rgb, r, st = s.render(radiance=True, window=win, traversal=0)
-    assert st["errors"] == 0
+def test_megakernel_engine_bit_exact(pt, monkeypatch):
+    """PT_TUNE engine=mega: the megakernel (one lane per pixel, whole paths) on the
+    replay traversal gives the same bytes as the path engine"""
+    monkeypatch.setenv("PT_TUNE", "engine=mega")
+    m, img, rad = U.golden_image("dragon_64x64x16")
+    with pt.Scene.load(U.golden_scene_path("dragon_64x64x16")) as s:
+        rgb, r, st = s.render(radiance=True, traversal=0)
+    assert st["rounds"] == 0 and st["errors"] == 0
     assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
     assert np.array_equal(rgb, img)
 

@@ -1,9 +1,8 @@
-# rank_sim over library variants: VARS="name:libdir:ENV=val,ENV=val ..."
+# rank_sim over library builds: VARS="name:libdir[:key=v+key=v] ..." (optional PT_TUNE settings)
 cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && mkdir -p gpurun_out/var2 || exit 1
 for spec in $VARS; do
-  IFS=: read name lib vars <<< "$spec"
-  envs=$(echo "$vars" | tr ',' ' ')
-  env PT_LIB=raytracing-course_amd/$lib/libpt.so $envs timeout -k 10 300 python3 tools/rank_sim.py --worlds ${WORLDS:-1 8} --steps ${STEPS:-2} > gpurun_out/var2/$name.jsonl 2> gpurun_out/var2/$name.err || { echo "FAILED $name"; tail -3 gpurun_out/var2/$name.err; exit 1; }
+  IFS=: read name lib tune <<< "$spec"
+  PT_LIB=raytracing-course_amd/$lib/libpt.so PT_TUNE=$(echo "$tune" | tr '+' ',') timeout -k 10 300 python3 tools/rank_sim.py --worlds ${WORLDS:-1 8} --steps ${STEPS:-2} > gpurun_out/var2/$name.jsonl 2> gpurun_out/var2/$name.err || { echo "FAILED $name"; tail -3 gpurun_out/var2/$name.err; exit 1; }
   echo "$name: $(python3 -c "
 import json
 for l in open('gpurun_out/var2/$name.jsonl'):

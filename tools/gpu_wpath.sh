@@ -4,7 +4,7 @@ for spec in ${LIBS:-wprof:build_wprof}; do
   IFS=: read name lib <<< "$spec"
   for w in ${WORLDS:-8 1}; do
     rm -f /tmp/wg.bin
-    PT_LIB=raytracing-course_amd/$lib/libpt.so PT_WGPROF=/tmp/wg.bin timeout -k 10 300 python3 tools/rank_sim.py --worlds $w --steps 1 > gpurun_out/wprof/${name}_w$w.jsonl 2> gpurun_out/wprof/${name}_w$w.err || exit 1
+    PT_LIB=raytracing-course_amd/$lib/libpt.so PT_TUNE=wgprof=/tmp/wg.bin timeout -k 10 300 python3 tools/rank_sim.py --worlds $w --steps 1 > gpurun_out/wprof/${name}_w$w.jsonl 2> gpurun_out/wprof/${name}_w$w.err || exit 1
     echo "== $name w$w $(tail -1 gpurun_out/wprof/${name}_w$w.jsonl)"
     python3 tools/wg_path.py /tmp/wg.bin 768 || exit 1
     python3 tools/wg_tail.py /tmp/wg.bin 768 > gpurun_out/wprof/${name}_tail_w$w.txt
