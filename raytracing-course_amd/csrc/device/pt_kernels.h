@@ -104,6 +104,7 @@ struct WaveParams {
     const uint32_t* tile_order;   // k_wcamera: block b seeds local tile tile_order[b] (null: tile b)
     uint32_t sparse_steps;        // steps per loop trip of the end-of-pass (sparse) kernel
     F4* ring;                     // per-workgroup ray/done rings, PT_RING_F4 F4 per workgroup
+    uint32_t coop_slim;           // k_wcoop: aux stack size above which a wave expands fewer nodes per round
 };
 
 // path engine geometry: PT_NQ query waves + 1 shade wave per workgroup; at most
@@ -117,6 +118,15 @@ struct WaveParams {
 #endif
 // per workgroup: ray ring ro, rd; PT_NQ done rings ro, rd; ray-ring plane ids
 #define PT_RING_F4 ((3u + 2u * PT_NQ) * PT_CMAX + PT_CMAX / 4u)
+
+// cooperative engine (k_wcoop, the end of a pass): one wave per chain, QC_WAVES
+// independent waves per workgroup, per-wave LDS for the query (pt_wave.hip QcLds)
+#ifndef QC_WAVES
+#define QC_WAVES 4u
+#endif
+#define QC_SCAP 448u               // aux node stack words per wave (also lane 0's exact DFS stack)
+#define QC_CCAP 320u               // candidate leaves per wave (< 64 + 4 x 64 at any time)
+#define QC_HCAP 64u                // hitting leaves per query (more: the exact DFS)
 
 struct ResolveParams {
     PixelState st;
@@ -140,4 +150,7 @@ hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s);
 // sparse: the end-of-pass kernel (few chains: every step kind and several steps per trip)
 hipError_t pt_launch_path_round(pt::WaveParams p, uint32_t path_grid, uint32_t shade_grid, hipStream_t s, bool sparse,
                                 hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+// cooperative engine: one launch runs every remaining chain of the pass to its end
+hipError_t pt_launch_coop(pt::WaveParams p, uint32_t grid, hipStream_t s, hipEvent_t e0 = nullptr,
+                          hipEvent_t e1 = nullptr);
 hipError_t pt_launch_resolve(const pt::ResolveParams& p, uint32_t n_tiles, hipStream_t s);

@@ -26,6 +26,7 @@
 
 #include "pt_devutil.h"
 #include "pt_kernels.h"
+#include "pt_coop.h"
 #include "pt_query.h"
 
 namespace pt {
@@ -798,6 +799,250 @@ __global__ void __launch_bounds__(PT_PATH_WG) __attribute__((amdgpu_waves_per_eu
 #endif
 }
 
+// ---- cooperative engine (end of a pass) ---------------------------------------
+// k_wcoop: ONE wave per pixel chain, run to the end of the pass.  With few chains
+// left, the path engine's lanes idle while every chain waits on its own long
+// sequence of dependent steps and ring hand-offs; here a chain's query is spread
+// over the wave's lanes (pt_coop.h: breadth-first aux expansion, every candidate
+// leaf and its primitives at once, a root path as one round of loads) and the
+// wave shades the result itself, so nothing waits in a ring.
+struct QcLds {
+    uint32_t stk[QC_SCAP];         // pending aux nodes (also the exact DFS stack of lane 0)
+    uint32_t cand[QC_CCAP];        // candidate leaves; after the expansion the sorted hitting leaves
+    uint32_t h_idx[QC_HCAP], h_t[QC_HCAP], h_lid[QC_HCAP];   // hitting leaves (unsorted)
+    uint32_t r_idx[QC_HCAP], r_t[QC_HCAP];                   // entered hits so far (preorder)
+};
+
+// The query of one ray by the whole wave (every argument wave-uniform).
+// `slim` = stack size above which the expansion takes fewer nodes per round
+// (host: QC_SCAP - 4 (aux depth + 2), so a depth-first descent still fits).
+// Returns the closest prim (-1 none); `exact` set = hand the ray to the exact DFS.
+__device__ int qc_wave(const SceneView& S, QcLds& L, const Ray& ray, float P, int pid, F4 pre, uint32_t slim,
+                       QCounts& C, bool& exact) {
+    const uint32_t lane = lane_id();
+    exact = pre.w != pre.w;
+    if (exact) return -1;
+    const bool par = signbit(pre.w);
+    const f3 inv = mk3(pre.x, pre.y, pre.z);
+    const f3 oinv = mk3(ray.o.x * inv.x, ray.o.y * inv.y, ray.o.z * inv.z);
+    uint32_t ns = 1u, nc = 0u, nh = 0u;
+    bool ovf = false;
+    if (lane == 0u) L.stk[0] = 0u;
+    for (;;) {
+        // 2. candidate leaves, 64 at a time (the rest once the expansion is over):
+        //    bound-free slab test, then the first strict minimum over the primitives
+        while (nc >= 64u || (ns == 0u && nc > 0u)) {
+            const uint32_t take = nc < 64u ? nc : 64u;
+            nc -= take;
+            const bool act = lane < take;
+            const uint32_t c = act ? L.cand[nc + lane] : 0u;
+            const Node nd = S.nodes[c];
+            C.nodes += act ? 1u : 0u;
+            const bool hb = act && qc_slab_hit(nd, ray, inv, par);
+            const uint32_t ref = f2u(nd.b.z), cnt = hb ? f2u(nd.b.w) : 0u;
+            float lt = PT_INF;
+            int lid = -1;
+            for (uint32_t i = 0; __ballot(i < cnt) != 0ull; ++i) {
+                if (i < cnt) {
+                    Hit hh;
+                    C.ptests++;
+                    if (bvh_prim_intersect(S.prims[ref + i], ray, hh) && hh.t < lt) { lt = hh.t; lid = (int)(ref + i); }
+                }
+            }
+            const unsigned long long m = __ballot(lid >= 0);
+            const uint32_t nm = (uint32_t)__popcll(m);
+            if (nh + nm > QC_HCAP) {
+                ovf = true;
+            } else if (lid >= 0) {
+                const uint32_t j = nh + lanes_below(m);
+                L.h_idx[j] = c;
+                L.h_t[j] = f2u(lt);
+                L.h_lid[j] = (uint32_t)lid;
+            }
+            nh += nm;
+        }
+        if (ns == 0u || ovf) break;
+        // 1. breadth-first expansion of the wide aux BVH: one node per lane
+        uint32_t k = slim > ns ? (slim - ns) / 3u : 0u;
+        k = k < 1u ? 1u : k;
+        k = k > 64u ? 64u : k;
+        k = k > ns ? ns : k;
+        if (ns + 3u * k > QC_SCAP) { ovf = true; break; }   // cannot happen with the host's slim (checked)
+        ns -= k;
+        const bool act = lane < k;
+        const uint32_t node = act ? L.stk[ns + lane] : 0u;
+        C.aux += act ? 1u : 0u;
+        const uint32_t b = S.o_aux + node * (uint32_t)(PT_AUXW * sizeof(AuxSL));
+        F4 r[2 * PT_AUXW];
+#pragma unroll
+        for (uint32_t e = 0; e < 2u * PT_AUXW; ++e) r[e] = blob_piece(S, b + 16u * e);
+#pragma unroll
+        for (uint32_t e = 0; e < PT_AUXW; ++e) {
+            const F4 ea = r[2 * e], eb = r[2 * e + 1];
+            const uint32_t code = f2u(eb.w);
+            bool h = act && code != 0xffffffffu;
+            if (h) h = par ? aux_box_par(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, ray, inv, oinv)
+                           : aux_box(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, inv, oinv);
+            const bool leaf = h && (code & 0x80000000u) != 0u;
+            const bool inner = h && (code & 0x80000000u) == 0u;
+            const unsigned long long mi = __ballot(inner), ml = __ballot(leaf);
+            if (inner) L.stk[ns + lanes_below(mi)] = code;
+            if (leaf) L.cand[nc + lanes_below(ml)] = code & 0x7fffffffu;
+            ns += (uint32_t)__popcll(mi);
+            nc += (uint32_t)__popcll(ml);
+        }
+    }
+    if (ovf) {
+        exact = true;
+        return -1;
+    }
+    // 3. the hitting leaves in reference preorder (distinct indices: rank = count below)
+    if (nh > 1u) {
+        const bool act = lane < nh;
+        const uint32_t c = act ? L.h_idx[lane] : 0u, t = act ? L.h_t[lane] : 0u, id = act ? L.h_lid[lane] : 0u;
+        uint32_t rank = 0u;
+        for (uint32_t j = 0; j < nh; ++j) rank += L.h_idx[j] < c ? 1u : 0u;
+        if (act) {
+            L.cand[rank] = c;
+            L.cand[64u + rank] = t;
+            L.cand[128u + rank] = id;
+        }
+    } else if (nh == 1u && lane == 0u) {
+        L.cand[0] = L.h_idx[0];
+        L.cand[64] = L.h_t[0];
+        L.cand[128] = L.h_lid[0];
+    }
+    uint32_t nrec = 0u;
+    float bt = PT_INF;
+    int res = pid;
+    for (uint32_t k = 0; k < nh; ++k) {
+        const uint32_t c = L.cand[k];
+        const float lt = u2f(L.cand[64u + k]);
+        const uint32_t info = S.anc_info[c];
+        const uint32_t off = info & 0x03ffffffu, len = info >> 26;
+        const bool on = lane < len;
+        const uint32_t v = on ? S.anc[off + lane] : 0u;
+        const uint32_t prev = __shfl(v, (int)(lane == 0u ? 0u : lane - 1u), 64);
+        const Node nd = S.nodes[v];
+        C.nodes += on ? 1u : 0u;
+        // the carried bound: at a right child the minimum over the entered hits of its
+        // left sibling's subtree (prev, v), if any; else the parent's (scan down the path)
+        const bool rc = on && lane > 0u && v != prev + 1u;
+        float m = 0.f;
+        bool any = false;
+        for (uint32_t q = 0; q < nrec; ++q) {
+            const uint32_t ri = L.r_idx[q];
+            const float rt = u2f(L.r_t[q]);
+            if (rc && ri > prev && ri < v) {
+                if (!any || rt < m) m = rt;
+                any = true;
+            }
+        }
+        const unsigned long long dm = __ballot(any);
+        const unsigned long long below = dm & ((2ull << lane) - 1ull);
+        const int src = below ? 63 - __clzll((long long)below) : (int)lane;
+        const float mb = __shfl(m, src, 64);
+        const float bound = below ? mb : P;
+        const bool ok = !on || node_enter(nd, ray, inv, bound, par);
+        if (__ballot(!ok) == 0ull) {
+            // 4. entered: record; first strict minimum; replaces the plane iff closer
+            if (lane == 0u) {
+                L.r_idx[nrec] = c;
+                L.r_t[nrec] = f2u(lt);
+            }
+            ++nrec;
+            if (lt < bt) {
+                bt = lt;
+                if (lt < P) res = (int)L.cand[128u + k];
+            }
+        }
+    }
+    return res;
+}
+
+__device__ __forceinline__ float bcast_f(float v) { return u2f(__builtin_amdgcn_readfirstlane(f2u(v))); }
+
+__global__ void __launch_bounds__(64u * QC_WAVES) k_wcoop(WaveParams P) {
+    __shared__ QcLds Ls[QC_WAVES];
+    QcLds& L = Ls[threadIdx.x >> 6];
+    const uint32_t lane = lane_id();
+    const uint32_t* in = P.ctl + PT_CTL_SET * P.parity;
+    uint32_t* out = P.ctl + PT_CTL_SET * (1u - P.parity);
+    const uint32_t n_carry = in[C_CARRY], n_total = in[C_FRESH] + n_carry;
+    const RayQ FQ = P.fq[P.parity];
+    QCounts C{0u, 0u, 0u, 0u};
+    uint32_t rays = 0u, fallbacks = 0u, prog = 0u;
+    for (;;) {
+        uint32_t gi = 0u;
+        if (lane == 0u) gi = atomicAdd(out + C_HEADS, 1u);
+        gi = __builtin_amdgcn_readfirstlane(gi);
+        if (gi >= n_total) break;
+        Ray ray;
+        float Pt;
+        int pid;
+        F4 pre;
+        uint32_t slot;
+        if (gi < n_carry) {
+            // a query suspended by the path engine: restarted from its ray (a query is a
+            // function of the ray alone; its ray and plane tests were counted when taken)
+            const uint32_t* w = P.cq[P.parity] + (size_t)gi * P.carry_words;
+            ray = reinterpret_cast<const Query*>(w)->ray;
+            slot = w[sizeof(Query) / 4u];
+            q_planes(P.S, ray, Pt, pid);
+            pre = q_prep(P.S, ray);
+        } else {
+            const uint32_t fi = gi - n_carry;
+            const F4 o = FQ.ro[fi], d = FQ.rd[fi];
+            ray.o = mk3(o.x, o.y, o.z);
+            ray.d = mk3(d.x, d.y, d.z);
+            slot = f2u(o.w);
+            Pt = d.w;
+            pid = FQ.pid[fi];
+            pre = FQ.ri[fi];
+            if (lane == 0u) { rays++; C.planes += P.S.n_planes; }
+        }
+        for (;;) {
+            bool ex;
+            int id = qc_wave(P.S, L, ray, Pt, pid, pre, P.coop_slim, C, ex);
+            if (ex) {
+                // the exact stack DFS on lane 0 (non-finite rays, > QC_HCAP hitting leaves)
+                if (lane == 0u) {
+                    LdsMemN<1u> stk{L.stk};
+                    Hit h;
+                    id = q_exact(P.S, ray, stk, h, C);
+                    fallbacks++;
+                }
+                id = __builtin_amdgcn_readfirstlane(id);
+            }
+            bool emit = false, sdone = false;
+            if (lane == 0u) {
+                emit = shade_item(P, slot, ray, id < 0 ? 0xffffffffu : (uint32_t)id, sdone);
+                prog += sdone ? 1u : 0u;
+                if (emit) { rays++; C.planes += P.S.n_planes; }
+            }
+            if (!__builtin_amdgcn_readfirstlane(emit ? 1u : 0u)) break;
+            // the chain's next ray (lane 0's), its plane test and query set-up on every lane
+            ray.o = mk3(bcast_f(ray.o.x), bcast_f(ray.o.y), bcast_f(ray.o.z));
+            ray.d = mk3(bcast_f(ray.d.x), bcast_f(ray.d.y), bcast_f(ray.d.z));
+            q_planes(P.S, ray, Pt, pid);
+            pre = q_prep(P.S, ray);
+        }
+        if (P.progress && lane == 0u && prog >= 256u) {
+            __hip_atomic_fetch_add(P.progress, (unsigned long long)prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            prog = 0u;
+        }
+    }
+    if (P.progress && lane == 0u && prog)
+        __hip_atomic_fetch_add(P.progress, (unsigned long long)prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    unsigned long long* ctr = ctr_copy(P.counters);
+    wave_add_u64(ctr + 0, rays);
+    wave_add_u64(ctr + 1, C.nodes);
+    wave_add_u64(ctr + 2, C.ptests);
+    wave_add_u64(ctr + 3, C.planes);
+    wave_add_u64(ctr + 5, C.aux);
+    wave_add_u64(ctr + 6, fallbacks);
+}
+
 // exact stack DFS for the handed-back rays; 64-lane workgroups, stack in LDS
 __global__ void __launch_bounds__(64) k_wexact(WaveParams P) {
     extern __shared__ uint32_t lds_stack[];
@@ -869,6 +1114,16 @@ hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s) {
     p.parity = 0u;
     hipLaunchKernelGGL(pt::k_wcamera, dim3(p.n_tiles_local), dim3(256), 0, s, p);
     hipLaunchKernelGGL(pt::k_wcamera_merge, dim3(p.n_tiles_local < 1024u ? p.n_tiles_local : 1024u), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_coop(pt::WaveParams p, uint32_t grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    hipError_t e = hipMemsetAsync(p.ctl + PT_CTL_SET * (1u - p.parity), 0, 4u * PT_CTL_SET, s);
+    if (e != hipSuccess) return e;
+    p.path = 1u;
+    if (e0 && (e = hipEventRecord(e0, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(pt::k_wcoop, dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
+    if (e1 && (e = hipEventRecord(e1, s)) != hipSuccess) return e;
     return hipGetLastError();
 }
 

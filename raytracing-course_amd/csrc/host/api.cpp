@@ -26,6 +26,7 @@
 #include <thread>
 #include <vector>
 
+#include "../device/pt_coop.h"
 #include "../device/pt_kernels.h"
 #include "pt_scene.h"
 
@@ -75,12 +76,15 @@ const Rccl& rccl() {
 //   runend=N          a round with at most N chains runs them to the end of the pass
 //   sparse=N          rounds with fewer than N chains run the end-of-pass kernel
 //   sparse_steps=N    steps per loop trip of the end-of-pass kernel
+//   coop=N            a round with at most N chains runs the cooperative engine (one wave
+//                     per chain) to the end of the pass (0: never)
 //   cap=N             chains a workgroup may hold
 //   rowmajor=1        seed a pass in row-major tile order instead of Z-order
 //   variant=V         megakernel variant bits (1 filtered tests, 2 XCD-banded tiles)
 //   roundlog=1|2      per-round kernel times / pixels' remaining samples on stderr
 //   wgprof=FILE       per-workgroup timelines (-DPT_WPROF builds)
 //   qstats=FILE       per-query work counters of the host self-test render
+//   qengine=coop      host self-tests: the cooperative engine's query algorithm (pt_coop.h)
 std::string tune_str(const char* key) {
     const char* e = getenv("PT_TUNE");
     if (!e) return {};
@@ -179,6 +183,7 @@ struct pt_session {
     bool wave = false;
     pt::F4* ring = nullptr;       // path engine: path_grid * PT_RING_F4
     uint32_t path_grid = 0, path_budget = 1024, path_runend = 0, path_sparse = 0, sparse_steps = 8;
+    uint32_t coop_max = 0, coop_grid = 0, coop_slim = 0;   // cooperative engine (k_wcoop) at the end of a pass
     pt::F4* qbuf = nullptr;       // 10 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd, fq0.ri, fq1.ri
     uint32_t* hid = nullptr;      // n_slots (done.id)
     uint32_t* pidbuf = nullptr;   // 2 * n_slots (fresh queues' plane prims)
@@ -725,6 +730,19 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         ss->path_sparse = ss->path_grid * PT_NQ * 32u;
         ss->path_sparse = (uint32_t)std::max(0, tune_int("sparse", (int)ss->path_sparse));
         ss->sparse_steps = (uint32_t)std::max(1, tune_int("sparse_steps", (int)ss->sparse_steps));
+        // a round whose chains are at most this many runs the cooperative engine (one
+        // wave per chain) to the end of the pass; it needs a wave's aux stack to hold
+        // a depth-first descent below its expansion limit, and lane 0's exact DFS stack
+        const uint32_t cus = (uint32_t)std::max(1, pr.multiProcessorCount);
+        ss->coop_max = cus * 256u;   // 65,536 on the 256-CU part (rank-of-8 sweep: 4 k / 16 k / 64 k)
+        ss->coop_max = (uint32_t)std::max(0, tune_int("coop", (int)ss->coop_max));
+        ss->coop_grid = cus * 8u;
+        const uint32_t reserve = 4u * (s->auxsl_depth + 2u);
+        if (QC_SCAP < reserve + 64u || s->max_stack > QC_SCAP) ss->coop_max = 0;
+        else ss->coop_slim = QC_SCAP - reserve;
+        // with the cooperative engine the path engine never runs a round to the end:
+        // its rounds stay budget-limited, so the host sees the chains fall below coop_max
+        if (ss->coop_max && !tune_has("runend")) ss->path_runend = 0;
         if (hipMalloc(&ss->ring, (size_t)ss->path_grid * PT_RING_F4 * sizeof(pt::F4)) != hipSuccess)
             return cleanup(fail(PT_E_OOM, "device allocation failed (path rings)"));
         if (ss->n_tiles_local) {
@@ -820,6 +838,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     if (tune_has("cap")) wp.path_cap = std::min<uint32_t>(PT_CMAX, (uint32_t)std::max(64, tune_int("cap", 0)));
     wp.tile_order = tune_int("rowmajor", 0) ? nullptr : ss->tile_order;
     wp.sparse_steps = ss->sparse_steps;
+    wp.coop_slim = ss->coop_slim;
     wp.ring = ss->ring;
     if (ss->on_progress && !ss->prog_host) {
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ss->prog_host), 8, hipHostMallocMapped | hipHostMallocCoherent));
@@ -838,7 +857,35 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     // end-of-pass kernel when the chains of the last counted round are few; before
     // the first count, the pass's pixels (at most one chain each) decide
     bool sparse = ss->n_slots < ss->path_sparse;
+    // the cooperative engine once the chains are few (before the first count: the pixels)
+    uint32_t chains = ss->n_slots;
     for (uint32_t guard = 0;; ++guard) {
+        if (chains <= ss->coop_max) {
+            // one launch runs every remaining chain to the end of the pass
+            wp.parity = p;
+            hipEvent_t i0, i1;
+            HIP_TRY(hipEventCreate(&i0));
+            HIP_TRY(hipEventCreate(&i1));
+            ss->pending_isect.emplace_back(i0, i1);
+            ss->isect_launches++;
+            const uint32_t grid = std::max(1u, std::min(ss->coop_grid, (chains + QC_WAVES - 1u) / QC_WAVES));
+            HIP_TRY(pt_launch_coop(wp, grid, ss->stream, i0, i1));
+            ss->rounds++;
+            p ^= 1u;
+            HIP_TRY(hipMemcpyAsync(ss->ctl_host, ss->ctl + PT_CTL_SET * p, 8, hipMemcpyDeviceToHost, ss->stream));
+            if (wp.progress) {
+                hipError_t e;
+                while ((e = hipStreamQuery(ss->stream)) == hipErrorNotReady) {
+                    ss->on_progress(__atomic_load_n(ss->prog_host, __ATOMIC_RELAXED));
+                    std::this_thread::sleep_for(std::chrono::microseconds(500));
+                }
+                HIP_TRY(e);
+            }
+            HIP_TRY(hipStreamSynchronize(ss->stream));
+            if (ss->ctl_host[pt::C_FRESH] != 0u || ss->ctl_host[pt::C_CARRY] != 0u)
+                return fail(PT_E_HIP, "cooperative engine left chains behind");
+            break;
+        }
         for (uint32_t r = 0; r < batch; ++r) {
             wp.parity = p;
             const std::string wgps = tune_str("wgprof");
@@ -901,8 +948,10 @@ int trace_wave(pt_session* ss, uint32_t spp) {
         }
         if (ss->ctl_host[pt::C_FRESH] == 0u && ss->ctl_host[pt::C_CARRY] == 0u) break;
         if (guard > 100000u) return fail(PT_E_HIP, "wavefront rounds did not drain");
-        batch = ss->ctl_host[pt::C_FRESH] + ss->ctl_host[pt::C_CARRY] > 4096u ? 4u : 2u;
-        sparse = ss->ctl_host[pt::C_FRESH] + ss->ctl_host[pt::C_CARRY] < ss->path_sparse;
+        chains = ss->ctl_host[pt::C_FRESH] + ss->ctl_host[pt::C_CARRY];
+        // near the cooperative hand-over every round is counted (the tail's rounds take ms)
+        batch = chains > 4096u && chains > 4u * ss->coop_max ? 4u : (chains > 4096u ? 1u : 2u);
+        sparse = chains < ss->path_sparse;
     }
     HIP_TRY(hipEventRecord(e1, ss->stream));
     ss->pending.emplace_back(e0, e1);
@@ -1359,6 +1408,7 @@ int pt_selftest_ray_intersection(pt_scene* s, int32_t traversal, uint32_t n, con
     const pt::ReplayCfg cfg = replay_cfg(s);
     HostStack stk;
     pt::Counts C{};
+    const bool coop = tune_str("qengine") == "coop";   // the cooperative engine's query (pt_coop.h)
     for (uint32_t i = 0; i < n; ++i) {
         pt::Ray r;
         r.o = pt::mk3(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
@@ -1368,7 +1418,7 @@ int pt_selftest_ray_intersection(pt_scene* s, int32_t traversal, uint32_t n, con
         if (traversal == PT_TRAVERSAL_REPLAY) {
             pt::QCounts Q{0u, 0u, 0u, 0u};
             uint32_t ex = 0;
-            id = pt::q_run(V, r, stk, h, Q, ex);
+            id = coop ? pt::qc_query(V, r, stk, h, Q, ex) : pt::q_run(V, r, stk, h, Q, ex);
             if (Q.planes & 0x80000000u) return fail(PT_E_INVALID, "recomputed closest hit differs from the query's");
             C.rays++;
             C.nodes += Q.nodes; C.ptests += Q.ptests; C.planes += Q.planes; C.aux += Q.aux; C.fallbacks += ex;
@@ -1405,6 +1455,7 @@ int pt_selftest_render_host(pt_scene* s, int32_t traversal, uint32_t x0, uint32_
     const std::string qpaths = tune_str("qstats");
     const char* qpath = qpaths.empty() ? nullptr : qpaths.c_str();
     std::vector<std::vector<std::array<uint32_t, 4>>> qlogs(nt);
+    const bool coop = tune_str("qengine") == "coop";   // the cooperative engine's query (pt_coop.h)
     for (uint32_t t = 0; t < nt; ++t) {
         th.emplace_back([&, t]() {
             std::vector<std::array<uint32_t, 4>>* qlog = qpath ? &qlogs[t] : nullptr;
@@ -1424,7 +1475,7 @@ int pt_selftest_render_host(pt_scene* s, int32_t traversal, uint32_t x0, uint32_
                         auto q = [&](const pt::Ray& rr, pt::Hit& hh, pt::Counts& cc) {
                             pt::QCounts Q{};
                             uint32_t ex = 0;
-                            const int id = pt::q_run(V, rr, stk, hh, Q, ex);
+                            const int id = coop ? pt::qc_query(V, rr, stk, hh, Q, ex) : pt::q_run(V, rr, stk, hh, Q, ex);
                             cc.fallbacks += ex;
                             if (Q.planes & 0x80000000u) cc.errs |= 4u;   // recomputed hit differs (checked below)
 #ifdef PT_QDIAG

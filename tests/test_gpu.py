@@ -26,6 +26,8 @@ TRAVERSALS = {"replay": 0, "exact": 1, "replay_div": 2}
 @pytest.mark.parametrize("trav", sorted(TRAVERSALS))
 @pytest.mark.parametrize("name", sorted(M["images"]))
 def test_golden_images_bit_exact(pt, name, trav):
+    # default engine choice: windows of at most 4,096 pixels run the cooperative
+    # engine (one wave per chain) from the start, larger ones the path engine first
     m, img, rad = U.golden_image(name)
     with pt.Scene.load(U.golden_scene_path(name)) as s:
         s.prepare()
@@ -151,7 +153,40 @@ def test_device_init(pt):
     assert pt._lib.pt_device_init(4096) == pt.PT_E_NO_GPU
 
 
-@pytest.mark.parametrize("engine", ["path", "path_dense"])
+@pytest.mark.parametrize("engine", ["coop", "path"])
+@pytest.mark.parametrize("name", sorted(M["images"]))
+def test_golden_images_each_engine(pt, name, engine, monkeypatch):
+    """The replay traversal with one engine for the whole pass: the cooperative
+    engine (one wave per chain: breadth-first aux expansion, all candidate leaves
+    at once, root paths as one round of loads; pt_coop.h) or the path engine alone
+    (coop=0).  Both must reproduce the reference's bytes and ray count."""
+    monkeypatch.setenv("PT_TUNE", "coop=%s" % ("100000000" if engine == "coop" else "0"))
+    m, img, rad = U.golden_image(name)
+    with pt.Scene.load(U.golden_scene_path(name)) as s:
+        s.prepare()
+        win = tuple(m["window"]) if m["window"] else None
+        rgb, r, st = s.render(radiance=True, window=win, traversal=0)
+    assert st["errors"] == 0
+    assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
+    assert np.array_equal(rgb, img)
+    if engine == "coop":
+        assert st["rounds"] == 1
+
+
+@pytest.mark.parametrize("cfg", ["c1", "c2"])
+def test_coop_engine_full_config_md5(pt, cfg, monkeypatch):
+    """Configs 1 and 2 entirely on the cooperative engine: reference md5 and ray count."""
+    monkeypatch.setenv("PT_TUNE", "coop=100000000")
+    full = M["full"][cfg]
+    with pt.Scene.load(U.scene_path(cfg)) as s:
+        rgb, _, st = s.render()
+        w, h = s.info["width"], s.info["height"]
+    ppm = b"P6\n%d %d\n255\n" % (w, h) + rgb.tobytes()
+    assert U.md5(ppm) == full["md5"]
+    assert st["rays"] == full["rays"] and st["rounds"] == 1
+
+
+@pytest.mark.parametrize("engine", ["path", "path_dense", "path_coop"])
 @pytest.mark.parametrize("budget", ["1", "3"])
 @pytest.mark.parametrize("name", ["c3s4_win_944_520_16x16", "c4glass_s4_win_900_560_16x16", "dragon_64x64x16",
                                   "hw3s4_48x48x8", "c2_win_240_200_24x24"])
@@ -161,15 +196,20 @@ def test_suspended_queries_resume_bit_exact(pt, name, budget, engine, monkeypatc
     queries then resume from the carry queue over many rounds, interleaving
     pixels' samples arbitrarily -- results must not change.  "path" lets the
     engine switch to its end-of-pass (sparse) kernel once few chains are left,
-    as it does by default; "path_dense" keeps the main kernel for every round."""
-    monkeypatch.setenv("PT_TUNE", "budget=%s,sparse=%s" % (budget, "0" if engine == "path_dense" else "100000000"))
+    as it does by default; "path_dense" keeps the main kernel for every round;
+    "path_coop" hands the suspended queries and queued rays to the cooperative
+    engine once fewer than a quarter of the pixels have chains left."""
     m, img, rad = U.golden_image(name)
+    npx = int(np.prod(img.shape[:2]))
+    coop = npx // 4 if engine == "path_coop" else 0
+    monkeypatch.setenv("PT_TUNE", "budget=%s,sparse=%s,coop=%d" % (
+        budget, "0" if engine == "path_dense" else "100000000", coop))
     with pt.Scene.load(U.golden_scene_path(name)) as s:
         s.prepare()
         win = tuple(m["window"]) if m["window"] else None
         rgb, r, st = s.render(radiance=True, window=win, traversal=0)
     assert st["errors"] == 0
-    assert st["rounds"] > 0
+    assert st["rounds"] > (1 if engine == "path_coop" else 0)
     assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
     assert np.array_equal(rgb, img)
 

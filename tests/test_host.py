@@ -162,6 +162,40 @@ def test_device_integrator_on_host_bit_exact(name, trav):
     assert np.array_equal(U.oracle_tonemap(got).reshape(img.shape), img)
 
 
+@pytest.mark.parametrize("name", sorted(M["trav"]))
+def test_coop_query_matches_reference_kat(name, monkeypatch):
+    """The cooperative engine's query algorithm (pt_coop.h qc_run: every candidate
+    leaf's bound-free result first, then only the hitting leaves' root paths with
+    the carried bounds), run on the host: the reference's closest hits, fewer node
+    records than the replay state machine."""
+    t = M["trav"][name]
+    rays, ((ids, f, inter), _) = U.read_trav(name)
+    with pt.Scene.load(U.scene_path(t["scene"])) as s:
+        s.prepare()
+        _, _, rctr = s.selftest_ray_intersection(rays, traversal=0)
+        monkeypatch.setenv("PT_TUNE", "qengine=coop")
+        gids, ghits, ctr = s.selftest_ray_intersection(rays, traversal=0)
+    assert np.array_equal(gids, ids)
+    hit = ids != -1
+    assert np.array_equal(ghits[hit, :4].view(np.uint32), f[hit].view(np.uint32))
+    assert np.array_equal(ghits[hit, 4].astype(np.uint32), inter[hit])
+    assert ctr["nodes"] < rctr["nodes"]
+
+
+@pytest.mark.parametrize("name", HOST_RENDER[:6])
+def test_coop_integrator_on_host_bit_exact(name, monkeypatch):
+    monkeypatch.setenv("PT_TUNE", "qengine=coop")
+    m, img, rad = U.golden_image(name)
+    with pt.Scene.load(U.golden_scene_path(name)) as s:
+        s.prepare()
+        if m["window"]:
+            x0, y0, w, h = m["window"]
+        else:
+            x0, y0, h, w = 0, 0, img.shape[0], img.shape[1]
+        got = s.selftest_render_host(x0, y0, w, h, traversal=0)
+    assert got.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
+
+
 def _gamma_table():
     with pt.Scene.load(U.scene_path("practice5_1.txt")) as s:
         s.prepare()
