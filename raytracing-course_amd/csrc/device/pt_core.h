@@ -476,22 +476,31 @@ PT_HD float pdf_ellipsoid(const Prim& E, f3 x, f3 d) {
     }
     return sum;
 }
+// The emitter records the mixture reads: EmitGlobal = the scene's arrays; the
+// cooperative engine passes a workgroup copy in LDS (same bits).
+struct EmitGlobal {
+    const SceneView& S;
+    PT_HD Prim operator()(uint32_t k) const { return S.prims[S.emitters[k]]; }
+};
 // src/distributions.cpp:385-399
-PT_HD f3 sample_mix(const SceneView& S, Rng& R, f3 x, f3 n) {
+template <class EM>
+PT_HD f3 sample_mix_e(const SceneView& S, const EM& em, Rng& R, f3 x, f3 n) {
     const float flip = rng_uniform(R);
     if (S.n_emitters == 0u || flip <= 0.5f) return sample_cosine(R, n);
     const float fid = rng_uniform(R);
     const uint32_t id = (uint32_t)floorf(fid * (float)S.n_emitters);
-    const Prim E = S.prims[S.emitters[id]];
+    const Prim E = em(id);
     return f2u(E.p0.w) == T_BOX ? sample_box(R, E, x) : sample_ellipsoid(R, E, x);
 }
+PT_HD f3 sample_mix(const SceneView& S, Rng& R, f3 x, f3 n) { return sample_mix_e(S, EmitGlobal{S}, R, x, n); }
 // src/distributions.cpp:401-416
-PT_HD float pdf_mix(const SceneView& S, f3 x, f3 n, f3 d) {
+template <class EM>
+PT_HD float pdf_mix_e(const SceneView& S, const EM& em, f3 x, f3 n, f3 d) {
     float sum = pdf_cosine(n, d);
     if (S.n_emitters != 0u) {
         float ps = 0.f;
         for (uint32_t k = 0; k < S.n_emitters; ++k) {
-            const Prim E = S.prims[S.emitters[k]];
+            const Prim E = em(k);
             ps += f2u(E.p0.w) == T_BOX ? pdf_box(E, x, d) : pdf_ellipsoid(E, x, d);
         }
         ps *= 1.f / (float)S.n_emitters;
@@ -499,6 +508,7 @@ PT_HD float pdf_mix(const SceneView& S, f3 x, f3 n, f3 d) {
     }
     return sum;
 }
+PT_HD float pdf_mix(const SceneView& S, f3 x, f3 n, f3 d) { return pdf_mix_e(S, EmitGlobal{S}, x, n, d); }
 
 // src/scene.cpp:79-81
 PT_HD f3 reflect(f3 n, f3 dir) { return dir - (2.0f * n) * dot(n, dir); }

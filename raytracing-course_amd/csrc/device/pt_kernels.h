@@ -104,7 +104,7 @@ struct WaveParams {
     const uint32_t* tile_order;   // k_wcamera: block b seeds local tile tile_order[b] (null: tile b)
     uint32_t sparse_steps;        // steps per loop trip of the end-of-pass (sparse) kernel
     F4* ring;                     // per-workgroup ray/done rings, PT_RING_F4 F4 per workgroup
-    uint32_t coop_slim;           // k_wcoop: aux stack size above which a wave expands fewer nodes per round
+    uint32_t coop_reserve;        // k_wcoop: aux stack words kept free for a depth-first descent (4 (aux depth + 2))
 };
 
 // path engine geometry: PT_NQ query waves + 1 shade wave per workgroup; at most
@@ -124,9 +124,11 @@ struct WaveParams {
 #ifndef QC_WAVES
 #define QC_WAVES 4u
 #endif
-#define QC_SCAP 448u               // aux node stack words per wave (also lane 0's exact DFS stack)
-#define QC_CCAP 320u               // candidate leaves per wave (< 64 + 4 x 64 at any time)
-#define QC_HCAP 64u                // hitting leaves per query (more: the exact DFS)
+#define QC_SCAP_MIN 128u           // aux stack words per team (the smallest; also the exact DFS stack)
+#define QC_FOLD 8u                 // fold records held in LDS per chain (RAY_DEPTH <= QC_FOLD, host-checked)
+#define QC_NPL 8u                  // plane records copied to LDS per workgroup (n_planes <= QC_NPL, host-checked)
+#define QC_NEM 8u                  // emitter records copied to LDS per workgroup (n_emitters <= QC_NEM)
+#define QC_TOPN 21u                // aux BVH nodes 0..20 (BFS order: the top three levels) copied to LDS
 
 struct ResolveParams {
     PixelState st;
@@ -151,6 +153,7 @@ hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s);
 hipError_t pt_launch_path_round(pt::WaveParams p, uint32_t path_grid, uint32_t shade_grid, hipStream_t s, bool sparse,
                                 hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 // cooperative engine: one launch runs every remaining chain of the pass to its end
-hipError_t pt_launch_coop(pt::WaveParams p, uint32_t grid, hipStream_t s, hipEvent_t e0 = nullptr,
+// team = lanes per chain (16, 32 or 64)
+hipError_t pt_launch_coop(pt::WaveParams p, uint32_t grid, uint32_t team, hipStream_t s, hipEvent_t e0 = nullptr,
                           hipEvent_t e1 = nullptr);
 hipError_t pt_launch_resolve(const pt::ResolveParams& p, uint32_t n_tiles, hipStream_t s);

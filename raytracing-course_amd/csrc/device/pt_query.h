@@ -133,12 +133,18 @@ struct QCounts {
 // the planes part of RayIntersection (src/scene.cpp:50-57): closest plane t and
 // its prim (-1 none).  Run by the ray's producer (camera / shade kernels), so
 // the query kernel starts at the BVH.
-PT_HD void q_planes(const SceneView& S, const Ray& ray, float& P, int& pid) {
+// `pl(k, pi)` = the k-th plane's record and prim index (PlanesGlobal, or a copy)
+struct PlanesGlobal {
+    const SceneView& S;
+    PT_HD Prim operator()(uint32_t k, uint32_t& pi) const { pi = S.planes[k]; return S.prims[pi]; }
+};
+template <class PL>
+PT_HD void q_planes_e(const SceneView& S, const PL& pl, const Ray& ray, float& P, int& pid) {
     P = PT_INF;
     pid = -1;
     for (uint32_t k = 0; k < S.n_planes; ++k) {
-        const uint32_t pi = S.planes[k];
-        const Prim pr = S.prims[pi];
+        uint32_t pi;
+        const Prim pr = pl(k, pi);
         Hit h;
         bool ok;
         if (f2u(pr.p1.x) == 0u && f2u(pr.p1.y) == 0u && f2u(pr.p1.z) == 0u && f2u(pr.p1.w) == 0x3f800000u) {
@@ -156,6 +162,7 @@ PT_HD void q_planes(const SceneView& S, const Ray& ray, float& P, int& pid) {
         if (ok && h.t < P) { P = h.t; pid = (int)pi; }
     }
 }
+PT_HD void q_planes(const SceneView& S, const Ray& ray, float& P, int& pid) { q_planes_e(S, PlanesGlobal{S}, ray, P, pid); }
 
 // Per-ray set-up a query needs, computed once by the ray's producer (so the
 // IEEE divisions run on the producer's full wave, not on the few lanes a query

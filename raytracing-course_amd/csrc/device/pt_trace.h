@@ -497,19 +497,20 @@ enum : uint32_t { V_TERM = 0u, V_DIFFUSE = 1u, V_COL = 2u, V_IDENT = 3u };
 // (idm = prim id | mode << 30, factors s1, s2) and whether the path continues
 // with `ray` set to the child ray.  Shared by the megakernel integrator and
 // the wavefront shade kernel.
-PT_HD bool shade_vertex(const SceneView& S, Rng& R, Ray& ray, const Hit& h, int id, uint32_t& idm, float& s1,
-                        float& s2) {
+// `em` = the emitter records (EmitGlobal or a copy), `sh` = the prim's shading record.
+template <class EM>
+PT_HD bool shade_vertex_e(const SceneView& S, const EM& em, const Shade& sh, Rng& R, Ray& ray, const Hit& h, int id,
+                          uint32_t& idm, float& s1, float& s2) {
     const float eps = 1e-4f;  // Scene::eps, include/scene.h:56
-    const Shade sh = S.shade[id];
     const uint32_t mat = f2u(sh.s1.w);
     const f3 p = ray.o + h.t * ray.d;
     const f3 n = h.n;
     if (mat == M_DIFFUSE) {
         const f3 p_outer = p + eps * n;
-        const f3 dir = sample_mix(S, R, p_outer, n);
+        const f3 dir = sample_mix_e(S, em, R, p_outer, n);
         const float cosv = dot(dir, n);
         if (cosv <= 0.f) { idm = (uint32_t)id | (V_TERM << 30); s1 = s2 = 0.f; return false; }
-        const float pw = pdf_mix(S, p_outer, n, dir);
+        const float pw = pdf_mix_e(S, em, p_outer, n, dir);
         idm = (uint32_t)id | (V_DIFFUSE << 30);
         s1 = cosv;
         s2 = 1.f / pw;
@@ -560,11 +561,14 @@ PT_HD bool shade_vertex(const SceneView& S, Rng& R, Ray& ray, const Hit& h, int 
     s1 = s2 = 0.f;
     return false;
 }
+PT_HD bool shade_vertex(const SceneView& S, Rng& R, Ray& ray, const Hit& h, int id, uint32_t& idm, float& s1,
+                        float& s2) {
+    return shade_vertex_e(S, EmitGlobal{S}, S.shade[id], R, ray, h, id, idm, s1, s2);
+}
 
-// backward fold of one vertex record: L = E_k + ((A_k * L) * s1_k) * s2_k
-PT_HD f3 fold_vertex(const SceneView& S, f3 L, uint32_t idm, float s1, float s2) {
-    const uint32_t id = idm & 0x3fffffffu, mode = idm >> 30;
-    const Shade sh = S.shade[id];
+// backward fold of one vertex record with its shading record: L = E_k + ((A_k * L) * s1_k) * s2_k
+PT_HD f3 fold_vertex_sh(const Shade& sh, f3 L, uint32_t idm, float s1, float s2) {
+    const uint32_t mode = idm >> 30;
     const f3 E = mk3(sh.s1.x, sh.s1.y, sh.s1.z);
     f3 other;
     if (mode == V_TERM) {
@@ -578,6 +582,9 @@ PT_HD f3 fold_vertex(const SceneView& S, f3 L, uint32_t idm, float s1, float s2)
         other = ((A * L) * s1) * s2;
     }
     return E + other;
+}
+PT_HD f3 fold_vertex(const SceneView& S, f3 L, uint32_t idm, float s1, float s2) {
+    return fold_vertex_sh(S.shade[idm & 0x3fffffffu], L, idm, s1, s2);
 }
 
 // One camera sample: src/scene.cpp:189-203 (inner) + RayTrace :83-178.

@@ -800,82 +800,159 @@ __global__ void __launch_bounds__(PT_PATH_WG) __attribute__((amdgpu_waves_per_eu
 }
 
 // ---- cooperative engine (end of a pass) ---------------------------------------
-// k_wcoop: ONE wave per pixel chain, run to the end of the pass.  With few chains
-// left, the path engine's lanes idle while every chain waits on its own long
-// sequence of dependent steps and ring hand-offs; here a chain's query is spread
-// over the wave's lanes (pt_coop.h: breadth-first aux expansion, every candidate
-// leaf and its primitives at once, a root path as one round of loads) and the
-// wave shades the result itself, so nothing waits in a ring.
-struct QcLds {
-    uint32_t stk[QC_SCAP];         // pending aux nodes (also the exact DFS stack of lane 0)
-    uint32_t cand[QC_CCAP];        // candidate leaves; after the expansion the sorted hitting leaves
-    uint32_t h_idx[QC_HCAP], h_t[QC_HCAP], h_lid[QC_HCAP];   // hitting leaves (unsorted)
-    uint32_t r_idx[QC_HCAP], r_t[QC_HCAP];                   // entered hits so far (preorder)
+// k_wcoop<T>: a TEAM of T lanes per pixel chain (64/T chains per wave), run to the
+// end of the pass.  With few chains left, the path engine's lanes idle while every
+// chain waits on its own long sequence of dependent steps and ring hand-offs; here
+// a chain's query is spread over its team's lanes (pt_coop.h: breadth-first aux
+// expansion, every candidate leaf and its primitives at once, root paths a block
+// of nodes per round) and the team's first lane shades the result itself, with
+// the pixel's state in registers and its fold records in LDS for the chain's
+// whole life, so nothing waits in a ring.  The teams of a wave run their chain
+// cycles in step (query, then shading), so one instruction stream shades 64/T
+// chains.
+enum : uint32_t { QH_IDX = 0u, QH_T, QH_LID, QH_NX, QH_NY, QH_NZ, QH_IN, QH_INFO, QH_N };
+template <uint32_t T>
+struct QcTeamLds {
+    static constexpr uint32_t SCAP = T == 64u ? 448u : T == 32u ? 192u : QC_SCAP_MIN;   // aux stack (also the
+                                                                                      // leader's exact DFS stack)
+    static constexpr uint32_t CCAP = 5u * T;                    // candidates (< T + 4 T at any time)
+    static constexpr uint32_t HCAP = T == 64u ? 32u : T;        // hitting leaves per query (more: exact DFS)
+    uint32_t stk[SCAP];
+    uint32_t cand[CCAP];
+    uint32_t hl[QH_N][HCAP];       // hitting leaves: index, first-min t, its prim, hit normal and side,
+                                   // ancestor-list info (sorted into preorder in place)
+    uint32_t r_idx[HCAP], r_t[HCAP];   // entered hits so far (preorder)
+    Shade fold_sh[QC_FOLD];        // the chain's fold records: the vertex prim's shading record ...
+    uint4 fold[QC_FOLD];           // ... and {idm, s1, s2, -}
+};
+// per workgroup: the records every chain cycle reads, copied once per launch
+struct QcScene {
+    Prim pl[QC_NPL];               // planes (q_planes order) and their prim indices
+    Prim em[QC_NEM];               // emitters
+    AuxSL top[QC_TOPN * PT_AUXW];  // aux nodes 0..QC_TOPN-1
+    uint32_t pl_id[QC_NPL];
+};
+struct PlanesLds {
+    const QcScene& Q;
+    __device__ Prim operator()(uint32_t k, uint32_t& pi) const { pi = Q.pl_id[k]; return Q.pl[k]; }
+};
+struct EmitLds {
+    const QcScene& Q;
+    __device__ Prim operator()(uint32_t k) const { return Q.em[k]; }
 };
 
-// The query of one ray by the whole wave (every argument wave-uniform).
-// `slim` = stack size above which the expansion takes fewer nodes per round
-// (host: QC_SCAP - 4 (aux depth + 2), so a depth-first descent still fits).
-// Returns the closest prim (-1 none); `exact` set = hand the ray to the exact DFS.
-__device__ int qc_wave(const SceneView& S, QcLds& L, const Ray& ray, float P, int pid, F4 pre, uint32_t slim,
-                       QCounts& C, bool& exact) {
-    const uint32_t lane = lane_id();
-    exact = pre.w != pre.w;
-    if (exact) return -1;
+#ifdef PT_CPROF
+// diagnostics build: per-phase shader cycles of the cooperative engine (summed per wave)
+#define QC_T0() uint64_t qc_t = __builtin_amdgcn_s_memtime()
+#define QC_TICK(i) do { const uint64_t n_ = __builtin_amdgcn_s_memtime(); cp[i] += n_ - qc_t; qc_t = n_; } while (0)
+#define QC_CP_ARG , uint64_t* cp
+#define QC_CP_PASS , cp
+#else
+#define QC_T0() (void)0
+#define QC_TICK(i) (void)0
+#define QC_CP_ARG
+#define QC_CP_PASS
+#endif
+
+// The query of one ray per team (every argument team-uniform; `on` = this team has
+// a query).  `reserve` = 4 (aux depth + 2): above SCAP - reserve pending nodes the
+// expansion takes fewer nodes per round, so a depth-first descent still fits.
+// Returns the closest prim (-1 none) and, for a BVH result, `hit` = its intersection
+// (t, n, side, from the same bvh_prim_intersect the consumer would repeat); `bvh`
+// tells which.  `exact` set = hand the ray to the exact DFS.
+template <uint32_t T>
+__device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bool on, const Ray& ray, float P,
+                       int pid, F4 pre, uint32_t reserve, QCounts& C, bool& exact, Hit& hit, bool& bvh QC_CP_ARG) {
+    QC_T0();
+    constexpr uint32_t SCAP = QcTeamLds<T>::SCAP, HCAP = QcTeamLds<T>::HCAP;
+    static_assert(HCAP <= T, "one hitting leaf per team lane when sorting");
+    const uint32_t lane = lane_id(), tl = lane % T, tbase = lane - tl;
+    const unsigned long long tmask = T == 64u ? ~0ull : (((1ull << T) - 1ull) << tbase);
+    const uint32_t slim = SCAP - reserve;
+    bvh = false;
+    exact = on && pre.w != pre.w;
+    const bool run = on && !exact;
     const bool par = signbit(pre.w);
     const f3 inv = mk3(pre.x, pre.y, pre.z);
     const f3 oinv = mk3(ray.o.x * inv.x, ray.o.y * inv.y, ray.o.z * inv.z);
-    uint32_t ns = 1u, nc = 0u, nh = 0u;
+    uint32_t ns = run ? 1u : 0u, nc = 0u, nh = 0u;
     bool ovf = false;
-    if (lane == 0u) L.stk[0] = 0u;
+    if (tl == 0u && run) L.stk[0] = 0u;
     for (;;) {
-        // 2. candidate leaves, 64 at a time (the rest once the expansion is over):
-        //    bound-free slab test, then the first strict minimum over the primitives
-        while (nc >= 64u || (ns == 0u && nc > 0u)) {
-            const uint32_t take = nc < 64u ? nc : 64u;
+        // 2. candidate leaves, T at a time (the rest once the expansion is over):
+        //    bound-free slab test, then the first strict minimum over the primitives;
+        //    the leaf's ancestor-list info is fetched alongside its record
+        for (;;) {
+            const bool want = run && !ovf && (nc >= T || (ns == 0u && nc > 0u));
+            if (__ballot(want) == 0ull) break;
+            QC_TICK(0);
+            const uint32_t take = want ? (nc < T ? nc : T) : 0u;
             nc -= take;
-            const bool act = lane < take;
-            const uint32_t c = act ? L.cand[nc + lane] : 0u;
+            const bool act = tl < take;
+            const uint32_t c = act ? L.cand[nc + tl] : 0u;
             const Node nd = S.nodes[c];
+            const uint32_t ainfo = S.anc_info[c];
             C.nodes += act ? 1u : 0u;
             const bool hb = act && qc_slab_hit(nd, ray, inv, par);
             const uint32_t ref = f2u(nd.b.z), cnt = hb ? f2u(nd.b.w) : 0u;
-            float lt = PT_INF;
+            Hit best;
+            best.t = PT_INF;
+            best.n = mk3(0.f, 0.f, 0.f);
+            best.interior = 0u;
             int lid = -1;
             for (uint32_t i = 0; __ballot(i < cnt) != 0ull; ++i) {
                 if (i < cnt) {
                     Hit hh;
                     C.ptests++;
-                    if (bvh_prim_intersect(S.prims[ref + i], ray, hh) && hh.t < lt) { lt = hh.t; lid = (int)(ref + i); }
+                    if (bvh_prim_intersect(S.prims[ref + i], ray, hh) && hh.t < best.t) { best = hh; lid = (int)(ref + i); }
                 }
             }
-            const unsigned long long m = __ballot(lid >= 0);
+            const unsigned long long m = __ballot(lid >= 0) & tmask;
             const uint32_t nm = (uint32_t)__popcll(m);
-            if (nh + nm > QC_HCAP) {
-                ovf = true;
-            } else if (lid >= 0) {
-                const uint32_t j = nh + lanes_below(m);
-                L.h_idx[j] = c;
-                L.h_t[j] = f2u(lt);
-                L.h_lid[j] = (uint32_t)lid;
+            if (want) {
+                if (nh + nm > HCAP) {
+                    ovf = true;
+                } else if (lid >= 0) {
+                    const uint32_t j = nh + lanes_below(m);
+                    L.hl[QH_IDX][j] = c;
+                    L.hl[QH_T][j] = f2u(best.t);
+                    L.hl[QH_LID][j] = (uint32_t)lid;
+                    L.hl[QH_NX][j] = f2u(best.n.x);
+                    L.hl[QH_NY][j] = f2u(best.n.y);
+                    L.hl[QH_NZ][j] = f2u(best.n.z);
+                    L.hl[QH_IN][j] = best.interior;
+                    L.hl[QH_INFO][j] = ainfo;
+                }
+                nh += nm;
             }
-            nh += nm;
+            QC_TICK(1);
         }
-        if (ns == 0u || ovf) break;
-        // 1. breadth-first expansion of the wide aux BVH: one node per lane
+        // 1. breadth-first expansion of the wide aux BVH: one node per team lane
+        const bool expand = run && !ovf && ns > 0u;
+        if (__ballot(expand) == 0ull) break;
         uint32_t k = slim > ns ? (slim - ns) / 3u : 0u;
         k = k < 1u ? 1u : k;
-        k = k > 64u ? 64u : k;
+        k = k > T ? T : k;
         k = k > ns ? ns : k;
-        if (ns + 3u * k > QC_SCAP) { ovf = true; break; }   // cannot happen with the host's slim (checked)
+        if (!expand) k = 0u;
+        if (ns + 3u * k > SCAP) { ovf = true; k = 0u; }   // cannot happen with the host's reserve (checked)
         ns -= k;
-        const bool act = lane < k;
-        const uint32_t node = act ? L.stk[ns + lane] : 0u;
+        const bool act = tl < k;
+        const uint32_t node = act ? L.stk[ns + tl] : 0u;
         C.aux += act ? 1u : 0u;
-        const uint32_t b = S.o_aux + node * (uint32_t)(PT_AUXW * sizeof(AuxSL));
         F4 r[2 * PT_AUXW];
+        if (node < QC_TOPN) {
+            // the top levels: the workgroup's LDS copy
 #pragma unroll
-        for (uint32_t e = 0; e < 2u * PT_AUXW; ++e) r[e] = blob_piece(S, b + 16u * e);
+            for (uint32_t e = 0; e < PT_AUXW; ++e) {
+                r[2 * e] = Q.top[node * PT_AUXW + e].a;
+                r[2 * e + 1] = Q.top[node * PT_AUXW + e].b;
+            }
+        } else {
+            const uint32_t b = S.o_aux + node * (uint32_t)(PT_AUXW * sizeof(AuxSL));
+#pragma unroll
+            for (uint32_t e = 0; e < 2u * PT_AUXW; ++e) r[e] = blob_piece(S, b + 16u * e);
+        }
 #pragma unroll
         for (uint32_t e = 0; e < PT_AUXW; ++e) {
             const F4 ea = r[2 * e], eb = r[2 * e + 1];
@@ -885,154 +962,333 @@ __device__ int qc_wave(const SceneView& S, QcLds& L, const Ray& ray, float P, in
                            : aux_box(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, inv, oinv);
             const bool leaf = h && (code & 0x80000000u) != 0u;
             const bool inner = h && (code & 0x80000000u) == 0u;
-            const unsigned long long mi = __ballot(inner), ml = __ballot(leaf);
+            const unsigned long long mi = __ballot(inner) & tmask, ml = __ballot(leaf) & tmask;
             if (inner) L.stk[ns + lanes_below(mi)] = code;
             if (leaf) L.cand[nc + lanes_below(ml)] = code & 0x7fffffffu;
             ns += (uint32_t)__popcll(mi);
             nc += (uint32_t)__popcll(ml);
         }
     }
-    if (ovf) {
-        exact = true;
-        return -1;
-    }
-    // 3. the hitting leaves in reference preorder (distinct indices: rank = count below)
-    if (nh > 1u) {
-        const bool act = lane < nh;
-        const uint32_t c = act ? L.h_idx[lane] : 0u, t = act ? L.h_t[lane] : 0u, id = act ? L.h_lid[lane] : 0u;
-        uint32_t rank = 0u;
-        for (uint32_t j = 0; j < nh; ++j) rank += L.h_idx[j] < c ? 1u : 0u;
-        if (act) {
-            L.cand[rank] = c;
-            L.cand[64u + rank] = t;
-            L.cand[128u + rank] = id;
-        }
-    } else if (nh == 1u && lane == 0u) {
-        L.cand[0] = L.h_idx[0];
-        L.cand[64] = L.h_t[0];
-        L.cand[128] = L.h_lid[0];
-    }
-    uint32_t nrec = 0u;
-    float bt = PT_INF;
-    int res = pid;
-    for (uint32_t k = 0; k < nh; ++k) {
-        const uint32_t c = L.cand[k];
-        const float lt = u2f(L.cand[64u + k]);
-        const uint32_t info = S.anc_info[c];
-        const uint32_t off = info & 0x03ffffffu, len = info >> 26;
-        const bool on = lane < len;
-        const uint32_t v = on ? S.anc[off + lane] : 0u;
-        const uint32_t prev = __shfl(v, (int)(lane == 0u ? 0u : lane - 1u), 64);
-        const Node nd = S.nodes[v];
-        C.nodes += on ? 1u : 0u;
-        // the carried bound: at a right child the minimum over the entered hits of its
-        // left sibling's subtree (prev, v), if any; else the parent's (scan down the path)
-        const bool rc = on && lane > 0u && v != prev + 1u;
-        float m = 0.f;
-        bool any = false;
-        for (uint32_t q = 0; q < nrec; ++q) {
-            const uint32_t ri = L.r_idx[q];
-            const float rt = u2f(L.r_t[q]);
-            if (rc && ri > prev && ri < v) {
-                if (!any || rt < m) m = rt;
-                any = true;
+    QC_TICK(0);
+    if (ovf) exact = true;
+    const bool dec = run && !ovf;
+    // 3. the hitting leaves in reference preorder (distinct indices: rank = count below),
+    //    sorted in place (every lane reads its entry before any lane writes)
+    {
+        const bool srt = dec && nh > 1u;
+        if (__ballot(srt) != 0ull) {
+            const bool act = srt && tl < nh;
+            uint32_t e[QH_N];
+#pragma unroll
+            for (uint32_t f = 0; f < QH_N; ++f) e[f] = act ? L.hl[f][tl] : 0u;
+            uint32_t rank = 0u;
+            for (uint32_t j = 0; __ballot(srt && j < nh) != 0ull; ++j)
+                if (srt && j < nh) rank += L.hl[QH_IDX][j] < e[QH_IDX] ? 1u : 0u;
+            if (act) {
+#pragma unroll
+                for (uint32_t f = 0; f < QH_N; ++f) L.hl[f][rank] = e[f];
             }
         }
-        const unsigned long long dm = __ballot(any);
-        const unsigned long long below = dm & ((2ull << lane) - 1ull);
-        const int src = below ? 63 - __clzll((long long)below) : (int)lane;
-        const float mb = __shfl(m, src, 64);
-        const float bound = below ? mb : P;
-        const bool ok = !on || node_enter(nd, ray, inv, bound, par);
-        if (__ballot(!ok) == 0ull) {
-            // 4. entered: record; first strict minimum; replaces the plane iff closer
-            if (lane == 0u) {
-                L.r_idx[nrec] = c;
+    }
+    // 4. decide them in order: lane j of the team holds nodes j, j + T, ... of the
+    //    leaf's root path with their exact slab results (the reference's division form)
+    constexpr uint32_t NB = 64u / T;            // path blocks (a root path has at most 63 nodes)
+    constexpr uint32_t NG = NB < 4u ? NB : 4u;  // blocks loaded together
+    uint32_t nrec = 0u;
+    float bt = PT_INF;
+    int res = pid, resk = -1;
+    for (uint32_t kk = 0;; ++kk) {
+        const bool dk = dec && kk < nh;
+        if (__ballot(dk) == 0ull) break;
+        const uint32_t info = dk ? L.hl[QH_INFO][kk] : 0u;
+        const uint32_t off = info & 0x03ffffffu, len = dk ? info >> 26 : 0u;
+        float carry = P;          // the bound at the previous block's last node
+        uint32_t vlast = 0u;      // that node
+        bool fail = false;
+        for (uint32_t g = 0; g < NB; g += NG) {
+            if (__ballot(g * T < len) == 0ull) break;
+            uint32_t v[NG], hf[NG];
+            float tq[NG];
+#pragma unroll
+            for (uint32_t b = 0; b < NG; ++b) {
+                const uint32_t j = (g + b) * T + tl;
+                v[b] = j < len ? S.anc[off + j] : 0u;
+            }
+#pragma unroll
+            for (uint32_t b = 0; b < NG; ++b) {
+                const bool pon = (g + b) * T + tl < len;
+                const Node nd = S.nodes[v[b]];
+                float t = 0.f;
+                uint32_t in = 0u;
+                const bool hs = pon && node_slab(nd, ray, t, in);
+                tq[b] = t;
+                hf[b] = (hs ? 1u : 0u) | (in << 1);
+                C.nodes += pon ? 1u : 0u;
+            }
+#pragma unroll
+            for (uint32_t b = 0; b < NG; ++b) {
+                if (__ballot((g + b) * T < len) == 0ull) break;
+                const uint32_t j = (g + b) * T + tl;
+                const bool pon = j < len;
+                const uint32_t up = __shfl(v[b], (int)(lane == 0u ? 0u : lane - 1u), 64);
+                const uint32_t prev = tl == 0u ? vlast : up;
+                // the carried bound: at a right child the minimum over the entered hits of its
+                // left sibling's subtree (prev, v), if any; else the parent's (scan down the path)
+                const bool rc = pon && j > 0u && v[b] != prev + 1u;
+                float m = 0.f;
+                bool any = false;
+                for (uint32_t r = 0; __ballot(r < nrec) != 0ull; ++r) {
+                    if (r < nrec) {
+                        const uint32_t ri = L.r_idx[r];
+                        const float rt = u2f(L.r_t[r]);
+                        if (rc && ri > prev && ri < v[b]) {
+                            if (!any || rt < m) m = rt;
+                            any = true;
+                        }
+                    }
+                }
+                const unsigned long long dm = __ballot(any) & tmask;
+                const unsigned long long below = dm & ((2ull << lane) - 1ull);
+                const int src = below ? 63 - __clzll((long long)below) : (int)lane;
+                const float mb = __shfl(m, src, 64);
+                const float bound = below ? mb : carry;
+                // src/bvh.cpp:188-198: slab miss, or pruned by the bound (not interior)
+                const bool ok = !pon || ((hf[b] & 1u) && !(bound < tq[b] && !(hf[b] & 2u)));
+                fail = fail || (__ballot(!ok) & tmask) != 0ull;
+                carry = __shfl(bound, (int)(tbase + T - 1u), 64);
+                vlast = __shfl(v[b], (int)(tbase + T - 1u), 64);
+            }
+        }
+        if (dk && !fail) {
+            // 5. entered: record; first strict minimum; replaces the plane iff closer
+            const float lt = u2f(L.hl[QH_T][kk]);
+            if (tl == 0u) {
+                L.r_idx[nrec] = L.hl[QH_IDX][kk];
                 L.r_t[nrec] = f2u(lt);
             }
             ++nrec;
             if (lt < bt) {
                 bt = lt;
-                if (lt < P) res = (int)L.cand[128u + k];
+                if (lt < P) {
+                    res = (int)L.hl[QH_LID][kk];
+                    resk = (int)kk;
+                }
             }
         }
     }
-    return res;
+    QC_TICK(2);
+    if (resk >= 0) {
+        bvh = true;
+        hit.t = u2f(L.hl[QH_T][resk]);
+        hit.n = mk3(u2f(L.hl[QH_NX][resk]), u2f(L.hl[QH_NY][resk]), u2f(L.hl[QH_NZ][resk]));
+        hit.interior = L.hl[QH_IN][resk];
+    }
+    return on ? res : -1;
 }
 
-__device__ __forceinline__ float bcast_f(float v) { return u2f(__builtin_amdgcn_readfirstlane(f2u(v))); }
+// the chain's pixel state while a team owns it (its first lane's registers)
+struct CoopPixel {
+    Rng R;
+    uint32_t nv, done;
+    f3 sum;
+};
 
-__global__ void __launch_bounds__(64u * QC_WAVES) k_wcoop(WaveParams P) {
-    __shared__ QcLds Ls[QC_WAVES];
-    QcLds& L = Ls[threadIdx.x >> 6];
-    const uint32_t lane = lane_id();
+// shade_item for the cooperative engine (a team's first lane): the same vertex /
+// fold / next sample logic (src/scene.cpp:91-203), with the pixel state in
+// registers, the fold records in LDS and the hit handed over by the query
+template <class TL>
+__device__ __forceinline__ bool coop_shade(const WaveParams& P, const QcScene& Q, TL& L, CoopPixel& px,
+                                           uint32_t slot, Ray& ray, int id, const Hit& h, bool& sdone) {
+    bool emit = false;
+    uint32_t end = PE_LIVE;
+    if (id < 0) {
+        end = PE_MISS;
+    } else {
+        uint32_t idm;
+        float s1, s2;
+        const Shade sh = P.S.shade[id];
+        const bool cont = shade_vertex_e(P.S, EmitLds{Q}, sh, px.R, ray, h, id, idm, s1, s2);
+        L.fold_sh[px.nv] = sh;
+        L.fold[px.nv] = make_uint4(idm, f2u(s1), f2u(s2), 0u);
+        ++px.nv;
+        if (!cont) end = PE_TERM;
+        else if (px.nv >= P.depth) end = PE_CUT;   // RayTrace(.., 0) = 0
+        else emit = true;
+    }
+    sdone = end != PE_LIVE;
+    if (end != PE_LIVE) {
+        // path over: backward fold (deepest vertex first), src/scene.cpp:198 sum += ...
+        f3 Lr = end == PE_MISS ? P.S.bg : mk3(0.f, 0.f, 0.f);
+        for (uint32_t k = px.nv; k > 0u; --k) {
+            const uint4 f = L.fold[k - 1u];
+            Lr = fold_vertex_sh(L.fold_sh[k - 1u], Lr, f.x, u2f(f.y), u2f(f.z));
+        }
+        px.sum = px.sum + Lr;
+        px.done += 1u;
+        px.nv = 0u;
+        if (px.done < P.target) {
+            uint32_t x, y;
+            slot_xy(P.tm, slot, x, y);
+            ray = camera_sample(P.cam, px.R, x, y);
+            emit = true;
+        }
+    }
+    return emit;
+}
+
+#ifndef QC_WAVES_PER_EU
+#define QC_WAVES_PER_EU 3
+#endif
+template <uint32_t T>
+__global__ void __launch_bounds__(64u * QC_WAVES) __attribute__((amdgpu_waves_per_eu(QC_WAVES_PER_EU, QC_WAVES_PER_EU)))
+k_wcoop(WaveParams P) {
+    __shared__ QcTeamLds<T> Ls[QC_WAVES * (64u / T)];
+    __shared__ QcScene Q;
+    const uint32_t lane = lane_id(), tl = lane % T, tbase = lane - tl;
+    QcTeamLds<T>& L = Ls[(threadIdx.x >> 6) * (64u / T) + lane / T];
+    {
+        // this launch's copies: planes, emitters, the aux BVH's top nodes (counts host-checked)
+        F4* q = reinterpret_cast<F4*>(&Q);
+        const uint32_t npl = P.S.n_planes * 5u, nem = P.S.n_emitters * 5u;
+        const uint32_t ntop = (P.n_aux < QC_TOPN * PT_AUXW ? P.n_aux : QC_TOPN * PT_AUXW) * 2u;
+        for (uint32_t i = threadIdx.x; i < npl; i += blockDim.x)
+            q[i] = reinterpret_cast<const F4*>(P.S.prims + P.S.planes[i / 5u])[i % 5u];
+        for (uint32_t i = threadIdx.x; i < nem; i += blockDim.x)
+            q[QC_NPL * 5u + i] = reinterpret_cast<const F4*>(P.S.prims + P.S.emitters[i / 5u])[i % 5u];
+        for (uint32_t i = threadIdx.x; i < ntop; i += blockDim.x)
+            q[(QC_NPL + QC_NEM) * 5u + i] = reinterpret_cast<const F4*>(P.aux)[i];
+        if (threadIdx.x < P.S.n_planes) Q.pl_id[threadIdx.x] = P.S.planes[threadIdx.x];
+        __syncthreads();
+    }
     const uint32_t* in = P.ctl + PT_CTL_SET * P.parity;
     uint32_t* out = P.ctl + PT_CTL_SET * (1u - P.parity);
     const uint32_t n_carry = in[C_CARRY], n_total = in[C_FRESH] + n_carry;
     const RayQ FQ = P.fq[P.parity];
     QCounts C{0u, 0u, 0u, 0u};
     uint32_t rays = 0u, fallbacks = 0u, prog = 0u;
+#ifdef PT_CPROF
+    // expansion, candidates, decisions, shading, next ray, chain cycles, chains, wave lifetime
+    uint64_t cp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint64_t cp_start = __builtin_amdgcn_s_memtime();
+#endif
+    bool have = false, exhausted = false;
+    uint32_t slot = 0u;
+    Ray ray;
+    ray.o = ray.d = mk3(0.f, 0.f, 0.f);
+    float Pt = PT_INF;
+    int pid = -1;
+    F4 pre = F4{0.f, 0.f, 0.f, 0.f};
+    CoopPixel px;
+    px.R.x = 0u;
+    px.R.saved = 0.f;
+    px.R.saved_ok = 0u;
+    px.nv = px.done = 0u;
+    px.sum = mk3(0.f, 0.f, 0.f);
     for (;;) {
-        uint32_t gi = 0u;
-        if (lane == 0u) gi = atomicAdd(out + C_HEADS, 1u);
-        gi = __builtin_amdgcn_readfirstlane(gi);
-        if (gi >= n_total) break;
-        Ray ray;
-        float Pt;
-        int pid;
-        F4 pre;
-        uint32_t slot;
-        if (gi < n_carry) {
-            // a query suspended by the path engine: restarted from its ray (a query is a
-            // function of the ray alone; its ray and plane tests were counted when taken)
-            const uint32_t* w = P.cq[P.parity] + (size_t)gi * P.carry_words;
-            ray = reinterpret_cast<const Query*>(w)->ray;
-            slot = w[sizeof(Query) / 4u];
-            q_planes(P.S, ray, Pt, pid);
-            pre = q_prep(P.S, ray);
-        } else {
-            const uint32_t fi = gi - n_carry;
-            const F4 o = FQ.ro[fi], d = FQ.rd[fi];
-            ray.o = mk3(o.x, o.y, o.z);
-            ray.d = mk3(d.x, d.y, d.z);
-            slot = f2u(o.w);
-            Pt = d.w;
-            pid = FQ.pid[fi];
-            pre = FQ.ri[fi];
-            if (lane == 0u) { rays++; C.planes += P.S.n_planes; }
-        }
-        for (;;) {
-            bool ex;
-            int id = qc_wave(P.S, L, ray, Pt, pid, pre, P.coop_slim, C, ex);
-            if (ex) {
-                // the exact stack DFS on lane 0 (non-finite rays, > QC_HCAP hitting leaves)
-                if (lane == 0u) {
-                    LdsMemN<1u> stk{L.stk};
-                    Hit h;
-                    id = q_exact(P.S, ray, stk, h, C);
-                    fallbacks++;
+        // teams without a chain take the next one (queue order: carry, then fresh)
+        const bool need = !have && !exhausted;
+        if (__ballot(need) != 0ull) {
+            uint32_t gi = wave_append(out + C_HEADS, need && tl == 0u);
+            gi = __shfl(gi, (int)tbase, 64);
+            if (need) {
+                if (gi >= n_total) {
+                    exhausted = true;
+                } else {
+                    have = true;
+#ifdef PT_CPROF
+                    if (tl == 0u) cp[6]++;
+#endif
+                    if (gi < n_carry) {
+                        // a query suspended by the path engine: restarted from its ray (a query is a
+                        // function of the ray alone; its ray and plane tests were counted when taken)
+                        const uint32_t* w = P.cq[P.parity] + (size_t)gi * P.carry_words;
+                        ray = reinterpret_cast<const Query*>(w)->ray;
+                        slot = w[sizeof(Query) / 4u];
+                        q_planes_e(P.S, PlanesLds{Q}, ray, Pt, pid);
+                        pre = q_prep(P.S, ray);
+                    } else {
+                        const uint32_t fi = gi - n_carry;
+                        const F4 o = FQ.ro[fi], d = FQ.rd[fi];
+                        ray.o = mk3(o.x, o.y, o.z);
+                        ray.d = mk3(d.x, d.y, d.z);
+                        slot = f2u(o.w);
+                        Pt = d.w;
+                        pid = FQ.pid[fi];
+                        pre = FQ.ri[fi];
+                        if (tl == 0u) { rays++; C.planes += P.S.n_planes; }
+                    }
+                    // the pixel's state for the chain's life: RNG / vertices / samples and the
+                    // sum in the first lane's registers, the current path's fold records in LDS
+                    const PixelHot hot = load_hot(P.st, slot);
+                    px.R = hot.R;
+                    px.nv = hot.nv;
+                    px.done = hot.done;
+                    px.sum = load_sum(P.st, slot);
+                    if (tl < hot.nv) {
+                        // the current path's vertices so far (written by the path engine)
+                        const uint4 f = P.st.fold[(size_t)slot * P.st.depth + tl];
+                        L.fold[tl] = f;
+                        L.fold_sh[tl] = P.S.shade[f.x & 0x3fffffffu];
+                    }
                 }
-                id = __builtin_amdgcn_readfirstlane(id);
             }
-            bool emit = false, sdone = false;
-            if (lane == 0u) {
-                emit = shade_item(P, slot, ray, id < 0 ? 0xffffffffu : (uint32_t)id, sdone);
-                prog += sdone ? 1u : 0u;
-                if (emit) { rays++; C.planes += P.S.n_planes; }
-            }
-            if (!__builtin_amdgcn_readfirstlane(emit ? 1u : 0u)) break;
-            // the chain's next ray (lane 0's), its plane test and query set-up on every lane
-            ray.o = mk3(bcast_f(ray.o.x), bcast_f(ray.o.y), bcast_f(ray.o.z));
-            ray.d = mk3(bcast_f(ray.d.x), bcast_f(ray.d.y), bcast_f(ray.d.z));
-            q_planes(P.S, ray, Pt, pid);
-            pre = q_prep(P.S, ray);
         }
-        if (P.progress && lane == 0u && prog >= 256u) {
+        if (__ballot(have) == 0ull) break;
+        bool ex, bvh;
+        Hit h;
+        int id = qc_team<T>(P.S, Q, L, have, ray, Pt, pid, pre, P.coop_reserve, C, ex, h, bvh QC_CP_PASS);
+        bool emit = false, sdone = false;
+        QC_T0();
+        if (tl == 0u && have) {
+            if (ex) {
+                // the exact stack DFS (non-finite rays, too many hitting leaves)
+                LdsMemN<1u> stk{L.stk};
+                id = q_exact(P.S, ray, stk, h, C);
+                fallbacks++;
+            } else if (id >= 0 && !bvh) {
+                // the plane hit (its record from the LDS copy)
+                Prim pr = P.S.prims[id];
+                for (uint32_t k = 0; k < P.S.n_planes; ++k)
+                    if (Q.pl_id[k] == (uint32_t)id) pr = Q.pl[k];
+                (void)prim_intersect(pr, ray, h);
+            }
+            emit = coop_shade(P, Q, L, px, slot, ray, id, h, sdone);
+            prog += sdone ? 1u : 0u;
+            if (emit) { rays++; C.planes += P.S.n_planes; }
+        }
+        emit = __shfl(emit ? 1 : 0, (int)tbase, 64) != 0;
+        QC_TICK(3);
+        if (have && !emit) {
+            // the pixel has reached the pass target: its state back to HBM
+            if (tl == 0u) {
+                PixelHot hot;
+                hot.R = px.R;
+                hot.nv = px.nv;
+                hot.done = px.done;
+                store_hot(P.st, slot, hot);
+                store_sum(P.st, slot, px.sum);
+            }
+            have = false;
+        }
+        if (__ballot(have) != 0ull) {
+            // the chains' next rays (the first lanes'), plane tests and query set-up on every lane
+            ray.o = mk3(__shfl(ray.o.x, (int)tbase, 64), __shfl(ray.o.y, (int)tbase, 64), __shfl(ray.o.z, (int)tbase, 64));
+            ray.d = mk3(__shfl(ray.d.x, (int)tbase, 64), __shfl(ray.d.y, (int)tbase, 64), __shfl(ray.d.z, (int)tbase, 64));
+            if (have) {
+                q_planes_e(P.S, PlanesLds{Q}, ray, Pt, pid);
+                pre = q_prep(P.S, ray);
+            }
+#ifdef PT_CPROF
+            if (have && tl == 0u) cp[5]++;
+#endif
+        }
+        QC_TICK(4);
+        if (P.progress && tl == 0u && prog >= 256u) {
             __hip_atomic_fetch_add(P.progress, (unsigned long long)prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             prog = 0u;
         }
     }
-    if (P.progress && lane == 0u && prog)
+    if (P.progress && tl == 0u && prog)
         __hip_atomic_fetch_add(P.progress, (unsigned long long)prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     unsigned long long* ctr = ctr_copy(P.counters);
     wave_add_u64(ctr + 0, rays);
@@ -1041,6 +1297,17 @@ __global__ void __launch_bounds__(64u * QC_WAVES) k_wcoop(WaveParams P) {
     wave_add_u64(ctr + 3, C.planes);
     wave_add_u64(ctr + 5, C.aux);
     wave_add_u64(ctr + 6, fallbacks);
+#ifdef PT_CPROF
+    // (per team first lanes: chain counts; cycle sums are per wave, counted by lane 0)
+    cp[7] = __builtin_amdgcn_s_memtime() - cp_start;
+    if (P.wg_prof && tl == 0u) {
+        for (int i = 5; i < 7; ++i) atomicAdd(P.wg_prof + i, (unsigned long long)cp[i]);
+        if (lane == 0u) {
+            for (int i = 0; i < 5; ++i) atomicAdd(P.wg_prof + i, (unsigned long long)cp[i]);
+            atomicAdd(P.wg_prof + 7, (unsigned long long)cp[7]);
+        }
+    }
+#endif
 }
 
 // exact stack DFS for the handed-back rays; 64-lane workgroups, stack in LDS
@@ -1117,12 +1384,16 @@ hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t pt_launch_coop(pt::WaveParams p, uint32_t grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+hipError_t pt_launch_coop(pt::WaveParams p, uint32_t grid, uint32_t team, hipStream_t s, hipEvent_t e0,
+                          hipEvent_t e1) {
     hipError_t e = hipMemsetAsync(p.ctl + PT_CTL_SET * (1u - p.parity), 0, 4u * PT_CTL_SET, s);
     if (e != hipSuccess) return e;
     p.path = 1u;
     if (e0 && (e = hipEventRecord(e0, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(pt::k_wcoop, dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
+    if (team == 8u) hipLaunchKernelGGL(pt::k_wcoop<8u>, dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
+    else if (team == 16u) hipLaunchKernelGGL(pt::k_wcoop<16u>, dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
+    else if (team == 32u) hipLaunchKernelGGL(pt::k_wcoop<32u>, dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
+    else hipLaunchKernelGGL(pt::k_wcoop<64u>, dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
     if (e1 && (e = hipEventRecord(e1, s)) != hipSuccess) return e;
     return hipGetLastError();
 }

@@ -78,11 +78,13 @@ const Rccl& rccl() {
 //   sparse_steps=N    steps per loop trip of the end-of-pass kernel
 //   coop=N            a round with at most N chains runs the cooperative engine (one wave
 //                     per chain) to the end of the pass (0: never)
+//   coop_team=T       lanes per chain in the cooperative engine (16, 32, 64)
 //   cap=N             chains a workgroup may hold
 //   rowmajor=1        seed a pass in row-major tile order instead of Z-order
 //   variant=V         megakernel variant bits (1 filtered tests, 2 XCD-banded tiles)
 //   roundlog=1|2      per-round kernel times / pixels' remaining samples on stderr
 //   wgprof=FILE       per-workgroup timelines (-DPT_WPROF builds)
+//   cprof=1           per-phase cycles of the cooperative engine on stderr (-DPT_CPROF builds)
 //   qstats=FILE       per-query work counters of the host self-test render
 //   qengine=coop      host self-tests: the cooperative engine's query algorithm (pt_coop.h)
 std::string tune_str(const char* key) {
@@ -183,7 +185,9 @@ struct pt_session {
     bool wave = false;
     pt::F4* ring = nullptr;       // path engine: path_grid * PT_RING_F4
     uint32_t path_grid = 0, path_budget = 1024, path_runend = 0, path_sparse = 0, sparse_steps = 8;
-    uint32_t coop_max = 0, coop_grid = 0, coop_slim = 0;   // cooperative engine (k_wcoop) at the end of a pass
+    uint32_t coop_max = 0, coop_grid = 0, coop_reserve = 0;   // cooperative engine (k_wcoop) at the end of a pass
+    uint32_t coop_team = 8;       // lanes per chain in the cooperative engine (pure-coop rate, teams of
+                                  // 64 / 32 / 16 / 8: 283 / 392 / 572 / 815 Mray/s)
     pt::F4* qbuf = nullptr;       // 10 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd, fq0.ri, fq1.ri
     uint32_t* hid = nullptr;      // n_slots (done.id)
     uint32_t* pidbuf = nullptr;   // 2 * n_slots (fresh queues' plane prims)
@@ -734,15 +738,27 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // wave per chain) to the end of the pass; it needs a wave's aux stack to hold
         // a depth-first descent below its expansion limit, and lane 0's exact DFS stack
         const uint32_t cus = (uint32_t)std::max(1, pr.multiProcessorCount);
-        ss->coop_max = cus * 256u;   // 65,536 on the 256-CU part (rank-of-8 sweep: 4 k / 16 k / 64 k)
+        // 131,072 on the 256-CU part (rank-of-8 sweep, teams of 8: 65 k 1,245-1,261, 131 k 1,280,
+        // 200 k 1,199, 300 k 789 Mray/s per GPU)
+        ss->coop_max = cus * 512u;
         ss->coop_max = (uint32_t)std::max(0, tune_int("coop", (int)ss->coop_max));
         ss->coop_grid = cus * 8u;
-        const uint32_t reserve = 4u * (s->auxsl_depth + 2u);
-        if (QC_SCAP < reserve + 64u || s->max_stack > QC_SCAP) ss->coop_max = 0;
-        else ss->coop_slim = QC_SCAP - reserve;
+        // (a depth-first descent below the expansion limit adds at most 3 entries per level)
+        const uint32_t reserve = 3u * (s->auxsl_depth + 2u);
+        ss->coop_team = (uint32_t)tune_int("coop_team", (int)ss->coop_team);
+        if (ss->coop_team != 8u && ss->coop_team != 16u && ss->coop_team != 32u) ss->coop_team = 64u;
+        const uint32_t scap = ss->coop_team == 64u ? 448u : ss->coop_team == 32u ? 192u : QC_SCAP_MIN;
+        if (scap < reserve + 64u || s->max_stack > scap) ss->coop_team = 64u;   // deep trees: whole-wave teams
+        if (448u < reserve + 64u || s->max_stack > 448u || ss->depth > QC_FOLD || s->planes.size() > QC_NPL ||
+            s->emitters.size() > QC_NEM)
+            ss->coop_max = 0;
+        else ss->coop_reserve = reserve;
         // with the cooperative engine the path engine never runs a round to the end:
         // its rounds stay budget-limited, so the host sees the chains fall below coop_max
         if (ss->coop_max && !tune_has("runend")) ss->path_runend = 0;
+        // ... and the end-of-pass (sparse) path kernel, whose rounds are long, never runs
+        // above the hand-over
+        if (ss->coop_max && !tune_has("sparse")) ss->path_sparse = std::min(ss->path_sparse, ss->coop_max);
         if (hipMalloc(&ss->ring, (size_t)ss->path_grid * PT_RING_F4 * sizeof(pt::F4)) != hipSuccess)
             return cleanup(fail(PT_E_OOM, "device allocation failed (path rings)"));
         if (ss->n_tiles_local) {
@@ -838,7 +854,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     if (tune_has("cap")) wp.path_cap = std::min<uint32_t>(PT_CMAX, (uint32_t)std::max(64, tune_int("cap", 0)));
     wp.tile_order = tune_int("rowmajor", 0) ? nullptr : ss->tile_order;
     wp.sparse_steps = ss->sparse_steps;
-    wp.coop_slim = ss->coop_slim;
+    wp.coop_reserve = ss->coop_reserve;
     wp.ring = ss->ring;
     if (ss->on_progress && !ss->prog_host) {
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ss->prog_host), 8, hipHostMallocMapped | hipHostMallocCoherent));
@@ -868,8 +884,28 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             HIP_TRY(hipEventCreate(&i1));
             ss->pending_isect.emplace_back(i0, i1);
             ss->isect_launches++;
-            const uint32_t grid = std::max(1u, std::min(ss->coop_grid, (chains + QC_WAVES - 1u) / QC_WAVES));
-            HIP_TRY(pt_launch_coop(wp, grid, ss->stream, i0, i1));
+            const uint32_t per_wg = QC_WAVES * (64u / ss->coop_team);   // chains per workgroup
+            const uint32_t grid = std::max(1u, std::min(ss->coop_grid, (chains + per_wg - 1u) / per_wg));
+            const bool cprof = tune_has("cprof");   // -DPT_CPROF builds: per-phase cycles on stderr
+            if (cprof) {
+                if (!ss->wg_prof) HIP_TRY(hipMalloc(&ss->wg_prof, 256ull * ss->path_grid));
+                HIP_TRY(hipMemsetAsync(ss->wg_prof, 0, 64, ss->stream));
+                wp.wg_prof = ss->wg_prof;
+            }
+            HIP_TRY(pt_launch_coop(wp, grid, ss->coop_team, ss->stream, i0, i1));
+            if (cprof) {
+                unsigned long long cp[8];
+                HIP_TRY(hipMemcpyAsync(cp, wp.wg_prof, 64, hipMemcpyDeviceToHost, ss->stream));
+                HIP_TRY(hipStreamSynchronize(ss->stream));
+                float ms = 0.f;
+                HIP_TRY(hipEventElapsedTime(&ms, i0, i1));
+                const double cyc = (double)std::max(1ull, cp[5] + cp[6]) / (64.0 / ss->coop_team);
+                fprintf(stderr, "coop chains %u grid %u: %.2f ms, chain cycles %llu, chains %llu; cycles per chain cycle: "
+                        "expand %.0f cand %.0f decide %.0f shade %.0f nextray %.0f; wave lifetime %.0f\n",
+                        chains, grid, ms, cp[5], cp[6], cp[0] / cyc, cp[1] / cyc, cp[2] / cyc, cp[3] / cyc, cp[4] / cyc,
+                        (double)cp[7] / (grid * (double)QC_WAVES));
+                wp.wg_prof = nullptr;
+            }
             ss->rounds++;
             p ^= 1u;
             HIP_TRY(hipMemcpyAsync(ss->ctl_host, ss->ctl + PT_CTL_SET * p, 8, hipMemcpyDeviceToHost, ss->stream));

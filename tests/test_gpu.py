@@ -153,14 +153,16 @@ def test_device_init(pt):
     assert pt._lib.pt_device_init(4096) == pt.PT_E_NO_GPU
 
 
-@pytest.mark.parametrize("engine", ["coop", "path"])
+@pytest.mark.parametrize("engine", ["coop64", "coop32", "coop16", "coop8", "path"])
 @pytest.mark.parametrize("name", sorted(M["images"]))
 def test_golden_images_each_engine(pt, name, engine, monkeypatch):
     """The replay traversal with one engine for the whole pass: the cooperative
-    engine (one wave per chain: breadth-first aux expansion, all candidate leaves
-    at once, root paths as one round of loads; pt_coop.h) or the path engine alone
-    (coop=0).  Both must reproduce the reference's bytes and ray count."""
-    monkeypatch.setenv("PT_TUNE", "coop=%s" % ("100000000" if engine == "coop" else "0"))
+    engine (a team of 64, 32 or 16 lanes per chain: breadth-first aux expansion,
+    all candidate leaves at once, root paths a block of nodes per round;
+    pt_coop.h) or the path engine alone (coop=0).  All must reproduce the
+    reference's bytes and ray count."""
+    coop = engine.startswith("coop")
+    monkeypatch.setenv("PT_TUNE", "coop=%s,coop_team=%s" % ("100000000" if coop else "0", engine[4:] if coop else "64"))
     m, img, rad = U.golden_image(name)
     with pt.Scene.load(U.golden_scene_path(name)) as s:
         s.prepare()
@@ -169,14 +171,15 @@ def test_golden_images_each_engine(pt, name, engine, monkeypatch):
     assert st["errors"] == 0
     assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
     assert np.array_equal(rgb, img)
-    if engine == "coop":
+    if coop:
         assert st["rounds"] == 1
 
 
+@pytest.mark.parametrize("team", ["64", "16", "8"])
 @pytest.mark.parametrize("cfg", ["c1", "c2"])
-def test_coop_engine_full_config_md5(pt, cfg, monkeypatch):
+def test_coop_engine_full_config_md5(pt, cfg, team, monkeypatch):
     """Configs 1 and 2 entirely on the cooperative engine: reference md5 and ray count."""
-    monkeypatch.setenv("PT_TUNE", "coop=100000000")
+    monkeypatch.setenv("PT_TUNE", "coop=100000000,coop_team=" + team)
     full = M["full"][cfg]
     with pt.Scene.load(U.scene_path(cfg)) as s:
         rgb, _, st = s.render()
