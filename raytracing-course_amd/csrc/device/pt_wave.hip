@@ -841,6 +841,27 @@ struct EmitLds {
     __device__ Prim operator()(uint32_t k) const { return Q.em[k]; }
 };
 
+// bvh_prim_intersect from the compact record (pt_query.h): a plain triangle (pos = +0,
+// rotation exactly (0,0,0,1)) is tested on the world ray -- the world->local transform
+// changes at most the sign of zero components, which changes neither the decision nor
+// t, nor the sign of dn that picks the normal's side (pt_query.h R_LEAF) -- and its
+// normal goes through the same last step, normalize(qrot(rotation, n)), so the Hit
+// has the full test's bits; other records expand to the full form.
+__device__ __forceinline__ bool qc_prim_hit(const SceneView& S, uint32_t i, const Ray& ray, Hit& h) {
+    const uint32_t o = S.o_qprim + 48u * i;
+    const F4 r0 = blob_piece(S, o), r1 = blob_piece(S, o + 16u), r2 = blob_piece(S, o + 32u);
+    const uint32_t ty = f2u(r0.w);
+    if (ty == T_TRIANGLE) {
+        if (!isect_triangle(ray, mk3(r0.x, r0.y, r0.z), mk3(r1.x, r1.y, r1.z), mk3(r1.w, r2.x, r2.y), h)) return false;
+        q4 q;
+        q.x = 0.f; q.y = 0.f; q.z = 0.f; q.w = 1.f;
+        h.n = normalize(qrot(q, h.n));
+        return true;
+    }
+    if (ty & PT_QP_FULL) return bvh_prim_intersect(S.prims[i], ray, h);
+    return bvh_prim_intersect(qprim_expand(r0, r1, r2), ray, h);
+}
+
 #ifdef PT_CPROF
 // diagnostics build: per-phase shader cycles of the cooperative engine (summed per wave)
 #define QC_T0() uint64_t qc_t = __builtin_amdgcn_s_memtime()
@@ -904,7 +925,7 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
                 if (i < cnt) {
                     Hit hh;
                     C.ptests++;
-                    if (bvh_prim_intersect(S.prims[ref + i], ray, hh) && hh.t < best.t) { best = hh; lid = (int)(ref + i); }
+                    if (qc_prim_hit(S, ref + i, ray, hh) && hh.t < best.t) { best = hh; lid = (int)(ref + i); }
                 }
             }
             const unsigned long long m = __ballot(lid >= 0) & tmask;

@@ -869,7 +869,9 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     HIP_TRY(pt_launch_wave_start(wp, ss->stream));
     // rounds until no fresh ray and no suspended query is left; counts are
     // checked every few rounds (empty rounds are cheap, syncs are not free)
-    uint32_t p = 0, batch = 4;
+    // (the first round is counted alone: it ends once the pass's work is handed out, and
+    // the cooperative engine may take over right after it)
+    uint32_t p = 0, batch = ss->coop_max ? 1u : 4u;
     // end-of-pass kernel when the chains of the last counted round are few; before
     // the first count, the pass's pixels (at most one chain each) decide
     bool sparse = ss->n_slots < ss->path_sparse;
