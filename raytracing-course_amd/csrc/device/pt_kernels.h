@@ -68,7 +68,8 @@ enum : uint32_t { PE_LIVE = 0u, PE_MISS = 1u, PE_CUT = 2u, PE_TERM = 3u };
 
 // round counters: set p = ctl + PT_CTL_SET * p; the work-batch heads are one per
 // XCD, each on its own 128-B line (C_HEADS + 32 x)
-enum : uint32_t { C_FRESH = 0u, C_CARRY = 1u, C_DONE = 3u, C_EXACT = 4u, C_FRONT = 5u, C_BACK = 6u, C_HEADS = 32u };
+enum : uint32_t { C_FRESH = 0u, C_CARRY = 1u, C_DONE = 3u, C_EXACT = 4u, C_FRONT = 5u, C_BACK = 6u, C_LIVE = 8u,
+                  C_HEADS = 32u };
 #define PT_CTL_SET 288u          // words per counter set (C_HEADS + 8 x 32)
 // statistics counters: one copy per XCD (PT_CTR_COPIES x PT_CTR_STRIDE u64), summed by the host
 #define PT_CTR_COPIES 8u
@@ -104,7 +105,9 @@ struct WaveParams {
     const uint32_t* tile_order;   // k_wcamera: block b seeds local tile tile_order[b] (null: tile b)
     uint32_t sparse_steps;        // steps per loop trip of the end-of-pass (sparse) kernel
     F4* ring;                     // per-workgroup ray/done rings, PT_RING_F4 F4 per workgroup
-    uint32_t coop_reserve;        // k_wcoop: aux stack words kept free for a depth-first descent (4 (aux depth + 2))
+    uint32_t coop_reserve;        // k_wcoop: aux stack words kept free for a depth-first descent (3 (aux depth + 2))
+    uint32_t coop_stop;           // k_wcoop: once the queue is empty and at most this many chains are held,
+                                  // they leave for the next launch (0: run to the end)
 };
 
 // path engine geometry: PT_NQ query waves + 1 shade wave per workgroup; at most

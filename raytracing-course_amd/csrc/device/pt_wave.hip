@@ -1211,6 +1211,11 @@ k_wcoop(WaveParams P) {
         if (__ballot(need) != 0ull) {
             uint32_t gi = wave_append(out + C_HEADS, need && tl == 0u);
             gi = __shfl(gi, (int)tbase, 64);
+            if (P.coop_stop) {
+                // chains held, for the hand-over to the next launch (coop_stop)
+                const uint32_t got = (uint32_t)__popcll(__ballot(need && tl == 0u && gi < n_total));
+                if (lane == 0u && got) atomicAdd(out + C_LIVE, got);
+            }
             if (need) {
                 if (gi >= n_total) {
                     exhausted = true;
@@ -1279,8 +1284,24 @@ k_wcoop(WaveParams P) {
         }
         emit = __shfl(emit ? 1 : 0, (int)tbase, 64) != 0;
         QC_TICK(3);
-        if (have && !emit) {
-            // the pixel has reached the pass target: its state back to HBM
+        // hand-over: once every chain has been taken and few are left, they leave for the
+        // next launch (whole-wave teams: a shorter chain cycle) at this cycle boundary
+        bool leave = false;
+        if (P.coop_stop && __ballot(have) != 0ull) {
+            uint32_t lv = 0u, hd = 0u;
+            const uint32_t fin = (uint32_t)__popcll(__ballot(have && !emit && tl == 0u));
+            if (lane == 0u) {
+                if (fin) atomicSub(out + C_LIVE, fin);
+                lv = __hip_atomic_load(out + C_LIVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                hd = __hip_atomic_load(out + C_HEADS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            lv = __builtin_amdgcn_readfirstlane(lv);
+            hd = __builtin_amdgcn_readfirstlane(hd);
+            leave = hd >= n_total && lv <= P.coop_stop;
+        }
+        if (have && (!emit || leave)) {
+            // the pixel's state back to HBM: at the pass target, or (leave) mid-path with its
+            // fold records, its next ray going to the next round's fresh queue
             if (tl == 0u) {
                 PixelHot hot;
                 hot.R = px.R;
@@ -1289,8 +1310,24 @@ k_wcoop(WaveParams P) {
                 store_hot(P.st, slot, hot);
                 store_sum(P.st, slot, px.sum);
             }
-            have = false;
+            if (emit) {
+                const uint32_t nv = (uint32_t)__shfl((int)px.nv, (int)tbase, 64);
+                if (tl < nv) P.st.fold[(size_t)slot * P.st.depth + tl] = L.fold[tl];
+            }
         }
+        if (leave) {
+            const bool go = have && emit && tl == 0u;
+            const uint32_t k = wave_append(out + C_FRESH, go);
+            if (go) {
+                push_ray(P, P.fq[1u - P.parity], k, ray, slot);
+                rays--;                          // counted again when the next launch takes it
+                C.planes -= P.S.n_planes;
+            }
+            const uint32_t ng = (uint32_t)__popcll(__ballot(go));
+            if (lane == 0u && ng) atomicSub(out + C_LIVE, ng);
+            emit = false;
+        }
+        if (have && !emit) have = false;
         if (__ballot(have) != 0ull) {
             // the chains' next rays (the first lanes'), plane tests and query set-up on every lane
             ray.o = mk3(__shfl(ray.o.x, (int)tbase, 64), __shfl(ray.o.y, (int)tbase, 64), __shfl(ray.o.z, (int)tbase, 64));

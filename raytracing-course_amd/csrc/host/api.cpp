@@ -78,7 +78,8 @@ const Rccl& rccl() {
 //   sparse_steps=N    steps per loop trip of the end-of-pass kernel
 //   coop=N            a round with at most N chains runs the cooperative engine (one wave
 //                     per chain) to the end of the pass (0: never)
-//   coop_team=T       lanes per chain in the cooperative engine (16, 32, 64)
+//   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
+//   coop_stop=N       the first cooperative launch hands its last N chains to whole-wave teams (0: never)
 //   cap=N             chains a workgroup may hold
 //   rowmajor=1        seed a pass in row-major tile order instead of Z-order
 //   variant=V         megakernel variant bits (1 filtered tests, 2 XCD-banded tiles)
@@ -186,6 +187,7 @@ struct pt_session {
     pt::F4* ring = nullptr;       // path engine: path_grid * PT_RING_F4
     uint32_t path_grid = 0, path_budget = 1024, path_runend = 0, path_sparse = 0, sparse_steps = 8;
     uint32_t coop_max = 0, coop_grid = 0, coop_reserve = 0;   // cooperative engine (k_wcoop) at the end of a pass
+    uint32_t coop_stop = 0;       // chains left when the first cooperative launch hands over to whole waves
     uint32_t coop_team = 8;       // lanes per chain in the cooperative engine (pure-coop rate, teams of
                                   // 64 / 32 / 16 / 8: 283 / 392 / 572 / 815 Mray/s)
     pt::F4* qbuf = nullptr;       // 10 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd, fq0.ri, fq1.ri
@@ -743,6 +745,10 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         ss->coop_max = cus * 512u;
         ss->coop_max = (uint32_t)std::max(0, tune_int("coop", (int)ss->coop_max));
         ss->coop_grid = cus * 8u;
+        // chains left when the first (narrow-team) launch hands over to whole-wave teams; off:
+        // letting the teams of 8 finish measured faster (1 / 4 / 12 / 32 / 64 k chains: rank-of-1
+        // 1,643 -> 1,592 / 1,543 / 1,555 / 1,605, rank-of-8 1,290 -> 1,267-1,283 Mray/s)
+        ss->coop_stop = (uint32_t)std::max(0, tune_int("coop_stop", 0));
         // (a depth-first descent below the expansion limit adds at most 3 entries per level)
         const uint32_t reserve = 3u * (s->auxsl_depth + 2u);
         ss->coop_team = (uint32_t)tune_int("coop_team", (int)ss->coop_team);
@@ -879,49 +885,56 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     uint32_t chains = ss->n_slots;
     for (uint32_t guard = 0;; ++guard) {
         if (chains <= ss->coop_max) {
-            // one launch runs every remaining chain to the end of the pass
-            wp.parity = p;
-            hipEvent_t i0, i1;
-            HIP_TRY(hipEventCreate(&i0));
-            HIP_TRY(hipEventCreate(&i1));
-            ss->pending_isect.emplace_back(i0, i1);
-            ss->isect_launches++;
-            const uint32_t per_wg = QC_WAVES * (64u / ss->coop_team);   // chains per workgroup
-            const uint32_t grid = std::max(1u, std::min(ss->coop_grid, (chains + per_wg - 1u) / per_wg));
-            const bool cprof = tune_has("cprof");   // -DPT_CPROF builds: per-phase cycles on stderr
-            if (cprof) {
-                if (!ss->wg_prof) HIP_TRY(hipMalloc(&ss->wg_prof, 256ull * ss->path_grid));
-                HIP_TRY(hipMemsetAsync(ss->wg_prof, 0, 64, ss->stream));
-                wp.wg_prof = ss->wg_prof;
-            }
-            HIP_TRY(pt_launch_coop(wp, grid, ss->coop_team, ss->stream, i0, i1));
-            if (cprof) {
-                unsigned long long cp[8];
-                HIP_TRY(hipMemcpyAsync(cp, wp.wg_prof, 64, hipMemcpyDeviceToHost, ss->stream));
-                HIP_TRY(hipStreamSynchronize(ss->stream));
-                float ms = 0.f;
-                HIP_TRY(hipEventElapsedTime(&ms, i0, i1));
-                const double cyc = (double)std::max(1ull, cp[5] + cp[6]) / (64.0 / ss->coop_team);
-                fprintf(stderr, "coop chains %u grid %u: %.2f ms, chain cycles %llu, chains %llu; cycles per chain cycle: "
-                        "expand %.0f cand %.0f decide %.0f shade %.0f nextray %.0f; wave lifetime %.0f\n",
-                        chains, grid, ms, cp[5], cp[6], cp[0] / cyc, cp[1] / cyc, cp[2] / cyc, cp[3] / cyc, cp[4] / cyc,
-                        (double)cp[7] / (grid * (double)QC_WAVES));
-                wp.wg_prof = nullptr;
-            }
-            ss->rounds++;
-            p ^= 1u;
-            HIP_TRY(hipMemcpyAsync(ss->ctl_host, ss->ctl + PT_CTL_SET * p, 8, hipMemcpyDeviceToHost, ss->stream));
-            if (wp.progress) {
-                hipError_t e;
-                while ((e = hipStreamQuery(ss->stream)) == hipErrorNotReady) {
-                    ss->on_progress(__atomic_load_n(ss->prog_host, __ATOMIC_RELAXED));
-                    std::this_thread::sleep_for(std::chrono::microseconds(500));
+            // the cooperative engine runs every remaining chain to the end of the pass: teams
+            // of coop_team lanes first; once the queue is empty and at most coop_stop chains are
+            // left, those move on to a second launch with whole-wave teams (shorter chain cycle)
+            for (uint32_t stage = 0; chains; ++stage) {
+                const uint32_t team = stage == 0 ? ss->coop_team : 64u;
+                wp.parity = p;
+                wp.coop_stop = stage == 0 && team != 64u ? ss->coop_stop : 0u;
+                hipEvent_t i0, i1;
+                HIP_TRY(hipEventCreate(&i0));
+                HIP_TRY(hipEventCreate(&i1));
+                ss->pending_isect.emplace_back(i0, i1);
+                ss->isect_launches++;
+                const uint32_t per_wg = QC_WAVES * (64u / team);   // chains per workgroup
+                const uint32_t grid = std::max(1u, std::min(ss->coop_grid, (chains + per_wg - 1u) / per_wg));
+                const bool cprof = tune_has("cprof");   // -DPT_CPROF builds: per-phase cycles on stderr
+                if (cprof) {
+                    if (!ss->wg_prof) HIP_TRY(hipMalloc(&ss->wg_prof, 256ull * ss->path_grid));
+                    HIP_TRY(hipMemsetAsync(ss->wg_prof, 0, 64, ss->stream));
+                    wp.wg_prof = ss->wg_prof;
                 }
-                HIP_TRY(e);
+                HIP_TRY(pt_launch_coop(wp, grid, team, ss->stream, i0, i1));
+                if (cprof) {
+                    unsigned long long cp[8];
+                    HIP_TRY(hipMemcpyAsync(cp, wp.wg_prof, 64, hipMemcpyDeviceToHost, ss->stream));
+                    HIP_TRY(hipStreamSynchronize(ss->stream));
+                    float ms = 0.f;
+                    HIP_TRY(hipEventElapsedTime(&ms, i0, i1));
+                    const double cyc = (double)std::max(1ull, cp[5] + cp[6]) / (64.0 / team);
+                    fprintf(stderr, "coop T=%u chains %u grid %u: %.2f ms, chain cycles %llu, chains %llu; cycles per chain "
+                            "cycle: expand %.0f cand %.0f decide %.0f shade %.0f nextray %.0f; wave lifetime %.0f\n",
+                            team, chains, grid, ms, cp[5], cp[6], cp[0] / cyc, cp[1] / cyc, cp[2] / cyc, cp[3] / cyc,
+                            cp[4] / cyc, (double)cp[7] / (grid * (double)QC_WAVES));
+                    wp.wg_prof = nullptr;
+                }
+                ss->rounds++;
+                p ^= 1u;
+                HIP_TRY(hipMemcpyAsync(ss->ctl_host, ss->ctl + PT_CTL_SET * p, 8, hipMemcpyDeviceToHost, ss->stream));
+                if (wp.progress) {
+                    hipError_t e;
+                    while ((e = hipStreamQuery(ss->stream)) == hipErrorNotReady) {
+                        ss->on_progress(__atomic_load_n(ss->prog_host, __ATOMIC_RELAXED));
+                        std::this_thread::sleep_for(std::chrono::microseconds(500));
+                    }
+                    HIP_TRY(e);
+                }
+                HIP_TRY(hipStreamSynchronize(ss->stream));
+                if (ss->ctl_host[pt::C_CARRY] != 0u || (stage > 0 && ss->ctl_host[pt::C_FRESH] != 0u))
+                    return fail(PT_E_HIP, "cooperative engine left chains behind");
+                chains = ss->ctl_host[pt::C_FRESH];
             }
-            HIP_TRY(hipStreamSynchronize(ss->stream));
-            if (ss->ctl_host[pt::C_FRESH] != 0u || ss->ctl_host[pt::C_CARRY] != 0u)
-                return fail(PT_E_HIP, "cooperative engine left chains behind");
             break;
         }
         for (uint32_t r = 0; r < batch; ++r) {

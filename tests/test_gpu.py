@@ -153,7 +153,7 @@ def test_device_init(pt):
     assert pt._lib.pt_device_init(4096) == pt.PT_E_NO_GPU
 
 
-@pytest.mark.parametrize("engine", ["coop64", "coop32", "coop16", "coop8", "path"])
+@pytest.mark.parametrize("engine", ["coop64", "coop32", "coop16", "coop8", "coop8h", "path"])
 @pytest.mark.parametrize("name", sorted(M["images"]))
 def test_golden_images_each_engine(pt, name, engine, monkeypatch):
     """The replay traversal with one engine for the whole pass: the cooperative
@@ -161,8 +161,12 @@ def test_golden_images_each_engine(pt, name, engine, monkeypatch):
     all candidate leaves at once, root paths a block of nodes per round;
     pt_coop.h) or the path engine alone (coop=0).  All must reproduce the
     reference's bytes and ray count."""
+    # coop8h: teams of 8, and every chain handed over to whole-wave teams (a second launch)
+    # after its first cycle, mid-path (pixel state, fold records and next ray via HBM)
     coop = engine.startswith("coop")
-    monkeypatch.setenv("PT_TUNE", "coop=%s,coop_team=%s" % ("100000000" if coop else "0", engine[4:] if coop else "64"))
+    team = engine[4:].rstrip("h") if coop else "64"
+    stop = "100000000" if engine.endswith("h") else "0"
+    monkeypatch.setenv("PT_TUNE", "coop=%s,coop_team=%s,coop_stop=%s" % ("100000000" if coop else "0", team, stop))
     m, img, rad = U.golden_image(name)
     with pt.Scene.load(U.golden_scene_path(name)) as s:
         s.prepare()
@@ -172,21 +176,23 @@ def test_golden_images_each_engine(pt, name, engine, monkeypatch):
     assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
     assert np.array_equal(rgb, img)
     if coop:
-        assert st["rounds"] == 1
+        assert st["rounds"] == (2 if engine.endswith("h") else 1)
 
 
-@pytest.mark.parametrize("team", ["64", "16", "8"])
+@pytest.mark.parametrize("team", ["64", "16", "8", "8h"])
 @pytest.mark.parametrize("cfg", ["c1", "c2"])
 def test_coop_engine_full_config_md5(pt, cfg, team, monkeypatch):
-    """Configs 1 and 2 entirely on the cooperative engine: reference md5 and ray count."""
-    monkeypatch.setenv("PT_TUNE", "coop=100000000,coop_team=" + team)
+    """Configs 1 and 2 entirely on the cooperative engine: reference md5 and ray count
+    (8h: teams of 8 handing their last 4,096 chains over to whole-wave teams)."""
+    monkeypatch.setenv("PT_TUNE", "coop=100000000,coop_team=%s,coop_stop=%s" % (team.rstrip("h"),
+                                                                                "4096" if team.endswith("h") else "0"))
     full = M["full"][cfg]
     with pt.Scene.load(U.scene_path(cfg)) as s:
         rgb, _, st = s.render()
         w, h = s.info["width"], s.info["height"]
     ppm = b"P6\n%d %d\n255\n" % (w, h) + rgb.tobytes()
     assert U.md5(ppm) == full["md5"]
-    assert st["rays"] == full["rays"] and st["rounds"] == 1
+    assert st["rays"] == full["rays"] and st["rounds"] == (2 if team.endswith("h") else 1)
 
 
 @pytest.mark.parametrize("engine", ["path", "path_dense", "path_coop"])
