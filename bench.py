@@ -287,17 +287,26 @@ def roofline(st0, st1, traffic_json, key):
     stream).  `traffic` = this run's algorithmic bytes x the profiled ratio of
     memory-side bytes to algorithmic bytes (rocprofv3 FETCH/WRITE passes of the
     same workload, profiles/traffic.json), so it scales with this run's launches."""
-    launches = max(st1["isect_launches"] - st0["isect_launches"], 1)
-    isect_ms = st1["isect_ms"] - st0["isect_ms"]
-    nodes = st1["node_visits"] - st0["node_visits"]
-    ptests = st1["prim_tests"] - st0["prim_tests"]
-    auxv = st1["aux_visits"] - st0["aux_visits"]
+    # the path engine's share: the cooperative end-of-pass launches (k_wcoop) are counted
+    # apart (pt_stats coop_*) and reported in `coop`
+    d = {k: st1[k] - st0[k] for k in ("isect_launches", "isect_ms", "node_visits", "prim_tests", "aux_visits", "rays",
+                                      "coop_launches", "coop_ms", "coop_node_visits", "coop_prim_tests",
+                                      "coop_aux_visits", "coop_rays")}
+    launches = max(d["isect_launches"] - d["coop_launches"], 1)
+    isect_ms = d["isect_ms"] - d["coop_ms"]
+    nodes = d["node_visits"] - d["coop_node_visits"]
+    ptests = d["prim_tests"] - d["coop_prim_tests"]
+    auxv = d["aux_visits"] - d["coop_aux_visits"]
     alg_bytes = (nodes * st1["node_bytes"] + ptests * st1["prim_bytes"] + auxv * st1["aux_bytes"]) / launches
     launch_s = (isect_ms / 1e3) / launches
     achieved = alg_bytes / launch_s / 1e9 if launch_s > 0 else 0.0
     rec = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_wpath",
-           "alg_bytes_per_launch": alg_bytes, "launch_ms": launch_s * 1e3, "launches": launches}
+           "alg_bytes_per_launch": alg_bytes, "launch_ms": launch_s * 1e3, "launches": launches,
+           "rays_share": (d["rays"] - d["coop_rays"]) / max(d["rays"], 1)}
+    if d["coop_launches"]:
+        rec["coop"] = {"kernel": "k_wcoop (end of pass)", "launches": d["coop_launches"], "ms": d["coop_ms"],
+                       "rays": d["coop_rays"], "mray_s": d["coop_rays"] / max(d["coop_ms"], 1e-9) / 1e3}
     prof = None
     try:
         prof = json.load(open(traffic_json)).get(key)

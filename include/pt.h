@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 2   /* 2: pt_render_opts.gather */
+#define PT_ABI_VERSION 3   /* 2: pt_render_opts.gather; 3: pt_stats per-engine (coop_*) fields */
 
 enum {
     PT_OK = 0,
@@ -129,6 +129,11 @@ typedef struct pt_stats {
     uint64_t isect_launches;
     uint64_t rounds;         /* wavefront rounds run */
     uint64_t gather_rccl;    /* 1: the multi-GPU framebuffer was gathered with RCCL (ncclGather over xGMI) */
+    /* the cooperative end-of-pass engine's share of rays / node_visits / prim_tests /
+       aux_visits / isect_ms / isect_launches (the rest is the path engine's) */
+    uint64_t coop_rays, coop_node_visits, coop_prim_tests, coop_aux_visits;
+    double coop_ms;
+    uint64_t coop_launches;
 } pt_stats;
 
 /* Scene::Render minus the stream write: renders W*H*3 u8 (row-major, top row

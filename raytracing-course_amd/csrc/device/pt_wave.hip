@@ -1355,6 +1355,11 @@ k_wcoop(WaveParams P) {
     wave_add_u64(ctr + 3, C.planes);
     wave_add_u64(ctr + 5, C.aux);
     wave_add_u64(ctr + 6, fallbacks);
+    // this engine's share (pt_stats coop_*)
+    wave_add_u64(ctr + 8, rays);
+    wave_add_u64(ctr + 9, C.nodes);
+    wave_add_u64(ctr + 10, C.ptests);
+    wave_add_u64(ctr + 13, C.aux);
 #ifdef PT_CPROF
     // (per team first lanes: chain counts; cycle sums are per wave, counted by lane 0)
     cp[7] = __builtin_amdgcn_s_memtime() - cp_start;

@@ -200,8 +200,9 @@ struct pt_session {
     uint32_t shade_grid = 0, rounds = 0;
     hipStream_t stream = nullptr;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, pending_isect;
-    double kernel_ms = 0.0, resolve_ms = 0.0, isect_ms = 0.0;
-    uint64_t isect_launches = 0;
+    std::vector<bool> pending_isect_coop;   // which of pending_isect are cooperative-engine launches
+    double kernel_ms = 0.0, resolve_ms = 0.0, isect_ms = 0.0, coop_ms = 0.0;
+    uint64_t isect_launches = 0, coop_launches = 0;
     uint64_t samples_done = 0;
     uint32_t deferred_spp = 0;    // wavefront engine: trace() calls not yet run (one pass at the next sync point)
     uint32_t* tile_order = nullptr;   // local tiles in Z-order of their image position (k_wcamera)
@@ -449,15 +450,20 @@ int finish_pending(pt_session* ss) {
     // diagnostics (PT_TUNE roundlog=1): per-launch ms of the rounds, one line per sync
     const bool log = tune_int("roundlog", 0) == 1 && !ss->pending_isect.empty();
     if (log) fprintf(stderr, "rounds_ms");
-    for (auto& e : ss->pending_isect) {
+    for (size_t i = 0; i < ss->pending_isect.size(); ++i) {
+        const auto& e = ss->pending_isect[i];
         float ms = 0.f;
-        if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) ss->isect_ms += ms;
+        if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) {
+            ss->isect_ms += ms;
+            if (i < ss->pending_isect_coop.size() && ss->pending_isect_coop[i]) ss->coop_ms += ms;
+        }
         if (log) fprintf(stderr, " %.3f", ms);
         (void)hipEventDestroy(e.first);
         (void)hipEventDestroy(e.second);
     }
     if (log) fprintf(stderr, "\n");
     ss->pending_isect.clear();
+    ss->pending_isect_coop.clear();
     return PT_OK;
 }
 
@@ -896,7 +902,10 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 HIP_TRY(hipEventCreate(&i0));
                 HIP_TRY(hipEventCreate(&i1));
                 ss->pending_isect.emplace_back(i0, i1);
+                ss->pending_isect_coop.resize(ss->pending_isect.size(), false);
+                ss->pending_isect_coop.back() = true;
                 ss->isect_launches++;
+                ss->coop_launches++;
                 const uint32_t per_wg = QC_WAVES * (64u / team);   // chains per workgroup
                 const uint32_t grid = std::max(1u, std::min(ss->coop_grid, (chains + per_wg - 1u) / per_wg));
                 const bool cprof = tune_has("cprof");   // -DPT_CPROF builds: per-phase cycles on stderr
@@ -1141,10 +1150,10 @@ int pt_session_stats(pt_session* ss, pt_stats* st) {
     if (!ss || !st) return fail(PT_E_INVALID, "null argument");
     int rc = pt_session_sync(ss);
     if (rc) return rc;
-    unsigned long long cc[PT_CTR_COPIES * PT_CTR_STRIDE], c[8] = {0};
+    unsigned long long cc[PT_CTR_COPIES * PT_CTR_STRIDE], c[PT_CTR_STRIDE] = {0};
     HIP_TRY(hipMemcpy(cc, ss->counters, sizeof(cc), hipMemcpyDeviceToHost));
     for (uint32_t x = 0; x < PT_CTR_COPIES; ++x)
-        for (uint32_t k = 0; k < 8; ++k) c[k] += cc[PT_CTR_STRIDE * x + k];
+        for (uint32_t k = 0; k < PT_CTR_STRIDE; ++k) c[k] += cc[PT_CTR_STRIDE * x + k];
     memset(st, 0, sizeof(*st));
     st->rays = c[0];
     st->node_visits = c[1];
@@ -1166,6 +1175,12 @@ int pt_session_stats(pt_session* ss, pt_stats* st) {
     st->isect_ms = ss->isect_ms;
     st->isect_launches = ss->isect_launches;
     st->rounds = ss->rounds;
+    st->coop_rays = c[8];
+    st->coop_node_visits = c[9];
+    st->coop_prim_tests = c[10];
+    st->coop_aux_visits = c[13];
+    st->coop_ms = ss->coop_ms;
+    st->coop_launches = ss->coop_launches;
     return PT_OK;
 }
 
@@ -1410,6 +1425,9 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
         agg.fallbacks_ray += st.fallbacks_ray;
         agg.isect_ms = std::max(agg.isect_ms, st.isect_ms);
         agg.isect_launches += st.isect_launches;
+        agg.coop_rays += st.coop_rays; agg.coop_node_visits += st.coop_node_visits;
+        agg.coop_prim_tests += st.coop_prim_tests; agg.coop_aux_visits += st.coop_aux_visits;
+        agg.coop_ms = std::max(agg.coop_ms, st.coop_ms); agg.coop_launches += st.coop_launches;
         agg.rounds += st.rounds; agg.aux_bytes = st.aux_bytes;
         agg.kernel_ms = std::max(agg.kernel_ms, st.kernel_ms);
         agg.resolve_ms = std::max(agg.resolve_ms, st.resolve_ms);

@@ -26,7 +26,7 @@ TRAVERSAL_REPLAY = 0
 TRAVERSAL_EXACT = 1
 TRAVERSAL_REPLAY_DIV = 2
 GATHER_AUTO, GATHER_RCCL, GATHER_HOST = 0, 1, 2
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # One HIP runtime per process: PyTorch bundles its own libamdhip64 (soname
 # libamdhip64.so.7, but its users link the unversioned name), so loading
@@ -64,7 +64,9 @@ class Stats(C.Structure):
                 ("kernel_ms", C.c_double), ("resolve_ms", C.c_double), ("wall_ms", C.c_double),
                 ("node_bytes", C.c_uint64), ("prim_bytes", C.c_uint64), ("aux_bytes", C.c_uint64),
                 ("fallbacks_ray", C.c_uint64), ("isect_ms", C.c_double), ("isect_launches", C.c_uint64),
-                ("rounds", C.c_uint64), ("gather_rccl", C.c_uint64)]
+                ("rounds", C.c_uint64), ("gather_rccl", C.c_uint64),
+                ("coop_rays", C.c_uint64), ("coop_node_visits", C.c_uint64), ("coop_prim_tests", C.c_uint64),
+                ("coop_aux_visits", C.c_uint64), ("coop_ms", C.c_double), ("coop_launches", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -50,7 +50,9 @@ def main():
                 rec = {"world": w, "rank": r, "tiles": ss.n_tiles, "spp_per_step": spp, "mray_s": rays / dt / 1e6,
                        "ms_per_step": dt * 1e3 / a.steps, "rounds_per_step": rounds / a.steps,
                        "rays_per_round": rays / max(rounds, 1),
-                       "isect_ms_per_round": (st1["isect_ms"] - st0["isect_ms"]) / max(rounds, 1)}
+                       "isect_ms_per_round": (st1["isect_ms"] - st0["isect_ms"]) / max(rounds, 1),
+                       "coop_ms_per_step": (st1["coop_ms"] - st0["coop_ms"]) / a.steps,
+                       "coop_ray_share": (st1["coop_rays"] - st0["coop_rays"]) / max(rays, 1)}
                 out.append(rec)
                 print(json.dumps(rec), flush=True)
                 ss.close()
