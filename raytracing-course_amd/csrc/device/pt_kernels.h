@@ -128,7 +128,7 @@ struct WaveParams {
 #define QC_WAVES 4u
 #endif
 #define QC_SCAP_MIN 128u           // aux stack words per team (the smallest; also the exact DFS stack)
-#define QC_FOLD 8u                 // fold records held in LDS per chain (RAY_DEPTH <= QC_FOLD, host-checked)
+#define QC_FOLD 6u                 // fold records held in LDS per chain (RAY_DEPTH <= QC_FOLD, host-checked)
 #define QC_NPL 8u                  // plane records copied to LDS per workgroup (n_planes <= QC_NPL, host-checked)
 #define QC_NEM 8u                  // emitter records copied to LDS per workgroup (n_emitters <= QC_NEM)
 #define QC_TOPN 21u                // aux BVH nodes 0..20 (BFS order: the top three levels) copied to LDS

@@ -816,11 +816,13 @@ struct QcTeamLds {
     static constexpr uint32_t SCAP = T == 64u ? 448u : T == 32u ? 192u : QC_SCAP_MIN;   // aux stack (also the
                                                                                       // leader's exact DFS stack)
     static constexpr uint32_t CCAP = 5u * T;                    // candidates (< T + 4 T at any time)
-    static constexpr uint32_t HCAP = T == 64u ? 32u : T;        // hitting leaves per query (more: exact DFS)
+    static constexpr uint32_t HCAP = T >= 32u ? 32u : T == 16u ? 16u : 12u;   // hitting leaves per query (more: the
+                                                                              // exact DFS); LDS fits 3 WGs per CU
     uint32_t stk[SCAP];
     uint32_t cand[CCAP];
     uint32_t hl[QH_N][HCAP];       // hitting leaves: index, first-min t, its prim, hit normal and side,
-                                   // ancestor-list info (sorted into preorder in place)
+                                   // ancestor-list info
+    uint32_t perm[HCAP];           // their preorder: perm[k] = the entry of the k-th smallest index
     uint32_t r_idx[HCAP], r_t[HCAP];   // entered hits so far (preorder)
     Shade fold_sh[QC_FOLD];        // the chain's fold records: the vertex prim's shading record ...
     uint4 fold[QC_FOLD];           // ... and {idm, s1, s2, -}
@@ -886,7 +888,6 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
                        int pid, F4 pre, uint32_t reserve, QCounts& C, bool& exact, Hit& hit, bool& bvh QC_CP_ARG) {
     QC_T0();
     constexpr uint32_t SCAP = QcTeamLds<T>::SCAP, HCAP = QcTeamLds<T>::HCAP;
-    static_assert(HCAP <= T, "one hitting leaf per team lane when sorting");
     const uint32_t lane = lane_id(), tl = lane % T, tbase = lane - tl;
     const unsigned long long tmask = T == 64u ? ~0ull : (((1ull << T) - 1ull) << tbase);
     const uint32_t slim = SCAP - reserve;
@@ -993,23 +994,16 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
     QC_TICK(0);
     if (ovf) exact = true;
     const bool dec = run && !ovf;
-    // 3. the hitting leaves in reference preorder (distinct indices: rank = count below),
-    //    sorted in place (every lane reads its entry before any lane writes)
-    {
-        const bool srt = dec && nh > 1u;
-        if (__ballot(srt) != 0ull) {
-            const bool act = srt && tl < nh;
-            uint32_t e[QH_N];
-#pragma unroll
-            for (uint32_t f = 0; f < QH_N; ++f) e[f] = act ? L.hl[f][tl] : 0u;
-            uint32_t rank = 0u;
-            for (uint32_t j = 0; __ballot(srt && j < nh) != 0ull; ++j)
-                if (srt && j < nh) rank += L.hl[QH_IDX][j] < e[QH_IDX] ? 1u : 0u;
-            if (act) {
-#pragma unroll
-                for (uint32_t f = 0; f < QH_N; ++f) L.hl[f][rank] = e[f];
-            }
-        }
+    // 3. the hitting leaves in reference preorder (distinct indices: rank = count below)
+    for (uint32_t i0 = 0;; i0 += T) {
+        const bool srt = dec && i0 < nh;
+        if (__ballot(srt) == 0ull) break;
+        const bool act = srt && i0 + tl < nh;
+        const uint32_t c = act ? L.hl[QH_IDX][i0 + tl] : 0u;
+        uint32_t rank = 0u;
+        for (uint32_t j = 0; __ballot(srt && j < nh) != 0ull; ++j)
+            if (srt && j < nh) rank += L.hl[QH_IDX][j] < c ? 1u : 0u;
+        if (act) L.perm[rank] = i0 + tl;
     }
     // 4. decide them in order: lane j of the team holds nodes j, j + T, ... of the
     //    leaf's root path with their exact slab results (the reference's division form)
@@ -1021,7 +1015,8 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
     for (uint32_t kk = 0;; ++kk) {
         const bool dk = dec && kk < nh;
         if (__ballot(dk) == 0ull) break;
-        const uint32_t info = dk ? L.hl[QH_INFO][kk] : 0u;
+        const uint32_t ke = dk ? L.perm[kk] : 0u;   // the kk-th hitting leaf in preorder
+        const uint32_t info = dk ? L.hl[QH_INFO][ke] : 0u;
         const uint32_t off = info & 0x03ffffffu, len = dk ? info >> 26 : 0u;
         float carry = P;          // the bound at the previous block's last node
         uint32_t vlast = 0u;      // that node
@@ -1082,17 +1077,17 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
         }
         if (dk && !fail) {
             // 5. entered: record; first strict minimum; replaces the plane iff closer
-            const float lt = u2f(L.hl[QH_T][kk]);
+            const float lt = u2f(L.hl[QH_T][ke]);
             if (tl == 0u) {
-                L.r_idx[nrec] = L.hl[QH_IDX][kk];
+                L.r_idx[nrec] = L.hl[QH_IDX][ke];
                 L.r_t[nrec] = f2u(lt);
             }
             ++nrec;
             if (lt < bt) {
                 bt = lt;
                 if (lt < P) {
-                    res = (int)L.hl[QH_LID][kk];
-                    resk = (int)kk;
+                    res = (int)L.hl[QH_LID][ke];
+                    resk = (int)ke;
                 }
             }
         }
