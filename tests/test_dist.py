@@ -2,6 +2,8 @@
 framebuffer gather (the N>1 data path; on the GPU box the same code runs
 over RCCL).  Tiles are 16x16, tile t belongs to rank t % world
 (include/pt.h sessions, bench.py gather_tiles)."""
+import importlib.util
+import json
 import os
 import socket
 
@@ -124,3 +126,28 @@ def test_bench_refuses_mismatched_world():
     rc, out, err = _bench(["--gpus", "2", "--probe-ranks"], {"WORLD_SIZE": "1", "RANK": "0"})
     assert rc == 2 and out is None
     assert "refusing" in err
+
+
+def test_bench_roofline_counts_the_path_engine_alone(tmp_path):
+    """bench.py's k_wpath roofline subtracts the cooperative engine's share
+    (pt_stats coop_* fields) from the visit counts, time and launches, and
+    scales the profiled traffic ratio by the path engine's own bytes."""
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    keys = ("isect_launches", "isect_ms", "node_visits", "prim_tests", "aux_visits", "rays", "coop_launches",
+            "coop_ms", "coop_node_visits", "coop_prim_tests", "coop_aux_visits", "coop_rays")
+    st0 = dict.fromkeys(keys, 0)
+    st0.update(node_bytes=32, prim_bytes=48, aux_bytes=128)
+    st1 = dict(st0, isect_launches=6, isect_ms=110.0, node_visits=1000, prim_tests=400, aux_visits=2000, rays=500,
+               coop_launches=1, coop_ms=10.0, coop_node_visits=100, coop_prim_tests=40, coop_aux_visits=200,
+               coop_rays=50)
+    tj = tmp_path / "traffic.json"
+    tj.write_text(json.dumps({"k": {"traffic_per_alg_byte": 1.5, "profile": "p"}}))
+    r = bench.roofline(st0, st1, str(tj), "k")
+    alg = (900 * 32 + 360 * 48 + 1800 * 128) / 5.0
+    assert r["launches"] == 5 and abs(r["launch_ms"] - 20.0) < 1e-9
+    assert abs(r["alg_bytes_per_launch"] - alg) < 1e-6
+    assert abs(r["achieved"] - alg / 0.020 / 1e9) < 1e-9
+    assert abs(r["traffic"] - 1.5 * alg) < 1e-6 and abs(r["rays_share"] - 0.9) < 1e-12
+    assert r["coop"]["launches"] == 1 and r["coop"]["rays"] == 50
