@@ -210,7 +210,7 @@ struct SceneView {
     // the query's single fetch space: every array above that the wavefront query
     // reads lives in one 16-B-aligned blob, addressed by 32-bit byte offsets
     const F4* blob;
-    uint32_t o_nodes, o_aux, o_ainfo, o_anc, o_qprim, o_prim;
+    uint32_t o_nodes, o_aux, o_ainfo, o_anc, o_qprim, o_prim, o_bundle;
     uint32_t aux_rshift;        // wide aux entries: leaf range packed >> aux_rshift (pt_query.h)
 };
 

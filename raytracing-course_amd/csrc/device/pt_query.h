@@ -14,33 +14,34 @@
 // offsets), so lanes in different phases share one round trip per step
 // instead of serialising one per phase and one per guarded load.
 //
-//   * auxiliary BVH: 4-wide, nodes of 4 x 32-B entries (one step); internal
-//     entries are conservative inflated boxes, leaf entries carry the
-//     reference leaf's exact (center, half-size), tested with node_enter();
-//     pending nodes on a per-lane LDS stack.
-//   * candidates: the PT_QK smallest reference-leaf indices of the pass,
-//     sorted in registers (min/max insertion network); more -> further passes
-//     above the last processed index.
-//   * replay per candidate: its leaf record (certain accept / certain reject),
-//     else its ancestor list below the LCA with the last hit, 4 entries then
-//     their 4 records per step; entered leaves test one primitive per step.
-// Rays with non-finite components or more than PT_REPLAY_HITS replay hits take the exact stack
-// DFS (bvh_exact) in a separate pass.
+//   * auxiliary BVH: 4-wide, nodes of 4 x 32-B entries (one step), conservative
+//     inflated boxes; pending items (aux nodes and candidate leaves) on a
+//     per-lane LDS stack.
+//   * probe: each candidate leaf the aux pass meets is probed at once -- its
+//     bundle (node record + first primitive, one step), then any further
+//     primitives, one per step: the first strict minimum over its primitives,
+//     which does not depend on any bound.  Only leaves with a primitive hit can
+//     change the result or a bound (src/bvh.cpp:205-223), so only they join the
+//     hitting-leaf list (PT_QHK, sorted by reference index = preorder; more ->
+//     another pass above the last decided leaf).
+//   * decision per hitting leaf, in preorder: its leaf record (certain accept /
+//     certain reject), else its ancestor list below the LCA with the last
+//     recorded hit, 4 entries then their 4 records per step.
+// Rays with non-finite components, or a list full of entered hits with another
+// hit to add, take the exact stack DFS (bvh_exact) in a separate pass.
 #pragma once
 #include "pt_trace.h"
 
 namespace pt {
 
-#ifndef PT_QK
-#define PT_QK 16
-#endif
 #ifndef PT_AUXW
 #define PT_AUXW 4               // auxiliary BVH width (nodes = PT_AUXW AuxSL entries)
 #endif
 
-// wide aux entry (AuxSL, 32 B): a = {lo.xyz, hi.x}, b = {hi.y, hi.z, leaf range, code}
-//   leaf range = (max reference leaf of the subtree >> S, rounded up) << 16 | (min >> S)
+// wide aux entry (AuxSL, 32 B): a = {lo.xyz, hi.x}, b = {hi.y, hi.z, range, code}
+//   internal entry: range = (max reference leaf of the subtree >> S, rounded up) << 16 | (min >> S)
 //   (S = SceneView::aux_rshift; annotate_aux_ranges in host/aux_bvh.cpp)
+//   leaf entry (code = 0x80000000 | reference leaf): range = the leaf's ordinal (its bundle)
 // stackless auxiliary node (32 B):
 //   internal: a = {lo.x, lo.y, lo.z, hi.x}, b = {hi.y, hi.z, u32 skip, 0xffffffff}
 //   leaf:     a = {c.x, c.y, c.z, s.x},     b = {s.y, s.z, u32 skip (= own index + 1), u32 reference leaf}
@@ -50,7 +51,8 @@ struct AuxSL { F4 a, b; };
 
 enum : uint32_t { Q_AUX = 0u, Q_REPLAY = 1u, Q_DONE = 2u, Q_EXACT = 3u };
 // replay step kinds: each issues one round of independent loads
-enum : uint32_t { R_CAND = 0u, R_LEAF = 1u, R_WALK_E = 2u, R_WALK_N = 3u };
+enum : uint32_t { R_CAND = 0u, R_WALK_E = 1u, R_WALK_N = 2u };
+#define PT_RKINDS 3u
 
 // compact primitive records of the query (48 B, blob section o_qprim, same index
 // as the full 80-B records):
@@ -80,46 +82,56 @@ PT_HD Prim qprim_expand(const F4& r0, const F4& r1, const F4& r2) {
     return P;
 }
 
-struct QHits {                  // replay hit list (reference leaf index, leaf first-min t)
-    uint32_t idx[PT_REPLAY_HITS];
-    float t[PT_REPLAY_HITS];
-};
+// leaf bundle (80 B, blob section o_bundle, one per reference leaf in preorder =
+// the leaf's "ordinal", carried in its wide aux entry's b.z): the leaf's node
+// record {c.xyz, s.x}, {s.y, s.z, first prim, prim count}, then the compact
+// record of its first primitive, whose spare last word holds the leaf's node index.
+#define PT_BUNDLE_BYTES 80u
+#define PT_LEAFQ 0x80000000u    // Q_AUX item: a candidate leaf to probe (| its ordinal)
+
+#ifndef PT_QHK
+#define PT_QHK 8                // hitting-leaf list: entered hits of earlier passes + this pass's undecided ones
+#endif
 
 struct Query {
     Ray ray;
     f3 inv;                     // 1/d (IEEE, once per ray)
     float P;                    // closest plane t (the BVH bound at the root)
-    // small state packed into one register
+    // small state packed into two registers
     uint32_t phase : 2;         // Q_*
-    uint32_t walk : 2;          // Q_REPLAY step kind: R_CAND, R_LEAF, R_WALK_E, R_WALK_N
+    uint32_t walk : 2;          // Q_REPLAY step kind: R_CAND, R_WALK_E, R_WALK_N
     uint32_t par : 1;           // near-zero direction component: exact node tests, robust aux boxes
     uint32_t robust : 1;        // leaf check: the ray crosses the leaf box robustly (t1c, mc valid)
     uint32_t known : 1;         // walk: the segment bound is known (below the LCA with the last hit)
-    uint32_t overflow : 1;      // aux pass dropped candidates above the kept PT_QK
-    uint32_t nh : 3;            // recorded replay hits (<= PT_REPLAY_HITS)
-    uint32_t sp : 7;            // Q_AUX: pending aux nodes on the per-lane stack
+    uint32_t overflow : 1;      // this pass dropped hitting leaves above the list's largest one
+    uint32_t sp : 7;            // Q_AUX: pending aux items on the per-lane stack
     uint32_t pos : 7;           // walk: position reached in the ancestor list
     uint32_t len : 7;           // walk: ancestor list length
-    uint32_t node;              // Q_AUX: aux node
-    uint32_t lb;                // every candidate below lb has been processed
-    uint32_t cand, skip, last;
+    uint32_t nh : 4;            // hitting leaves in the list (<= PT_QHK)
+    uint32_t ne : 4;            // ... of which the first ne are decided and entered (the recorded hits)
+    uint32_t spare : 24;        // (fills the word: a narrower unit is accessed bytewise, which keeps
+                                //  the whole Query out of registers)
+    uint32_t node;              // Q_AUX: aux node, or PT_LEAFQ | ordinal of the leaf being probed
+    uint32_t lb;                // every hitting leaf below lb has been decided
+    uint32_t cand;              // probe: its leaf; Q_REPLAY: the hitting leaf being decided (hidx[ne])
     float bound;
     float dl;                   // certification margin (t units, see q_leaf_certain)
-    uint32_t lref, lcnt;        // the candidate leaf's primitive range
-    uint32_t li;                // R_LEAF: primitives tested so far (bit 31: next fetch = full record)
-    float lt;                   // R_LEAF: leaf first-min t so far
-    int lid;                    // R_LEAF: its primitive (-1 none)
+    uint32_t lref, lcnt;        // probe: the leaf's primitive range
+    uint32_t li;                // probe: primitives tested (bit 31: next fetch = full record)
+    float lt;                   // probe: leaf first-min t so far
+    int lid;                    // probe: its primitive (-1 none)
     uint32_t off;               // walk: ancestor list offset
     uint32_t e[4];              // walk: the entries under test (0xffffffff = none)
     uint32_t astar;             // walk: deepest ancestor at or above that LCA seen so far
     float t1c, mc;              // leaf check: approximate entry and certification margin
-    uint32_t c[PT_QK];          // sorted candidates of this pass (0xffffffff = empty)
-    QHits H;
+    uint32_t hidx[PT_QHK];      // hitting leaves (reference index, sorted; 0xffffffff = empty)
+    float ht[PT_QHK];           // ... their first-min t
+    int hid[PT_QHK];            // ... and its primitive
     float bt;                   // best BVH leaf hit so far (first strict minimum)
     float res_t;                // result so far (plane, then BVH hits that beat it): t and prim;
     int res_id;                 // the normal is recomputed from the prim by the consumer
 };
-static_assert(PT_REPLAY_HITS < 8, "nh is a 3-bit field");
+static_assert(PT_QHK < 16, "nh and ne are 4-bit fields");
 #define PT_QUERY_SP_MAX 127u    // Query::sp is a 7-bit field: pt_scene_prepare rejects deeper aux stacks
 
 struct QCounts {
@@ -190,12 +202,14 @@ PT_HD void q_init_pre(const Ray& ray, float P, int pid, F4 pre, Query& q) {
     q.P = P;
     q.bt = PT_INF;
     q.nh = 0;
+    q.ne = 0;
     q.lb = 0;
     q.overflow = 0;
     q.node = 0;
     q.sp = 0;
+    q.li = 0;
 #pragma unroll
-    for (int i = 0; i < PT_QK; ++i) q.c[i] = 0xffffffffu;
+    for (int i = 0; i < PT_QHK; ++i) q.hidx[i] = 0xffffffffu;
     q.inv = mk3(pre.x, pre.y, pre.z);
     q.par = signbit(pre.w) ? 1u : 0u;
     q.dl = fabsf(pre.w);
@@ -206,72 +220,100 @@ PT_HD void q_init(const SceneView& S, const Ray& ray, float P, int pid, Query& q
     q_init_pre(ray, P, pid, q_prep(S, ray), q);
 }
 
-PT_HD void q_insert(Query& q, uint32_t v) {
+// hidx[k] / ht[k] / hid[k] for a lane-varying k < PT_QHK: an unrolled select
+// chain.  Its default is not an element, so the optimiser cannot fold the chain
+// into a dynamically indexed load (which would keep the whole Query in scratch).
+template <class T>
+PT_HD T q_sel(const T (&a)[PT_QHK], uint32_t k, T dflt) {
+    T v = dflt;
 #pragma unroll
-    for (int i = 0; i < PT_QK; ++i) {
-        const uint32_t lo = q.c[i] < v ? q.c[i] : v;
-        v = q.c[i] < v ? v : q.c[i];
-        q.c[i] = lo;
-    }
-    if (v != 0xffffffffu) q.overflow = 1u;   // a candidate above the kept PT_QK was dropped
-}
-
-PT_HD uint32_t q_pop(Query& q) {
-    const uint32_t v = q.c[0];
-#pragma unroll
-    for (int i = 0; i + 1 < PT_QK; ++i) q.c[i] = q.c[i + 1];
-    q.c[PT_QK - 1] = 0xffffffffu;
+    for (int i = 0; i < PT_QHK; ++i)
+        if ((uint32_t)i == k) v = a[i];
     return v;
 }
 
-// next candidate (>= skip), or end of pass (-> next pass / done).  The pass's
-// candidates are distinct (each reference leaf has one aux leaf entry), inserted
-// only if >= lb (= skip at the pass end) and popped in ascending order after
-// skip = cand + 1: the smallest one left is always >= skip.
-PT_HD void q_next_candidate(Query& q) {
-    const uint32_t v = q_pop(q);
-    if (v != 0xffffffffu) {
-        q.last = v;
-        q.cand = v;
-        q.walk = R_CAND;
-        q.phase = Q_REPLAY;
-        return;
+// A probed leaf with a primitive hit joins the list, sorted by reference index.
+// Entered hits of earlier passes lie below lb <= c, so they never move; with
+// the list full the largest entry (undecided: it is above c >= lb) or c itself
+// drops out and another pass follows.  Returns false when every slot holds an
+// entered hit (the exact DFS takes the ray).
+PT_HD bool q_add_hit(Query& q, uint32_t c, float t, int id) {
+    if (q.ne == PT_QHK) return false;
+#pragma unroll
+    for (int k = 0; k < PT_QHK; ++k) {
+        const bool sw = q.hidx[k] > c;   // empty slots hold 0xffffffff
+        const uint32_t xi = q.hidx[k];
+        const float xt = q.ht[k];
+        const int xd = q.hid[k];
+        if (sw) {
+            q.hidx[k] = c; q.ht[k] = t; q.hid[k] = id;
+            c = xi; t = xt; id = xd;
+        }
     }
+    if (c != 0xffffffffu) q.overflow = 1u;   // a hitting leaf above the kept ones dropped out
+    else q.nh = q.nh + 1u;
+    return true;
+}
+
+// every hitting leaf of the pass is decided: another pass above lb, or done
+PT_HD void q_pass_done(Query& q) {
     if (q.overflow) {
-        // candidates above the last processed one were dropped: another aux pass
-        q.lb = q.skip > q.last + 1u ? q.skip : q.last + 1u;
+        if (q.ne == PT_QHK) {
+            q.phase = Q_EXACT;
+            return;
+        }
         q.overflow = 0;
         q.node = 0;
         q.sp = 0;
+        q.li = 0;
         q.phase = Q_AUX;
         return;
     }
     q.phase = Q_DONE;
 }
 
-// leaf finished: record its first-min hit (src/bvh.cpp:205-213 + the replay
-// hit list); returns false when the hit list is full (exact DFS instead)
-PT_HD bool q_leaf_done(Query& q) {
-    if (q.lid >= 0) {
-        if (q.nh == PT_REPLAY_HITS) return false;
-#pragma unroll
-        for (int k = 0; k < PT_REPLAY_HITS; ++k)
-            if ((uint32_t)k == q.nh) { q.H.idx[k] = q.cand; q.H.t[k] = q.lt; }
-        ++q.nh;
-        // BVH result = first strict minimum; it replaces the plane hit iff strictly closer
-        if (q.lt < q.bt) {
-            q.bt = q.lt;
-            if (q.lt < q.P) { q.res_t = q.lt; q.res_id = q.lid; }
-        }
+// decide the next undecided hitting leaf, if any
+PT_HD void q_next_decision(Query& q) {
+    if (q.ne < q.nh) {
+        q.cand = q_sel(q.hidx, q.ne, 0xffffffffu);
+        q.walk = R_CAND;
+        q.phase = Q_REPLAY;
+        return;
     }
-    return true;
+    q_pass_done(q);
 }
 
-PT_HD void q_enter_leaf(Query& q) {
-    q.walk = R_LEAF;
-    q.li = 0u;
-    q.lt = PT_INF;
-    q.lid = -1;
+// hitting leaf hidx[ne] is entered: it becomes a recorded hit
+// (src/bvh.cpp:205-213 + the recursion's fold: the BVH result is the first
+// strict minimum over entered hits in preorder; it replaces the plane hit iff
+// strictly closer, src/scene.cpp:68-74)
+PT_HD void q_entered(Query& q) {
+    const float t = q_sel(q.ht, q.ne, PT_INF);
+    const int id = q_sel(q.hid, q.ne, -1);
+    if (t < q.bt) {
+        q.bt = t;
+        if (t < q.P) { q.res_t = t; q.res_id = id; }
+    }
+    q.ne = q.ne + 1u;
+    q.lb = q.cand + 1u;
+    q_next_decision(q);
+}
+
+// hitting leaf hidx[ne] is not entered: it leaves the list (an unentered leaf
+// changes neither the result nor any bound)
+PT_HD void q_rejected(Query& q) {
+#pragma unroll
+    for (int k = 0; k + 1 < PT_QHK; ++k) {
+        if ((uint32_t)k >= q.ne) {
+            q.hidx[k] = q.hidx[k + 1];
+            q.ht[k] = q.ht[k + 1];
+            q.hid[k] = q.hid[k + 1];
+        }
+    }
+    q.hidx[PT_QHK - 1] = 0xffffffffu;
+    q.nh = q.nh - 1u;
+    q.lb = q.cand + 1u;
+    q_next_decision(q);
 }
 
 // min of the recorded hits strictly inside (a, r) (the left subtree of a when
@@ -280,16 +322,16 @@ PT_HD float q_bound_between(const Query& q, uint32_t a, uint32_t r) {
     float m = q.P;
     bool any = false;
 #pragma unroll
-    for (int k = 0; k < PT_REPLAY_HITS; ++k) {
-        if ((uint32_t)k < q.nh && q.H.idx[k] > a && q.H.idx[k] < r) {
-            if (!any || q.H.t[k] < m) m = q.H.t[k];
+    for (int k = 0; k < PT_QHK; ++k) {
+        if ((uint32_t)k < q.ne && q.hidx[k] > a && q.hidx[k] < r) {
+            if (!any || q.ht[k] < m) m = q.ht[k];
             any = true;
         }
     }
     return m;
 }
 
-// Candidate leaf check before any root-path replay.  Every bound the replay
+// Hitting-leaf check before any root-path replay.  Every bound the replay
 // can carry is P or a minimum over earlier hits, so it lies in [lo, hi] =
 // [min, max](P, recorded hits).
 //  * certain accept: the ray crosses the leaf box robustly (slab interval
@@ -308,8 +350,8 @@ PT_HD float q_bound_between(const Query& q, uint32_t a, uint32_t r) {
 PT_HD uint32_t q_leaf_certain(Query& q, const Node& nd) {
     float lo = q.P, hi = q.P;
 #pragma unroll
-    for (int k = 0; k < PT_REPLAY_HITS; ++k)
-        if ((uint32_t)k < q.nh) { lo = fminf(lo, q.H.t[k]); hi = fmaxf(hi, q.H.t[k]); }
+    for (int k = 0; k < PT_QHK; ++k)
+        if ((uint32_t)k < q.ne) { lo = fminf(lo, q.ht[k]); hi = fmaxf(hi, q.ht[k]); }
     const f3 c = mk3(nd.a.x, nd.a.y, nd.a.z);
     const f3 s = mk3(nd.a.w, nd.b.x, nd.b.y);
     const f3 o = q.ray.o + -1.f * c;
@@ -335,28 +377,29 @@ PT_HD uint32_t q_leaf_certain(Query& q, const Node& nd) {
 
 // byte offsets (into S.blob) of the 8 pieces this lane's next step reads
 PT_HD void q_addr(const SceneView& S, const Query& q, uint32_t off[8]) {
-    if (q.phase == Q_AUX) {
-        const uint32_t b = S.o_aux + q.node * (uint32_t)(PT_AUXW * sizeof(AuxSL));
-#pragma unroll
-        for (int k = 0; k < 8; ++k) off[k] = b + 16u * (uint32_t)k;
-        return;
-    }
     uint32_t b0, b1, b2;
-    if (q.walk == R_CAND) {
-        b0 = S.o_nodes + 32u * q.cand;
-        b1 = b0 + 16u;
-        b2 = S.o_ainfo + 16u * (q.cand >> 2);     // the 16 B holding anc_info[cand]
-    } else if (q.walk == R_LEAF) {
-        const uint32_t i = q.lref + (q.li & 0x7fffffffu);
-        if (q.li & 0x80000000u) {
-            b0 = S.o_prim + 80u * i;              // full record: 5 pieces
+    if (q.phase == Q_AUX) {
+        if (!(q.node & PT_LEAFQ)) {
+            const uint32_t b = S.o_aux + q.node * (uint32_t)(PT_AUXW * sizeof(AuxSL));
+#pragma unroll
+            for (int k = 0; k < 8; ++k) off[k] = b + 16u * (uint32_t)k;
+            return;
+        }
+        if (q.li == 0u || (q.li & 0x80000000u)) {
+            // the leaf's bundle (record + first primitive), or a full primitive record: 5 pieces
+            b0 = q.li == 0u ? S.o_bundle + PT_BUNDLE_BYTES * (q.node & 0x7fffffffu)
+                            : S.o_prim + 80u * (q.lref + (q.li & 0x7fffffffu));
 #pragma unroll
             for (int k = 0; k < 8; ++k) off[k] = b0 + 16u * (uint32_t)(k < 5 ? k : 4);
             return;
         }
-        b0 = S.o_qprim + 48u * i;
+        b0 = S.o_qprim + 48u * (q.lref + q.li);   // the leaf's next compact primitive
         b1 = b0 + 16u;
         b2 = b0 + 32u;
+    } else if (q.walk == R_CAND) {
+        b0 = S.o_nodes + 32u * q.cand;
+        b1 = b0 + 16u;
+        b2 = S.o_ainfo + 16u * (q.cand >> 2);     // the 16 B holding anc_info[cand]
     } else if (q.walk == R_WALK_E) {
         b0 = S.o_anc + 4u * (q.off + q.pos);      // 4 entries (lists padded to 16 B)
         b1 = b0;
@@ -376,9 +419,21 @@ PT_HD void q_addr(const SceneView& S, const Query& q, uint32_t off[8]) {
     for (int k = 3; k < 8; ++k) off[k] = b0;
 }
 
+// Q_AUX: the next item of the aux pass (top of the lane's stack), or the end
+// of the pass: its hitting leaves are decided next
+template <class Mem>
+PT_HD void q_aux_next(Query& q, Mem& stk, uint32_t next) {
+    if (next == 0xffffffffu && q.sp > 0u) next = stk.get(--q.sp);
+    if (next != 0xffffffffu) {
+        q.node = next;
+        return;
+    }
+    q_next_decision(q);
+}
+
 template <class Mem>
 PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r[8]) {
-    if (q.phase == Q_AUX) {
+    if (q.phase == Q_AUX && !(q.node & PT_LEAFQ)) {
         // one wide node: PT_AUXW child entries
         C.aux++;
         const f3 oinv = mk3(q.ray.o.x * q.inv.x, q.ray.o.y * q.inv.y, q.ray.o.z * q.inv.z);
@@ -398,92 +453,74 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
             }
         }
         uint32_t next = 0xffffffffu;
-        // the largest kept candidate when the list is full (else none)
-        const uint32_t cmax = q.c[PT_QK - 1];
+        // the largest listed hitting leaf when the list is full (else none): a leaf
+        // above it could only join the list to drop out again
+        const uint32_t hmax = q.hidx[PT_QHK - 1];
 #pragma unroll
         for (int k = 0; k < PT_AUXW; ++k) {
             // every entry's box is conservative: a reference leaf passing it is a
-            // candidate (its exact slab test runs in the candidate step -- a leaf
-            // failing that test is never entered, src/bvh.cpp:188-198)
+            // candidate, probed next (its own slab test is decided only if one of
+            // its primitives is hit: a leaf failing it is never entered,
+            // src/bvh.cpp:188-198)
             const uint32_t code = f2u(r[2 * k + 1].w);
+            const uint32_t rng = f2u(r[2 * k + 1].z);   // leaf: its ordinal; internal: its leaf range
             const bool h = hit[k] && code != 0xffffffffu;
-            const bool leaf = h && (code & 0x80000000u) != 0u && (code & 0x7fffffffu) >= q.lb;
-            // a subtree is skipped when all its leaves lie below lb (processed in an
-            // earlier pass), or above the largest kept candidate of a full list: it
-            // could only add candidates the list would drop, so another pass follows
-            const uint32_t rng = f2u(r[2 * k + 1].z);
-            const bool above = cmax != 0xffffffffu && ((rng & 0xffffu) << S.aux_rshift) > cmax;
-            const bool inner = h && (code & 0x80000000u) == 0u && ((rng >> 16) << S.aux_rshift) >= q.lb && !above;
-            if (h && (code & 0x80000000u) == 0u && above) q.overflow = 1u;
-            if (pt_any(leaf)) {
-#ifdef PT_QDIAG
-                if (leaf) C.cands++;
-#endif
-                if (leaf) q_insert(q, code & 0x7fffffffu);
-            }
-            const bool push = inner && next != 0xffffffffu;
-            if (inner && next == 0xffffffffu) next = code;
-            if (push) stk.set(q.sp++, code);
-        }
-        if (next == 0xffffffffu && q.sp > 0u) next = stk.get(--q.sp);
-        if (next != 0xffffffffu) {
-            q.node = next;
-            return;
+            const bool isleaf = (code & 0x80000000u) != 0u;
+            const uint32_t lidx = code & 0x7fffffffu;
+            // a subtree is skipped when all its leaves lie below lb (decided in an
+            // earlier pass), or above the largest listed hitting leaf of a full
+            // list: it could only add hits the list would drop, so another pass follows
+            const bool above = isleaf ? lidx > hmax
+                                      : (hmax != 0xffffffffu && ((rng & 0xffffu) << S.aux_rshift) > hmax);
+            const bool fresh = isleaf ? lidx >= q.lb : ((rng >> 16) << S.aux_rshift) >= q.lb;
+            if (h && fresh && above) q.overflow = 1u;
+            const bool take = h && fresh && !above;
+            const uint32_t item = isleaf ? (PT_LEAFQ | rng) : code;
+            const bool push = take && next != 0xffffffffu;
+            if (take && next == 0xffffffffu) next = item;
+            if (push) stk.set(q.sp++, item);
         }
 #ifdef PT_QDIAG
-        C.passes++;
+        if (next == 0xffffffffu && q.sp == 0u) C.passes++;
 #endif
-        // aux pass complete: replay the candidates in reference preorder
-        q.skip = q.lb;
-        q_next_candidate(q);
+        q_aux_next(q, stk, next);
         return;
     }
-    bool reject = false;
-    if (q.walk == R_CAND) {
-        // the candidate's own leaf record (+ where its ancestor list is)
-        Node nd;
-        nd.a = r[0];
-        nd.b = r[1];
-        const uint32_t k4 = q.cand & 3u;
-        const uint32_t info = f2u(k4 == 0u ? r[2].x : k4 == 1u ? r[2].y : k4 == 2u ? r[2].z : r[2].w);
-        C.nodes++;
-        q.lref = f2u(nd.b.z);
-        q.lcnt = f2u(nd.b.w);
-        const uint32_t v = q_leaf_certain(q, nd);
-        if (v == 1u) {
-            q_enter_leaf(q);
-            return;
-        }
-        if (v == 0u) {
-            reject = true;
-        } else {
-            // undecided: test the root path below a* = LCA(last recorded hit, cand).
-            // Ancestors at or above a* were entered on that hit's path (same
-            // node, same bound: both depend only on earlier hits) -- they are the
-            // list entries <= the hit.  Below a* no left subtree holds a hit, so
-            // the bound is constant: B = min{hits in (a*, right child of a*)}.
-            // Each remaining ancestor, then the leaf itself (the list's last
-            // entry), is tested with B.
-            q.off = info & 0x03ffffffu;
-            q.len = info >> 26;
-            q.pos = 0u;
-            q.known = q.nh == 0u ? 1u : 0u;   // no earlier hit: the bound is P on the whole path
-            q.bound = q.P;
-            q.astar = 0u;
-            q.walk = R_WALK_E;
-            return;
-        }
-    } else if (q.walk == R_LEAF) {
-        // one primitive of the entered leaf (src/bvh.cpp:205-213: first strict min)
+    if (q.phase == Q_AUX) {
+        // probe a candidate leaf: the first strict minimum over its primitives
+        // (src/bvh.cpp:205-213), independent of any bound
         Hit h;
-        bool ok;
-        if (q.li & 0x80000000u) {
+        bool ok = false;
+        if (q.li == 0u) {
+            // its bundle: the node record (primitive range) and its first primitive
+            q.lref = f2u(r[1].z);
+            q.lcnt = f2u(r[1].w);
+            q.cand = f2u(r[4].w);
+            q.lt = PT_INF;
+            q.lid = -1;
+            C.nodes++;
+#ifdef PT_QDIAG
+            C.cands++;
+#endif
+            if (q.lcnt == 0u) {
+                q_aux_next(q, stk, 0xffffffffu);
+                return;
+            }
+            if (f2u(r[2].w) & PT_QP_FULL) {
+                q.li = 0x80000000u;               // not representable compactly: full record next step
+                return;
+            }
+            ok = f2u(r[2].w) == T_TRIANGLE
+                     ? isect_triangle(q.ray, mk3(r[2].x, r[2].y, r[2].z), mk3(r[3].x, r[3].y, r[3].z),
+                                      mk3(r[3].w, r[4].x, r[4].y), h)
+                     : bvh_prim_intersect(qprim_expand(r[2], r[3], r[4]), q.ray, h);
+        } else if (q.li & 0x80000000u) {
             Prim pr;
             pr.p0 = r[0]; pr.p1 = r[1]; pr.p2 = r[2]; pr.p3 = r[3]; pr.p4 = r[4];
             q.li &= 0x7fffffffu;
             ok = bvh_prim_intersect(pr, q.ray, h);
         } else if (f2u(r[0].w) & PT_QP_FULL) {
-            q.li |= 0x80000000u;              // not representable compactly: full record next step
+            q.li |= 0x80000000u;
             return;
         } else if (f2u(r[0].w) == T_TRIANGLE) {
             // plain triangle (pos = +0, identity rotation): the world->local rotation
@@ -498,17 +535,53 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
         }
         C.ptests++;
         if (ok && h.t < q.lt) { q.lt = h.t; q.lid = (int)(q.lref + q.li); }
-        if (++q.li < q.lcnt) return;
-        if (!q_leaf_done(q)) {
+        q.li = q.li + 1u;
+        if (q.li < q.lcnt) return;
+        q.li = 0u;
+        if (q.lid >= 0 && !q_add_hit(q, q.cand, q.lt, q.lid)) {
             q.phase = Q_EXACT;
             return;
         }
-    } else if (q.walk == R_WALK_E) {
+        q_aux_next(q, stk, 0xffffffffu);
+        return;
+    }
+    // Q_REPLAY: is hitting leaf hidx[ne] (= cand) entered?
+    if (q.walk == R_CAND) {
+        // its own leaf record (+ where its ancestor list is)
+        Node nd;
+        nd.a = r[0];
+        nd.b = r[1];
+        const uint32_t k4 = q.cand & 3u;
+        const uint32_t info = f2u(k4 == 0u ? r[2].x : k4 == 1u ? r[2].y : k4 == 2u ? r[2].z : r[2].w);
+        C.nodes++;
+        const uint32_t v = q_leaf_certain(q, nd);
+        if (v == 1u) {
+            q_entered(q);
+            return;
+        }
+        if (v == 0u) {
+            q_rejected(q);
+            return;
+        }
+        // undecided: test the root path below a* = LCA(last recorded hit, cand).
+        // Ancestors at or above a* were entered on that hit's path (same
+        // node, same bound: both depend only on earlier hits) -- they are the
+        // list entries <= the hit.  Below a* no left subtree holds a hit, so
+        // the bound is constant: B = min{hits in (a*, right child of a*)}.
+        // Each remaining ancestor, then the leaf itself (the list's last
+        // entry), is tested with B.
+        q.off = info & 0x03ffffffu;
+        q.len = info >> 26;
+        q.pos = 0u;
+        q.known = q.ne == 0u ? 1u : 0u;   // no earlier hit: the bound is P on the whole path
+        q.bound = q.P;
+        q.astar = 0u;
+        q.walk = R_WALK_E;
+        return;
+    }
+    if (q.walk == R_WALK_E) {
         // next 4 list entries (ancestors, then the leaf; 0xffffffff = padding)
-        uint32_t hlast = 0u;   // last recorded hit (unrolled select: no dynamic register indexing)
-#pragma unroll
-        for (int k = 0; k < PT_REPLAY_HITS; ++k)
-            if ((uint32_t)k + 1u == q.nh) hlast = q.H.idx[k];
+        const uint32_t hlast = q_sel(q.hidx, q.ne - 1u, 0u);   // last recorded hit (none: 0)
         bool any = false, accept = false;
         const uint32_t ent[4] = {f2u(r[0].x), f2u(r[0].y), f2u(r[0].z), f2u(r[0].w)};
 #pragma unroll
@@ -529,33 +602,31 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
             any = any || e != 0xffffffffu;
         }
         if (accept) {
-            q_enter_leaf(q);
+            q_entered(q);
             return;
         }
         if (any) q.walk = R_WALK_N;
         else q.pos += 4u;                // all at or above a*
         return;
-    } else {
-        // R_WALK_N: the records of the pending entries, tested with B
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (q.e[j] == 0xffffffffu) continue;
-            Node nd;
-            nd.a = r[2 * j];
-            nd.b = r[2 * j + 1];
-            C.nodes++;
-            if (!node_enter(nd, q.ray, q.inv, q.bound, q.par != 0u)) reject = true;
-        }
-        if (!reject) {
-            q.pos += 4u;
-            if (q.pos >= q.len) q_enter_leaf(q);   // the leaf (last entry) was entered too
-            else q.walk = R_WALK_E;
-            return;
-        }
     }
-    (void)reject;
-    q.skip = q.cand + 1u;
-    q_next_candidate(q);
+    // R_WALK_N: the records of the pending entries, tested with B
+    bool reject = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (q.e[j] == 0xffffffffu) continue;
+        Node nd;
+        nd.a = r[2 * j];
+        nd.b = r[2 * j + 1];
+        C.nodes++;
+        if (!node_enter(nd, q.ray, q.inv, q.bound, q.par != 0u)) reject = true;
+    }
+    if (reject) {
+        q_rejected(q);
+        return;
+    }
+    q.pos += 4u;
+    if (q.pos >= q.len) q_entered(q);   // the leaf (last entry) was entered too
+    else q.walk = R_WALK_E;
 }
 
 PT_HD F4 blob_piece(const SceneView& S, uint32_t off) {

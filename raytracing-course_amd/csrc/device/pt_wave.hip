@@ -505,12 +505,12 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
             const uint32_t kind = active && q.phase == Q_REPLAY ? 1u + q.walk : active && q.phase == Q_AUX ? 0u : 7u;
             uint32_t present = 0u;
 #pragma unroll
-            for (uint32_t k = 1; k <= 4u; ++k)
+            for (uint32_t k = 1; k <= PT_RKINDS; ++k)
                 if (__ballot(kind == k) != 0ull) present |= 1u << k;
             uint32_t pick = 0u, pick2 = 0u;
 #pragma unroll
-            for (uint32_t j = 1; j <= 4u; ++j) {
-                const uint32_t c = (rr + j - 1u) % 4u + 1u;
+            for (uint32_t j = 1; j <= PT_RKINDS; ++j) {
+                const uint32_t c = (rr + j - 1u) % PT_RKINDS + 1u;
                 if ((present >> c) & 1u) {
                     if (pick == 0u) pick = c;
                     else if (PT_PVOTE_K > 1 && pick2 == 0u) pick2 = c;
@@ -846,7 +846,7 @@ struct EmitLds {
 // bvh_prim_intersect from the compact record (pt_query.h): a plain triangle (pos = +0,
 // rotation exactly (0,0,0,1)) is tested on the world ray -- the world->local transform
 // changes at most the sign of zero components, which changes neither the decision nor
-// t, nor the sign of dn that picks the normal's side (pt_query.h R_LEAF) -- and its
+// t, nor the sign of dn that picks the normal's side (pt_query.h probe) -- and its
 // normal goes through the same last step, normalize(qrot(rotation, n)), so the Hit
 // has the full test's bits; other records expand to the full form.
 __device__ __forceinline__ bool qc_prim_hit(const SceneView& S, uint32_t i, const Ray& ray, Hit& h) {

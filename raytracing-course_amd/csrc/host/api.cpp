@@ -164,7 +164,7 @@ struct pt_scene {
     float box_extent = 0.f;     // max |coordinate| of the reference node boxes
     std::vector<uint32_t> anc_info, anc;   // per-leaf ancestor lists (replay walk)
     std::vector<pt::F4> blob;   // the wavefront query's fetch space (pt_core.h SceneView::blob)
-    uint32_t o_nodes = 0, o_aux = 0, o_ainfo = 0, o_anc = 0, o_qprim = 0, o_prim = 0;
+    uint32_t o_nodes = 0, o_aux = 0, o_ainfo = 0, o_anc = 0, o_qprim = 0, o_prim = 0, o_bundle = 0;
     uint32_t auxw_stack = 0;    // per-lane stack words of the wide aux traversal
     uint32_t aux_rshift = 0;    // leaf-range packing of the wide aux entries (annotate_aux_ranges)
     float thr[256];
@@ -309,8 +309,21 @@ void build_query_blob(pt_scene* s) {
         if (bytes) memcpy(&b[o / 16], p, bytes);
         return o;
     };
+    // leaf ordinals (reference leaves in preorder): each wide aux leaf entry
+    // carries its leaf's ordinal in b.z, the index of the leaf's bundle
+    std::vector<uint32_t> ordinal(s->dnodes.size(), 0xFFFFFFFFu), leaves;
+    for (uint32_t i = 0; i < (uint32_t)s->dnodes.size(); ++i)
+        if (!(pt::f2u(s->dnodes[i].b.w) & 0x80000000u)) { ordinal[i] = (uint32_t)leaves.size(); leaves.push_back(i); }
+    std::vector<pt::AuxSL> aux = s->auxsl;
+    for (pt::AuxSL& e : aux) {
+        const uint32_t code = pt::f2u(e.b.w);
+        if (code == 0xFFFFFFFFu || !(code & 0x80000000u)) continue;
+        const uint32_t o = ordinal.at(code & 0x7FFFFFFFu);
+        if (o == 0xFFFFFFFFu) throw std::runtime_error("aux leaf entry names an internal node");
+        e.b.z = pt::u2f(o);
+    }
     s->o_nodes = append(s->dnodes.data(), s->dnodes.size() * sizeof(pt::Node));
-    s->o_aux = append(s->auxsl.data(), s->auxsl.size() * sizeof(pt::AuxSL));
+    s->o_aux = append(aux.data(), aux.size() * sizeof(pt::AuxSL));
     s->o_ainfo = append(s->anc_info.data(), s->anc_info.size() * 4);
     s->o_anc = append(s->anc.data(), s->anc.size() * 4);
     std::vector<pt::F4> qp(3 * s->dprims.size());
@@ -335,6 +348,22 @@ void build_query_blob(pt_scene* s) {
         }
     }
     s->o_qprim = append(qp.data(), qp.size() * sizeof(pt::F4));
+    // leaf bundles (pt_query.h): node record + the compact record of the first
+    // primitive, the leaf's node index in its spare last word
+    std::vector<pt::F4> bu(5 * leaves.size());
+    for (size_t k = 0; k < leaves.size(); ++k) {
+        const pt::Node& n = s->dnodes[leaves[k]];
+        pt::F4* r = &bu[5 * k];
+        r[0] = n.a;
+        r[1] = n.b;
+        const uint32_t first = pt::f2u(n.b.z), cnt = pt::f2u(n.b.w);
+        if (cnt) {
+            if (first >= s->dprims.size()) throw std::runtime_error("leaf primitive out of range");
+            r[2] = qp[3 * first]; r[3] = qp[3 * first + 1]; r[4] = qp[3 * first + 2];
+        }
+        r[4].w = pt::u2f(leaves[k]);
+    }
+    s->o_bundle = append(bu.data(), bu.size() * sizeof(pt::F4));
     s->o_prim = append(s->dprims.data(), s->dprims.size() * sizeof(pt::Prim));
     if (b.size() * 16 >= 0xFFFFFFF0ull) throw std::runtime_error("scene too large for 32-bit query offsets");
 }
@@ -402,7 +431,7 @@ uint32_t lane_words(const pt_scene* s, int traversal) {
 void set_blob(pt::SceneView& v, const pt_scene* s, const pt::F4* blob) {
     v.blob = blob;
     v.o_nodes = s->o_nodes; v.o_aux = s->o_aux; v.o_ainfo = s->o_ainfo;
-    v.o_anc = s->o_anc; v.o_qprim = s->o_qprim; v.o_prim = s->o_prim;
+    v.o_anc = s->o_anc; v.o_qprim = s->o_qprim; v.o_prim = s->o_prim; v.o_bundle = s->o_bundle;
     v.aux_rshift = s->aux_rshift;
 }
 

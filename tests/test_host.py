@@ -166,8 +166,10 @@ def test_device_integrator_on_host_bit_exact(name, trav):
 def test_coop_query_matches_reference_kat(name, monkeypatch):
     """The cooperative engine's query algorithm (pt_coop.h qc_run: every candidate
     leaf's bound-free result first, then only the hitting leaves' root paths with
-    the carried bounds), run on the host: the reference's closest hits, fewer node
-    records than the replay state machine."""
+    the carried bounds), run on the host: the reference's closest hits.  The path
+    engine's query probes the same candidates but decides a hitting leaf from its
+    record or the part of its root path below the LCA with the last hit, so it
+    reads no more node records than the whole root paths."""
     t = M["trav"][name]
     rays, ((ids, f, inter), _) = U.read_trav(name)
     with pt.Scene.load(U.scene_path(t["scene"])) as s:
@@ -179,7 +181,7 @@ def test_coop_query_matches_reference_kat(name, monkeypatch):
     hit = ids != -1
     assert np.array_equal(ghits[hit, :4].view(np.uint32), f[hit].view(np.uint32))
     assert np.array_equal(ghits[hit, 4].astype(np.uint32), inter[hit])
-    assert ctr["nodes"] < rctr["nodes"]
+    assert rctr["nodes"] <= ctr["nodes"]
 
 
 @pytest.mark.parametrize("name", HOST_RENDER[:6])
