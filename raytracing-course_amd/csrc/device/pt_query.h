@@ -90,7 +90,7 @@ PT_HD Prim qprim_expand(const F4& r0, const F4& r1, const F4& r2) {
 #define PT_LEAFQ 0x80000000u    // Q_AUX item: a candidate leaf to probe (| its ordinal)
 
 #ifndef PT_QHK
-#define PT_QHK 8                // hitting-leaf list: entered hits of earlier passes + this pass's undecided ones
+#define PT_QHK 6                // hitting-leaf list: entered hits of earlier passes + this pass's undecided ones
 #endif
 
 struct Query {

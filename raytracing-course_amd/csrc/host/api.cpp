@@ -775,9 +775,10 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // wave per chain) to the end of the pass; it needs a wave's aux stack to hold
         // a depth-first descent below its expansion limit, and lane 0's exact DFS stack
         const uint32_t cus = (uint32_t)std::max(1, pr.multiProcessorCount);
-        // 131,072 on the 256-CU part (rank-of-8 sweep, teams of 8: 65 k 1,245-1,261, 131 k 1,280,
-        // 200 k 1,199, 300 k 789 Mray/s per GPU)
-        ss->coop_max = cus * 512u;
+        // 98,304 on the 256-CU part (with the probe-first query, rank-of-8 per GPU, teams of 8:
+        // 32 k 1,620, 48 k 1,653, 65 k 1,649, 98 k 1,644, 131 k 1,580-1,587, 262 k 794 Mray/s;
+        // rank-of-2 / -4 best at 98 k)
+        ss->coop_max = cus * 384u;
         ss->coop_max = (uint32_t)std::max(0, tune_int("coop", (int)ss->coop_max));
         ss->coop_grid = cus * 8u;
         // chains left when the first (narrow-team) launch hands over to whole-wave teams; off:
