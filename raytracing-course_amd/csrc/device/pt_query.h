@@ -82,11 +82,10 @@ PT_HD Prim qprim_expand(const F4& r0, const F4& r1, const F4& r2) {
     return P;
 }
 
-// leaf bundle (80 B, blob section o_bundle, one per reference leaf in preorder =
-// the leaf's "ordinal", carried in its wide aux entry's b.z): the leaf's node
-// record {c.xyz, s.x}, {s.y, s.z, first prim, prim count}, then the compact
-// record of its first primitive, whose spare last word holds the leaf's node index.
-#define PT_BUNDLE_BYTES 80u
+// leaf bundle (64 B, blob section o_bundle, one per reference leaf in preorder =
+// the leaf's "ordinal", carried in its wide aux entry's b.z): the compact record
+// of the leaf's first primitive, then {leaf node index, first prim, prim count, 0}
+#define PT_BUNDLE_BYTES 64u
 #define PT_LEAFQ 0x80000000u    // Q_AUX item: a candidate leaf to probe (| its ordinal)
 
 #ifndef PT_QHK
@@ -385,10 +384,16 @@ PT_HD void q_addr(const SceneView& S, const Query& q, uint32_t off[8]) {
             for (int k = 0; k < 8; ++k) off[k] = b + 16u * (uint32_t)k;
             return;
         }
-        if (q.li == 0u || (q.li & 0x80000000u)) {
-            // the leaf's bundle (record + first primitive), or a full primitive record: 5 pieces
-            b0 = q.li == 0u ? S.o_bundle + PT_BUNDLE_BYTES * (q.node & 0x7fffffffu)
-                            : S.o_prim + 80u * (q.lref + (q.li & 0x7fffffffu));
+        if (q.li == 0u) {
+            // the leaf's bundle (first primitive + primitive range): 4 pieces
+            b0 = S.o_bundle + PT_BUNDLE_BYTES * (q.node & 0x7fffffffu);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) off[k] = b0 + 16u * (uint32_t)(k < 4 ? k : 3);
+            return;
+        }
+        if (q.li & 0x80000000u) {
+            // a full primitive record: 5 pieces
+            b0 = S.o_prim + 80u * (q.lref + (q.li & 0x7fffffffu));
 #pragma unroll
             for (int k = 0; k < 8; ++k) off[k] = b0 + 16u * (uint32_t)(k < 5 ? k : 4);
             return;
@@ -492,13 +497,12 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
         Hit h;
         bool ok = false;
         if (q.li == 0u) {
-            // its bundle: the node record (primitive range) and its first primitive
-            q.lref = f2u(r[1].z);
-            q.lcnt = f2u(r[1].w);
-            q.cand = f2u(r[4].w);
+            // its bundle: its first primitive and the primitive range
+            q.cand = f2u(r[3].x);
+            q.lref = f2u(r[3].y);
+            q.lcnt = f2u(r[3].z);
             q.lt = PT_INF;
             q.lid = -1;
-            C.nodes++;
 #ifdef PT_QDIAG
             C.cands++;
 #endif
@@ -506,14 +510,14 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
                 q_aux_next(q, stk, 0xffffffffu);
                 return;
             }
-            if (f2u(r[2].w) & PT_QP_FULL) {
+            if (f2u(r[0].w) & PT_QP_FULL) {
                 q.li = 0x80000000u;               // not representable compactly: full record next step
                 return;
             }
-            ok = f2u(r[2].w) == T_TRIANGLE
-                     ? isect_triangle(q.ray, mk3(r[2].x, r[2].y, r[2].z), mk3(r[3].x, r[3].y, r[3].z),
-                                      mk3(r[3].w, r[4].x, r[4].y), h)
-                     : bvh_prim_intersect(qprim_expand(r[2], r[3], r[4]), q.ray, h);
+            ok = f2u(r[0].w) == T_TRIANGLE
+                     ? isect_triangle(q.ray, mk3(r[0].x, r[0].y, r[0].z), mk3(r[1].x, r[1].y, r[1].z),
+                                      mk3(r[1].w, r[2].x, r[2].y), h)
+                     : bvh_prim_intersect(qprim_expand(r[0], r[1], r[2]), q.ray, h);
         } else if (q.li & 0x80000000u) {
             Prim pr;
             pr.p0 = r[0]; pr.p1 = r[1]; pr.p2 = r[2]; pr.p3 = r[3]; pr.p4 = r[4];

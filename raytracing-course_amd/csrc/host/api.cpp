@@ -348,20 +348,18 @@ void build_query_blob(pt_scene* s) {
         }
     }
     s->o_qprim = append(qp.data(), qp.size() * sizeof(pt::F4));
-    // leaf bundles (pt_query.h): node record + the compact record of the first
-    // primitive, the leaf's node index in its spare last word
-    std::vector<pt::F4> bu(5 * leaves.size());
+    // leaf bundles (pt_query.h): the compact record of the leaf's first primitive,
+    // then {leaf node index, first primitive, primitive count, 0}
+    std::vector<pt::F4> bu(4 * leaves.size());
     for (size_t k = 0; k < leaves.size(); ++k) {
         const pt::Node& n = s->dnodes[leaves[k]];
-        pt::F4* r = &bu[5 * k];
-        r[0] = n.a;
-        r[1] = n.b;
+        pt::F4* r = &bu[4 * k];
         const uint32_t first = pt::f2u(n.b.z), cnt = pt::f2u(n.b.w);
         if (cnt) {
             if (first >= s->dprims.size()) throw std::runtime_error("leaf primitive out of range");
-            r[2] = qp[3 * first]; r[3] = qp[3 * first + 1]; r[4] = qp[3 * first + 2];
+            r[0] = qp[3 * first]; r[1] = qp[3 * first + 1]; r[2] = qp[3 * first + 2];
         }
-        r[4].w = pt::u2f(leaves[k]);
+        r[3] = pt::F4{pt::u2f(leaves[k]), pt::u2f(first), pt::u2f(cnt), 0.f};
     }
     s->o_bundle = append(bu.data(), bu.size() * sizeof(pt::F4));
     s->o_prim = append(s->dprims.data(), s->dprims.size() * sizeof(pt::Prim));
