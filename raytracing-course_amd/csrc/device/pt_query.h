@@ -82,9 +82,10 @@ PT_HD Prim qprim_expand(const F4& r0, const F4& r1, const F4& r2) {
     return P;
 }
 
-// leaf bundle (64 B, blob section o_bundle, one per reference leaf in preorder =
-// the leaf's "ordinal", carried in its wide aux entry's b.z): the compact record
-// of the leaf's first primitive, then {leaf node index, first prim, prim count, 0}
+// leaf bundle (64 B, blob section o_bundle, one per reference leaf, numbered in
+// the order the wide aux nodes hold the leaves; the number -- the leaf's
+// "ordinal" -- is carried in its wide aux entry's b.z): the compact record of
+// the leaf's first primitive, then {leaf node index, first prim, prim count, 0}
 #define PT_BUNDLE_BYTES 64u
 #define PT_LEAFQ 0x80000000u    // Q_AUX item: a candidate leaf to probe (| its ordinal)
 

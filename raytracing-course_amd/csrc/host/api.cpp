@@ -309,18 +309,21 @@ void build_query_blob(pt_scene* s) {
         if (bytes) memcpy(&b[o / 16], p, bytes);
         return o;
     };
-    // leaf ordinals (reference leaves in preorder): each wide aux leaf entry
-    // carries its leaf's ordinal in b.z, the index of the leaf's bundle
-    std::vector<uint32_t> ordinal(s->dnodes.size(), 0xFFFFFFFFu), leaves;
-    for (uint32_t i = 0; i < (uint32_t)s->dnodes.size(); ++i)
-        if (!(pt::f2u(s->dnodes[i].b.w) & 0x80000000u)) { ordinal[i] = (uint32_t)leaves.size(); leaves.push_back(i); }
+    // leaf ordinals: each wide aux leaf entry carries in b.z the index of its leaf's
+    // bundle; bundles are numbered in the order the wide aux nodes hold the leaves,
+    // so the leaves of one aux node (spatial neighbours, often probed by the same
+    // ray) share cache lines
+    std::vector<uint32_t> leaves;
+    std::vector<uint8_t> seen(s->dnodes.size(), 0);
     std::vector<pt::AuxSL> aux = s->auxsl;
     for (pt::AuxSL& e : aux) {
         const uint32_t code = pt::f2u(e.b.w);
         if (code == 0xFFFFFFFFu || !(code & 0x80000000u)) continue;
-        const uint32_t o = ordinal.at(code & 0x7FFFFFFFu);
-        if (o == 0xFFFFFFFFu) throw std::runtime_error("aux leaf entry names an internal node");
-        e.b.z = pt::u2f(o);
+        const uint32_t leaf = code & 0x7FFFFFFFu;
+        if (leaf >= s->dnodes.size() || (pt::f2u(s->dnodes[leaf].b.w) & 0x80000000u) || seen[leaf]++)
+            throw std::runtime_error("aux leaf entry names an internal node or a leaf twice");
+        e.b.z = pt::u2f((uint32_t)leaves.size());
+        leaves.push_back(leaf);
     }
     s->o_nodes = append(s->dnodes.data(), s->dnodes.size() * sizeof(pt::Node));
     s->o_aux = append(aux.data(), aux.size() * sizeof(pt::AuxSL));
