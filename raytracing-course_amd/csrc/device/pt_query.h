@@ -38,6 +38,30 @@ namespace pt {
 #define PT_AUXW 4               // auxiliary BVH width (nodes = PT_AUXW AuxSL entries)
 #endif
 
+// Leaf entries (in the query blob) carry the box of the region where their
+// primitives can report a hit, when the host could bound it (host/api.cpp
+// leaf_hit_region: a plain triangle is only ever hit on its copy moved onto the
+// plane through the origin, and that box is widened there for the edge tests'
+// rounding); a leaf whose primitives can be hit nowhere along the ray is not a
+// candidate, whatever its own box.  The computed hit point lies within ~22u (2|o|
+// + 3X) of the ray (u = 2^-24, X = scene box extent), so the entry is widened
+// per ray by PT_LEAF_MARGIN x dl, where dl = 2^-18 (X + |o|max) / |d|min (q_prep)
+// is 64u (X + |o|) per unit of t: ~60x headroom.  Rays with a near-zero direction
+// component take every leaf entry of a visited node.
+#define PT_LEAF_MARGIN 64.f
+// the leaf entry test with the per-ray widening (dlw = the q_prep record's w:
+// dl, negative for a near-zero direction component)
+PT_HD bool aux_leaf_hit(float lx, float ly, float lz, float hx, float hy, float hz, f3 inv, f3 oinv, float dlw) {
+    const float mt = PT_LEAF_MARGIN * dlw;
+    if (!(mt >= 0.f && mt < INFINITY)) return true;
+    const float ax = fmaf(lx, inv.x, -oinv.x), bx = fmaf(hx, inv.x, -oinv.x);
+    const float ay = fmaf(ly, inv.y, -oinv.y), by = fmaf(hy, inv.y, -oinv.y);
+    const float az = fmaf(lz, inv.z, -oinv.z), bz = fmaf(hz, inv.z, -oinv.z);
+    const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    return tn - mt <= tf + mt && tf + mt >= 0.f;
+}
+
 // wide aux entry (AuxSL, 32 B): a = {lo.xyz, hi.x}, b = {hi.y, hi.z, range, code}
 //   internal entry: range = (max reference leaf of the subtree >> S, rounded up) << 16 | (min >> S)
 //   (S = SceneView::aux_rshift; annotate_aux_ranges in host/aux_bvh.cpp)
@@ -445,17 +469,30 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
         const f3 oinv = mk3(q.ray.o.x * q.inv.x, q.ray.o.y * q.inv.y, q.ray.o.z * q.inv.z);
         // all PT_AUXW slab tests first, branch-free (the robust form only when a lane
         // of the wave needs it); then the bookkeeping per entry
+        // (a leaf entry is widened by the per-ray margin mt: its box bounds where the
+        // leaf's primitives can be hit, see PT_LEAF_MARGIN)
+        const float mt = PT_LEAF_MARGIN * q.dl;
+        const bool mwide = !(mt < INFINITY);
         bool hit[PT_AUXW];
 #pragma unroll
         for (int k = 0; k < PT_AUXW; ++k) {
             const F4 ea = r[2 * k], eb = r[2 * k + 1];
-            hit[k] = aux_box(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, q.inv, oinv);
+            const float ax = fmaf(ea.x, q.inv.x, -oinv.x), bx = fmaf(ea.w, q.inv.x, -oinv.x);
+            const float ay = fmaf(ea.y, q.inv.y, -oinv.y), by = fmaf(eb.x, q.inv.y, -oinv.y);
+            const float az = fmaf(ea.z, q.inv.z, -oinv.z), bz = fmaf(eb.y, q.inv.z, -oinv.z);
+            const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+            const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+            const bool lf = (f2u(eb.w) & 0x80000000u) != 0u;   // leaf (or empty: dropped below)
+            const float m = lf ? mt : 0.f;
+            hit[k] = (lf && mwide) || (tn - m <= tf + m && tf + m >= 0.f);
         }
         if (pt_any(q.par != 0u)) {
 #pragma unroll
             for (int k = 0; k < PT_AUXW; ++k) {
                 const F4 ea = r[2 * k], eb = r[2 * k + 1];
-                if (q.par) hit[k] = aux_box_par(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, q.ray, q.inv, oinv);
+                if (q.par)
+                    hit[k] = (f2u(eb.w) & 0x80000000u) != 0u ||
+                             aux_box_par(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, q.ray, q.inv, oinv);
             }
         }
         uint32_t next = 0xffffffffu;

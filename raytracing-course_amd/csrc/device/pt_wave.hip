@@ -980,8 +980,9 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
             const F4 ea = r[2 * e], eb = r[2 * e + 1];
             const uint32_t code = f2u(eb.w);
             bool h = act && code != 0xffffffffu;
-            if (h) h = par ? aux_box_par(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, ray, inv, oinv)
-                           : aux_box(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, inv, oinv);
+            if (h) h = (code & 0x80000000u) ? aux_leaf_hit(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, inv, oinv, pre.w)
+                       : par ? aux_box_par(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, ray, inv, oinv)
+                             : aux_box(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, inv, oinv);
             const bool leaf = h && (code & 0x80000000u) != 0u;
             const bool inner = h && (code & 0x80000000u) == 0u;
             const unsigned long long mi = __ballot(inner) & tmask, ml = __ballot(leaf) & tmask;

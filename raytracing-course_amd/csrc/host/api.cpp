@@ -167,6 +167,7 @@ struct pt_scene {
     uint32_t o_nodes = 0, o_aux = 0, o_ainfo = 0, o_anc = 0, o_qprim = 0, o_prim = 0, o_bundle = 0;
     uint32_t auxw_stack = 0;    // per-lane stack words of the wide aux traversal
     uint32_t aux_rshift = 0;    // leaf-range packing of the wide aux entries (annotate_aux_ranges)
+    uint32_t n_region_leaves = 0;   // leaf entries carrying their primitives' hit region (leaf_hit_region)
     float thr[256];
     std::map<int, DevScene> dev;
     std::mutex mu;
@@ -296,12 +297,78 @@ void build_device_layout(pt_scene* s) {
     if (s->nodes.size() >= (1u << 24)) throw std::runtime_error("BVH larger than 2^24 nodes");
 }
 
+// The region where a reference leaf's primitives can report a hit, as a box for
+// its wide aux leaf entry (pt_query.h PT_LEAF_MARGIN).  IntersectTriangle hits
+// the plane through the local origin (src/primitives.cpp:156-157) and accepts a
+// point whose projection along n lies in the triangle, so a plain triangle (pos
+// = +0, identity rotation) can only be hit on T' = T - (a.n) n, the triangle
+// moved onto that plane, with n the float normal the test itself computes.
+// Rounding (u = 2^-24, X = scene box extent; derivation in DESIGN.md §2):
+//  * each edge test dot(cross(e, p - a), n) > 0 is decided within 36u |e| |p - a|,
+//    i.e. a point up to 36u |p - a| <= 144u X outside an edge may pass; at a corner
+//    of angle phi that widens the accepted region by 1/sin(phi/2): the box here is
+//    widened by 4 x 144u X / sin(phi_min/2);
+//  * the computed point p = o + t d lies within ~22u (2|o| + 3X) of the ray and of
+//    the plane: the per-ray margin the query adds (64 dl = 4096u (X + |o|) / |d|min).
+// Degenerate triangles (an angle under ~0.1 degree) and non-plain primitives keep
+// the leaf's own box, which is the candidate test of the first replay: correct,
+// just unfiltered.
+bool leaf_hit_region(const pt_scene* s, uint32_t leaf, float lo[3], float hi[3]) {
+    if (!(s->box_extent < INFINITY)) return false;
+    const pt::Node& n = s->dnodes[leaf];
+    const uint32_t first = pt::f2u(n.b.z), cnt = pt::f2u(n.b.w);
+    double l[3] = {INFINITY, INFINITY, INFINITY}, h[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t i = first; i < first + cnt; ++i) {
+        const pt::Prim& P = s->dprims.at(i);
+        const bool plain = pt::f2u(P.p0.w) == pt::T_TRIANGLE && pt::f2u(P.p0.x) == 0u && pt::f2u(P.p0.y) == 0u &&
+                           pt::f2u(P.p0.z) == 0u && pt::f2u(P.p1.x) == 0u && pt::f2u(P.p1.y) == 0u &&
+                           pt::f2u(P.p1.z) == 0u && pt::f2u(P.p1.w) == 0x3f800000u;
+        if (!plain) return false;
+        const pt::f3 a = pt::mk3(P.p2.x, P.p2.y, P.p2.z), b = pt::mk3(P.p3.x, P.p3.y, P.p3.z),
+                     c = pt::mk3(P.p3.w, P.p4.x, P.p4.y);
+        const pt::f3 nf = pt::normalize(pt::cross(b - a, c - a));   // the test's own float normal
+        if (!(std::isfinite(nf.x) && std::isfinite(nf.y) && std::isfinite(nf.z))) return false;
+        const double V[3][3] = {{a.x, a.y, a.z}, {b.x, b.y, b.z}, {c.x, c.y, c.z}};
+        double smin = 1.0;   // sin(phi/2) of the sharpest corner
+        for (int k = 0; k < 3; ++k) {
+            const double* o = V[k];
+            const double* p1 = V[(k + 1) % 3];
+            const double* p2 = V[(k + 2) % 3];
+            double uu = 0, vv = 0, uv = 0;
+            for (int j = 0; j < 3; ++j) {
+                const double u = p1[j] - o[j], v = p2[j] - o[j];
+                uu += u * u; vv += v * v; uv += u * v;
+            }
+            if (!(uu > 0 && vv > 0)) return false;
+            smin = std::min(smin, sqrt(std::max(0.0, (1.0 - uv / sqrt(uu * vv)) * 0.5)));
+        }
+        if (!(smin > 1e-3)) return false;
+        const double wid = 4.0 * 144.0 * 0x1p-24 * (double)s->box_extent / smin;
+        const double nd[3] = {nf.x, nf.y, nf.z};
+        const double d = V[0][0] * nd[0] + V[0][1] * nd[1] + V[0][2] * nd[2];
+        for (int k = 0; k < 3; ++k)
+            for (int j = 0; j < 3; ++j) {
+                const double x = V[k][j] - d * nd[j];
+                l[j] = std::min(l[j], x - wid);
+                h[j] = std::max(h[j], x + wid);
+            }
+    }
+    if (!(l[0] <= h[0])) return false;
+    for (int j = 0; j < 3; ++j) {
+        // outward to float, with the aux build's static widening
+        lo[j] = (float)(l[j] - fabs(l[j]) * 1.52587890625e-05 - 7.62939453125e-06);
+        hi[j] = (float)(h[j] + fabs(h[j]) * 1.52587890625e-05 + 7.62939453125e-06);
+    }
+    return true;
+}
+
 // one 16-B-aligned blob holding every array the wavefront query reads
 // (SceneView::blob; 32-bit byte offsets).  The compact primitive records
 // (pt_query.h qprim_expand) are built here.
 void build_query_blob(pt_scene* s) {
     std::vector<pt::F4>& b = s->blob;
     b.clear();
+    s->n_region_leaves = 0;
     auto append = [&b](const void* p, size_t bytes) {
         const uint32_t o = (uint32_t)(b.size() * 16);
         const size_t n = (bytes + 15) / 16;
@@ -324,6 +391,12 @@ void build_query_blob(pt_scene* s) {
             throw std::runtime_error("aux leaf entry names an internal node or a leaf twice");
         e.b.z = pt::u2f((uint32_t)leaves.size());
         leaves.push_back(leaf);
+        float lo[3], hi[3];
+        if (leaf_hit_region(s, leaf, lo, hi)) {
+            e.a.x = lo[0]; e.a.y = lo[1]; e.a.z = lo[2];
+            e.a.w = hi[0]; e.b.x = hi[1]; e.b.y = hi[2];
+            s->n_region_leaves++;
+        }
     }
     s->o_nodes = append(s->dnodes.data(), s->dnodes.size() * sizeof(pt::Node));
     s->o_aux = append(aux.data(), aux.size() * sizeof(pt::AuxSL));
