@@ -122,9 +122,7 @@ PT_HD int qc_run(const SceneView& S, const Ray& ray, float P, int pid, F4 pre, M
             const F4 ea = blob_piece(S, o), eb = blob_piece(S, o + 16u);
             const uint32_t code = f2u(eb.w);
             if (code == 0xffffffffu) continue;
-            const bool h = (code & 0x80000000u) ? aux_leaf_hit(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, inv, oinv, pre.w)
-                           : par ? aux_box_par(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, ray, inv, oinv)
-                                 : aux_box(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, inv, oinv);
+            const bool h = aux_entry_hit(ea, eb, ray, inv, oinv, pre.w);
             if (!h) continue;
             if (!(code & 0x80000000u)) {
                 M.set(sp++, code);

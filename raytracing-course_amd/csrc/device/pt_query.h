@@ -38,28 +38,47 @@ namespace pt {
 #define PT_AUXW 4               // auxiliary BVH width (nodes = PT_AUXW AuxSL entries)
 #endif
 
-// Leaf entries (in the query blob) carry the box of the region where their
-// primitives can report a hit, when the host could bound it (host/api.cpp
-// leaf_hit_region: a plain triangle is only ever hit on its copy moved onto the
-// plane through the origin, and that box is widened there for the edge tests'
-// rounding); a leaf whose primitives can be hit nowhere along the ray is not a
-// candidate, whatever its own box.  The computed hit point lies within ~22u (2|o|
-// + 3X) of the ray (u = 2^-24, X = scene box extent), so the entry is widened
-// per ray by PT_LEAF_MARGIN x dl, where dl = 2^-18 (X + |o|max) / |d|min (q_prep)
-// is 64u (X + |o|) per unit of t: ~60x headroom.  Rays with a near-zero direction
-// component take every leaf entry of a visited node.
+// Query-blob form of a wide aux entry (32 B, the AuxSL slot): two boxes in
+// binary16, each rounded outward, then {range, code}:
+//   w0..w2: the subtree's own box  (lo.x | lo.y << 16, lo.z | hi.x << 16, hi.y | hi.z << 16)
+//   w3..w5: the subtree's hit region (same packing; +-inf halves: unbounded)
+//   w6: internal entry -- its leaf range; leaf entry -- the leaf's bundle ordinal
+//   w7: code (internal child node, 0x80000000 | reference leaf, 0xffffffff empty)
+// A reference leaf matters only if its own box is crossed (else it is never
+// entered) AND one of its primitives is hit, which can only happen inside its
+// hit region (host/api.cpp leaf_hit_region: a plain triangle is only ever hit
+// on its copy moved onto the plane through the origin, widened there for the
+// edge tests' rounding).  A subtree holds such a leaf only if the ray crosses
+// both the union of its own boxes and the union of its hit regions, so an entry
+// is taken iff both tests pass.  The computed hit point lies within ~22u (2|o| +
+// 3X) of the ray (u = 2^-24, X = scene box extent), so the hit-region test is
+// widened per ray by PT_LEAF_MARGIN x dl, where dl = 2^-18 (X + |o|max) / |d|min
+// (q_prep) is 64u (X + |o|) per unit of t: ~60x headroom.  Rays with a
+// near-zero direction component test the own boxes only (robust form).
 #define PT_LEAF_MARGIN 64.f
-// the leaf entry test with the per-ray widening (dlw = the q_prep record's w:
-// dl, negative for a near-zero direction component)
-PT_HD bool aux_leaf_hit(float lx, float ly, float lz, float hx, float hy, float hz, f3 inv, f3 oinv, float dlw) {
+
+PT_HD float h16(uint32_t bits) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(bits & 0xffffu)); }
+
+// slab interval of the ray against a box given by its binary16 halves
+PT_HD void aux_slab16(uint32_t w0, uint32_t w1, uint32_t w2, f3 inv, f3 oinv, float& tn, float& tf) {
+    const float ax = fmaf(h16(w0), inv.x, -oinv.x), bx = fmaf(h16(w1 >> 16), inv.x, -oinv.x);
+    const float ay = fmaf(h16(w0 >> 16), inv.y, -oinv.y), by = fmaf(h16(w2), inv.y, -oinv.y);
+    const float az = fmaf(h16(w1), inv.z, -oinv.z), bz = fmaf(h16(w2 >> 16), inv.z, -oinv.z);
+    tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+}
+
+// is the entry (ea, eb) taken?  dlw = the q_prep record's w (dl; negative: a
+// near-zero direction component)
+PT_HD bool aux_entry_hit(const F4& ea, const F4& eb, const Ray& ray, f3 inv, f3 oinv, float dlw) {
+    if (signbit(dlw))
+        return aux_box_par(h16(f2u(ea.x)), h16(f2u(ea.x) >> 16), h16(f2u(ea.y)), h16(f2u(ea.y) >> 16),
+                           h16(f2u(ea.z)), h16(f2u(ea.z) >> 16), ray, inv, oinv);
+    float tn, tf, un, uf;
+    aux_slab16(f2u(ea.x), f2u(ea.y), f2u(ea.z), inv, oinv, tn, tf);
+    aux_slab16(f2u(ea.w), f2u(eb.x), f2u(eb.y), inv, oinv, un, uf);
     const float mt = PT_LEAF_MARGIN * dlw;
-    if (!(mt >= 0.f && mt < INFINITY)) return true;
-    const float ax = fmaf(lx, inv.x, -oinv.x), bx = fmaf(hx, inv.x, -oinv.x);
-    const float ay = fmaf(ly, inv.y, -oinv.y), by = fmaf(hy, inv.y, -oinv.y);
-    const float az = fmaf(lz, inv.z, -oinv.z), bz = fmaf(hz, inv.z, -oinv.z);
-    const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-    const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-    return tn - mt <= tf + mt && tf + mt >= 0.f;
+    return tn <= tf && tf >= 0.f && (!(mt < INFINITY) || (un - mt <= uf + mt && uf + mt >= 0.f));
 }
 
 // wide aux entry (AuxSL, 32 B): a = {lo.xyz, hi.x}, b = {hi.y, hi.z, range, code}
@@ -469,30 +488,26 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
         const f3 oinv = mk3(q.ray.o.x * q.inv.x, q.ray.o.y * q.inv.y, q.ray.o.z * q.inv.z);
         // all PT_AUXW slab tests first, branch-free (the robust form only when a lane
         // of the wave needs it); then the bookkeeping per entry
-        // (a leaf entry is widened by the per-ray margin mt: its box bounds where the
-        // leaf's primitives can be hit, see PT_LEAF_MARGIN)
+        // both boxes of each entry (own box, hit region: see PT_LEAF_MARGIN),
+        // branch-free; the robust own-box form only when a lane of the wave needs it
         const float mt = PT_LEAF_MARGIN * q.dl;
         const bool mwide = !(mt < INFINITY);
         bool hit[PT_AUXW];
 #pragma unroll
         for (int k = 0; k < PT_AUXW; ++k) {
             const F4 ea = r[2 * k], eb = r[2 * k + 1];
-            const float ax = fmaf(ea.x, q.inv.x, -oinv.x), bx = fmaf(ea.w, q.inv.x, -oinv.x);
-            const float ay = fmaf(ea.y, q.inv.y, -oinv.y), by = fmaf(eb.x, q.inv.y, -oinv.y);
-            const float az = fmaf(ea.z, q.inv.z, -oinv.z), bz = fmaf(eb.y, q.inv.z, -oinv.z);
-            const float tn = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
-            const float tf = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
-            const bool lf = (f2u(eb.w) & 0x80000000u) != 0u;   // leaf (or empty: dropped below)
-            const float m = lf ? mt : 0.f;
-            hit[k] = (lf && mwide) || (tn - m <= tf + m && tf + m >= 0.f);
+            float tn, tf, un, uf;
+            aux_slab16(f2u(ea.x), f2u(ea.y), f2u(ea.z), q.inv, oinv, tn, tf);
+            aux_slab16(f2u(ea.w), f2u(eb.x), f2u(eb.y), q.inv, oinv, un, uf);
+            hit[k] = tn <= tf && tf >= 0.f && (mwide || (un - mt <= uf + mt && uf + mt >= 0.f));
         }
         if (pt_any(q.par != 0u)) {
 #pragma unroll
             for (int k = 0; k < PT_AUXW; ++k) {
-                const F4 ea = r[2 * k], eb = r[2 * k + 1];
+                const F4 ea = r[2 * k];
                 if (q.par)
-                    hit[k] = (f2u(eb.w) & 0x80000000u) != 0u ||
-                             aux_box_par(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, q.ray, q.inv, oinv);
+                    hit[k] = aux_box_par(h16(f2u(ea.x)), h16(f2u(ea.x) >> 16), h16(f2u(ea.y)), h16(f2u(ea.y) >> 16),
+                                         h16(f2u(ea.z)), h16(f2u(ea.z) >> 16), q.ray, q.inv, oinv);
             }
         }
         uint32_t next = 0xffffffffu;

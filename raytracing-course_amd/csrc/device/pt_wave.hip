@@ -980,9 +980,7 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
             const F4 ea = r[2 * e], eb = r[2 * e + 1];
             const uint32_t code = f2u(eb.w);
             bool h = act && code != 0xffffffffu;
-            if (h) h = (code & 0x80000000u) ? aux_leaf_hit(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, inv, oinv, pre.w)
-                       : par ? aux_box_par(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, ray, inv, oinv)
-                             : aux_box(ea.x, ea.y, ea.z, ea.w, eb.x, eb.y, inv, oinv);
+            if (h) h = aux_entry_hit(ea, eb, ray, inv, oinv, pre.w);
             const bool leaf = h && (code & 0x80000000u) != 0u;
             const bool inner = h && (code & 0x80000000u) == 0u;
             const unsigned long long mi = __ballot(inner) & tmask, ml = __ballot(leaf) & tmask;
@@ -1173,7 +1171,7 @@ k_wcoop(WaveParams P) {
         for (uint32_t i = threadIdx.x; i < nem; i += blockDim.x)
             q[QC_NPL * 5u + i] = reinterpret_cast<const F4*>(P.S.prims + P.S.emitters[i / 5u])[i % 5u];
         for (uint32_t i = threadIdx.x; i < ntop; i += blockDim.x)
-            q[(QC_NPL + QC_NEM) * 5u + i] = reinterpret_cast<const F4*>(P.aux)[i];
+            q[(QC_NPL + QC_NEM) * 5u + i] = P.S.blob[P.S.o_aux / 16u + i];   // (the query-blob form)
         if (threadIdx.x < P.S.n_planes) Q.pl_id[threadIdx.x] = P.S.planes[threadIdx.x];
         __syncthreads();
     }

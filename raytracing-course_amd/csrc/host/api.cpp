@@ -362,6 +362,72 @@ bool leaf_hit_region(const pt_scene* s, uint32_t leaf, float lo[3], float hi[3])
     return true;
 }
 
+// binary16 bits of x rounded toward -inf (down) or +inf (up)
+uint32_t f16_out(float x, bool up) {
+    const _Float16 h = (_Float16)x;
+    uint16_t b = __builtin_bit_cast(uint16_t, h);
+    const float back = (float)h;
+    if (up ? back < x : back > x) {
+        // one step outward
+        const bool neg = (b & 0x8000u) != 0u;
+        if ((b & 0x7fffu) == 0u) b = up ? 0x0001u : 0x8001u;
+        else if (neg == up) b = (uint16_t)(b - 1u);
+        else b = (uint16_t)(b + 1u);
+    }
+    return b;
+}
+
+// The query blob's form of the wide aux entries (pt_query.h PT_LEAF_MARGIN):
+// own box and hit region, both binary16 rounded outward, then {range, code}.
+// A leaf's hit region is leaf_hit_region's box, or unbounded; an internal
+// entry's is the union over its child node's entries (children follow their
+// parent in the wide tree's numbering).
+void encode_aux_entries(pt_scene* s, std::vector<pt::AuxSL>& aux) {
+    const uint32_t W = PT_AUXW, nn = (uint32_t)(aux.size() / W);
+    std::vector<std::array<float, 6>> nodeB(nn), entB(aux.size());
+    const std::array<float, 6> unb = {-INFINITY, -INFINITY, -INFINITY, INFINITY, INFINITY, INFINITY};
+    for (uint32_t n = nn; n-- > 0;) {
+        std::array<float, 6> u = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        for (uint32_t k = 0; k < W; ++k) {
+            const pt::AuxSL& e = aux[(size_t)n * W + k];
+            const uint32_t code = pt::f2u(e.b.w);
+            if (code == 0xFFFFFFFFu) continue;
+            std::array<float, 6> b;
+            float lo[3], hi[3];
+            if (code & 0x80000000u) {
+                if (leaf_hit_region(s, code & 0x7FFFFFFFu, lo, hi)) {
+                    b = {lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]};
+                    s->n_region_leaves++;
+                } else {
+                    b = unb;
+                }
+            } else {
+                if (code <= n || code >= nn) throw std::runtime_error("aux wide tree: child before its parent");
+                b = nodeB[code];
+            }
+            entB[(size_t)n * W + k] = b;
+            for (int j = 0; j < 3; ++j) { u[j] = std::min(u[j], b[j]); u[3 + j] = std::max(u[3 + j], b[3 + j]); }
+        }
+        nodeB[n] = u;
+    }
+    for (size_t i = 0; i < aux.size(); ++i) {
+        pt::AuxSL& e = aux[i];
+        if (pt::f2u(e.b.w) == 0xFFFFFFFFu) continue;
+        const float A[6] = {e.a.x, e.a.y, e.a.z, e.a.w, e.b.x, e.b.y};
+        const std::array<float, 6>& B = entB[i];
+        uint32_t h[12];
+        for (int j = 0; j < 6; ++j) {
+            h[j] = f16_out(A[j], j >= 3);
+            h[6 + j] = f16_out(B[j], j >= 3);
+        }
+        const uint32_t range = pt::f2u(e.b.z), code = pt::f2u(e.b.w);
+        // {lo.x, lo.y}, {lo.z, hi.x}, {hi.y, hi.z} per box
+        e.a = pt::F4{pt::u2f(h[0] | h[1] << 16), pt::u2f(h[2] | h[3] << 16), pt::u2f(h[4] | h[5] << 16),
+                     pt::u2f(h[6] | h[7] << 16)};
+        e.b = pt::F4{pt::u2f(h[8] | h[9] << 16), pt::u2f(h[10] | h[11] << 16), pt::u2f(range), pt::u2f(code)};
+    }
+}
+
 // one 16-B-aligned blob holding every array the wavefront query reads
 // (SceneView::blob; 32-bit byte offsets).  The compact primitive records
 // (pt_query.h qprim_expand) are built here.
@@ -391,13 +457,8 @@ void build_query_blob(pt_scene* s) {
             throw std::runtime_error("aux leaf entry names an internal node or a leaf twice");
         e.b.z = pt::u2f((uint32_t)leaves.size());
         leaves.push_back(leaf);
-        float lo[3], hi[3];
-        if (leaf_hit_region(s, leaf, lo, hi)) {
-            e.a.x = lo[0]; e.a.y = lo[1]; e.a.z = lo[2];
-            e.a.w = hi[0]; e.b.x = hi[1]; e.b.y = hi[2];
-            s->n_region_leaves++;
-        }
     }
+    encode_aux_entries(s, aux);
     s->o_nodes = append(s->dnodes.data(), s->dnodes.size() * sizeof(pt::Node));
     s->o_aux = append(aux.data(), aux.size() * sizeof(pt::AuxSL));
     s->o_ainfo = append(s->anc_info.data(), s->anc_info.size() * 4);
