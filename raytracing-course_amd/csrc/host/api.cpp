@@ -756,7 +756,19 @@ int pt_scene_prepare(pt_scene* s) {
         for (const auto& n : s->nodes)
             for (int a = 0; a < 3; ++a) s->box_extent = std::max({s->box_extent, fabsf(n.mn[a]), fabsf(n.mx[a])});
         if (!std::isfinite(s->box_extent)) s->box_extent = INFINITY;   // certification then never succeeds
-        pth::build_aux_bvh(s->nodes, s->aux, s->aux_depth);
+        {
+            // the leaves' hit regions, for the aux build's split choice
+            std::vector<float> reg(6 * s->dnodes.size(), 1.f);
+            for (uint32_t i = 0; i < (uint32_t)s->dnodes.size(); ++i) {
+                float lo[3], hi[3];
+                if ((pt::f2u(s->dnodes[i].b.w) & 0x80000000u) || !leaf_hit_region(s, i, lo, hi)) {
+                    reg[6 * i] = 1.f; reg[6 * i + 3] = -1.f;   // none
+                    continue;
+                }
+                for (int a = 0; a < 3; ++a) { reg[6 * i + a] = lo[a]; reg[6 * i + 3 + a] = hi[a]; }
+            }
+            pth::build_aux_bvh(s->nodes, reg, s->aux, s->aux_depth);
+        }
         pth::build_aux_wide(s->aux, s->dnodes, PT_AUXW, s->auxsl, s->auxsl_depth, s->auxw_stack);
         pth::annotate_aux_ranges(s->auxsl, PT_AUXW, (uint32_t)s->dnodes.size(), s->aux_rshift);
         // Query::sp (pt_query.h) counts pending aux nodes in a 7-bit field

@@ -47,7 +47,9 @@ void parse_scene(const char* text, size_t len, HScene& S);
 void build_reference_bvh(std::vector<HPrim>& prims, uint32_t n, std::vector<HNode>& nodes);
 
 // Auxiliary BVH2 over the reference leaf boxes (aux_bvh.cpp)
-void build_aux_bvh(const std::vector<HNode>& nodes, std::vector<pt::AuxNode>& out, uint32_t& max_depth);
+// (regions: 6 floats per reference node, the leaf's hit region {lo, hi}, or lo > hi: none)
+void build_aux_bvh(const std::vector<HNode>& nodes, const std::vector<float>& regions, std::vector<pt::AuxNode>& out,
+                   uint32_t& max_depth);
 
 // Stackless preorder form of the auxiliary BVH for the wavefront query (aux_bvh.cpp)
 void build_aux_stackless(const std::vector<pt::AuxNode>& pairs, const std::vector<pt::Node>& dnodes,
