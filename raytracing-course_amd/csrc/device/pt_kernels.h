@@ -111,11 +111,17 @@ struct WaveParams {
 };
 
 // path engine geometry: PT_NQ query waves + 1 shade wave per workgroup; at most
-// PT_CMAX chains resident per workgroup (= the capacity of its two rings)
+// PT_CMAX chains resident per workgroup (= the capacity of its two rings).
+// Two query waves per shade wave since the hit-region query made the queries
+// cheaper than their shading (3 -> 2 at 4 workgroups per CU: +13 % at rank-of-1,
+// +20 % at rank-of-8; 1 query wave: -8 %)
 #ifndef PT_NQ
-#define PT_NQ 3u
+#define PT_NQ 2u
 #endif
 #define PT_PATH_WG (64u * (PT_NQ + 1u))
+#ifndef PT_PATH_WAVES_PER_EU
+#define PT_PATH_WAVES_PER_EU 3u        // k_wpath occupancy (waves per SIMD) the compiler is held to
+#endif
 #ifndef PT_CMAX
 #define PT_CMAX 512u
 #endif

@@ -247,9 +247,6 @@ struct PathRing {
     F4* dq_rd;                    //                               {d.xyz, u32 closest prim | 0xffffffff}
 };
 
-#ifndef PT_PATH_WAVES_PER_EU
-#define PT_PATH_WAVES_PER_EU 3
-#endif
 #ifndef PT_PVOTE
 #define PT_PVOTE 1                 // one replay step kind per trip, round-robin over the kinds present
 #endif

@@ -907,9 +907,11 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         if (hipGetDeviceProperties(&pr, ss->dev) != hipSuccess) return cleanup(fail(PT_E_HIP, "device query failed"));
         ss->shade_grid = std::min<uint32_t>((uint32_t)std::max(1, pr.multiProcessorCount) * 8u,
                                             std::max(1u, ss->n_tiles_local));
-        // path engine: PT_NQ query waves + 1 shade wave per workgroup, 3 workgroups per CU
+        // path engine: PT_NQ query waves + 1 shade wave per workgroup, as many workgroups
+        // per CU as its waves-per-SIMD occupancy holds (4 SIMDs per CU)
         ss->path_budget = (uint32_t)std::max(1, tune_int("budget", (int)ss->path_budget));
-        ss->path_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * (uint32_t)std::max(1, tune_int("wg_per_cu", 3));
+        const int wg_cu = std::max(1, (int)(PT_PATH_WAVES_PER_EU * 4u / (PT_NQ + 1u)));
+        ss->path_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * (uint32_t)std::max(1, tune_int("wg_per_cu", wg_cu));
         // a round whose chains are this few runs them to the end of the pass (a few
         // per query wave: rebalancing them costs more rounds than it saves)
         ss->path_runend = ss->path_grid * PT_NQ * 4u;

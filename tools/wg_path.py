@@ -6,6 +6,7 @@ import sys
 import numpy as np
 
 G = int(sys.argv[2])
+NQ = int(sys.argv[3]) if len(sys.argv) > 3 else 2   # query waves per workgroup (PT_NQ)
 a = np.fromfile(sys.argv[1], np.uint64).reshape(-1, G, 32).astype(np.int64)
 tot = a.sum(axis=(0, 1))
 span = []
@@ -17,13 +18,13 @@ span = np.array(span)
 print("rounds %d, span us mean %.0f p50 %.0f max %.0f, total ms %.1f" % (len(span), span.mean(), np.median(span), span.max(), span.sum() / 1e3))
 qw_wave_trips = tot[2]
 print("QW: trips/wave-round %.0f, lane util %.3f, sleep frac %.3f, ring takes %d, rays(lane0) %d, rays per wave-trip %.3f"
-      % (qw_wave_trips / max(len(span) * G * 3, 1), tot[3] / max(64 * tot[2], 1), tot[4] / max(tot[2], 1), tot[5], tot[6], tot[6] / max(tot[2], 1)))
-print("SW: batches %d, items/batch %.1f, spins/batch %.2f, busy cycles/batch %.0f, SW busy frac of span %.3f"
+      % (qw_wave_trips / max(len(span) * G * NQ, 1), tot[3] / max(64 * tot[2], 1), tot[4] / max(tot[2], 1), tot[5], tot[6], tot[6] / max(tot[2], 1)))
+print("SW: batches %d, items/batch %.1f, spins/batch %.2f, busy cycles/batch %.0f, SW busy frac of span %.3f (shader clocks / 24 per 100-MHz tick)"
       % (tot[7], tot[8] / max(tot[7], 1), tot[9] / max(tot[7], 1), tot[10] / max(tot[7], 1),
-         tot[10] / 100.0 / max(span.sum() * G, 1)))
+         tot[10] / 24.0 / 100.0 / max(span.sum() * G, 1)))
 print("QW trip samples: mean resident %.1f, done-ring %.1f, ray-ring %.1f; chains pulled per WG-round %.1f; waves ending on the budget %.3f"
       % (tot[13] / max(tot[2], 1), tot[14] / max(tot[2], 1), tot[15] / max(tot[2], 1), tot[11] / max(len(span) * G, 1),
-         tot[12] / max(len(span) * G * 3, 1)))
+         tot[12] / max(len(span) * G * NQ, 1)))
 print("QW cycles per trip %.0f (refill part %.0f); query latency %.0f cycles over %.1f trips (%d queries)"
       % (tot[16] / max(tot[2], 1), tot[21] / max(tot[2], 1), tot[17] / max(tot[18], 1), tot[19] / max(tot[18], 1), tot[18]))
 print("QW cycles per trip: refill %.0f, step %.0f, done %.0f; trips with aux lanes %.3f, with a replay kind %.3f; lanes stepped per trip %.1f"
