@@ -30,3 +30,5 @@ print("QW cycles per trip %.0f (refill part %.0f); query latency %.0f cycles ove
 print("QW cycles per trip: refill %.0f, step %.0f, done %.0f; trips with aux lanes %.3f, with a replay kind %.3f; lanes stepped per trip %.1f"
       % (tot[21] / max(tot[2], 1), tot[22] / max(tot[2], 1), tot[26] / max(tot[2], 1), tot[23] / max(tot[2], 1),
          tot[24] / max(tot[2], 1), tot[25] / max(tot[2], 1)))
+print("SW cycles per batch: shade_item %.0f, next-ray push + publish %.0f, the rest (ring reads, fences) %.0f"
+      % (tot[27] / max(tot[7], 1), tot[28] / max(tot[7], 1), (tot[10] - tot[27] - tot[28]) / max(tot[7], 1)))
