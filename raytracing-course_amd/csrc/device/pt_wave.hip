@@ -626,7 +626,7 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
     for (uint32_t w = 0; w < PT_NQ; ++w) head[w] = 0u;
     uint32_t tail = 0u;               // ray ring published
 #ifdef PT_WPROF
-    uint64_t pf_batches = 0, pf_items = 0, pf_spin = 0, pf_cyc = 0;
+    uint64_t pf_batches = 0, pf_items = 0, pf_spin = 0, pf_cyc = 0, pf_shc = 0, pf_pushc = 0;
 #endif
     uint32_t prog = 0u;               // finished samples not yet added to P.progress
     bool waiting = false;             // holding back a small batch (since wait_t0)
@@ -696,6 +696,9 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
         Ray ray;
         uint32_t slot = 0u;
         bool emit = false, sdone = false;
+#ifdef PT_WPROF
+        const uint64_t c1 = __builtin_amdgcn_s_memtime();
+#endif
         if (have) {
             const F4 o = G.dq_ro[j], d = G.dq_rd[j];
             slot = f2u(o.w);
@@ -703,6 +706,10 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
             ray.d = mk3(d.x, d.y, d.z);
             emit = shade_item(P, slot, ray, f2u(d.w), sdone);
         }
+#ifdef PT_WPROF
+        const uint64_t c2 = __builtin_amdgcn_s_memtime();
+        pf_shc += c2 - c1;
+#endif
         // finished samples for the host's progress bar: a system-scope add per ~4 k
         prog += (uint32_t)__popcll(__ballot(sdone));
         if (P.progress && prog >= 4096u) {
@@ -728,7 +735,9 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
         }
         if (lane == 0u && gone) atomicSub(&L.resident, gone);
 #ifdef PT_WPROF
-        pf_cyc += __builtin_amdgcn_s_memtime() - c0;
+        const uint64_t c3 = __builtin_amdgcn_s_memtime();
+        pf_pushc += c3 - c2;
+        pf_cyc += c3 - c0;
 #endif
     }
 #ifdef PT_WPROF
@@ -738,6 +747,8 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
         w[8] = pf_items;
         w[9] = pf_spin;
         w[10] = pf_cyc;
+        w[27] = pf_shc;
+        w[28] = pf_pushc;
 
         w[1] = __builtin_amdgcn_s_memrealtime();
     }
