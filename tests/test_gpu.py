@@ -310,3 +310,30 @@ def test_cli_rccl_gather_config1(pt, tmp_path):
     assert r.returncode == 0, r.stderr
     assert "gather_rccl=1" in r.stderr, r.stderr
     assert U.md5(out.read_bytes()) == M["full"]["c1"]["md5"]
+
+
+@pytest.mark.parametrize("engine", ["path", "coop8", "coop64"])
+def test_many_hitting_leaves_vs_oracle(pt, tmp_path, engine, monkeypatch):
+    """A stack of tilted triangles whose hit regions (their copies on the plane
+    through the origin) overlap: camera and bounce rays have dozens of hitting
+    leaves, so the path engine's query runs overflow passes and hands rays to the
+    exact DFS; every engine must give the oracle's bytes and ray count."""
+    import test_host as H
+    text = H._stack_scene().replace("DIMENSIONS 8 8", "DIMENSIONS 40 32").replace("SAMPLES 1", "SAMPLES 4")
+    text = text.replace("RAY_DEPTH 1", "RAY_DEPTH 3")
+    text += "NEW_PRIMITIVE\nPLANE 0 0 1\nPOSITION 0 0 -1\nCOLOR 0.7 0.7 0.7\n"
+    text += "NEW_PRIMITIVE\nBOX 0.5 0.5 0.5\nPOSITION 0 0 8\nEMISSION 4 4 4\n"
+    p = tmp_path / "stack.txt"
+    p.write_text(text)
+    o = U.OracleScene(str(p))
+    orgb, orad, octr = o.render()
+    coop = engine.startswith("coop")
+    monkeypatch.setenv("PT_TUNE", "coop=%s,coop_team=%s" % ("100000000" if coop else "0", engine[4:] if coop else "64"))
+    with pt.Scene.load(str(p)) as s:
+        rgb, rad, st = s.render(radiance=True, traversal=0)
+    assert st["errors"] == 0
+    assert rad.view(np.uint32).tolist() == orad.view(np.uint32).tolist()
+    assert np.array_equal(rgb, orgb)
+    assert st["rays"] == octr["rays"]
+    if not coop:
+        assert st["fallbacks"] > 0

@@ -238,3 +238,52 @@ def test_device_init_without_gpu_fails_loudly():
     if U.gpu_available():
         pytest.skip("GPU present")
     assert pt._lib.pt_device_init(0) in (pt.PT_E_NO_GPU, pt.PT_E_HIP)
+
+
+def _stack_scene(n=60, seed=7):
+    """n small triangles stacked along z above the plane z = 0, with small tilts:
+    IntersectTriangle hits the plane through the origin (src/primitives.cpp:156-157),
+    so their hit regions all overlap near (0, 0, 0) while their own boxes are
+    spread along z -- a ray crossing the stack has dozens of hitting leaves (the
+    query's overflow passes and its exact-DFS hand-over)."""
+    rng = np.random.default_rng(seed)
+    lines = ["DIMENSIONS 8 8", "SAMPLES 1", "RAY_DEPTH 1",
+             "CAMERA_POSITION 0 0 5", "CAMERA_RIGHT 1 0 0", "CAMERA_UP 0 1 0", "CAMERA_FORWARD 0 0 -1",
+             "CAMERA_FOV_X 1.0"]
+    for k in range(n):
+        z = 0.5 + 0.05 * k
+        v = np.array([[-0.3, -0.3, z], [0.3, -0.3, z], [0.0, 0.3, z]]) + rng.normal(0, 0.02, (3, 3))
+        lines += ["NEW_PRIMITIVE", "TRIANGLE " + " ".join("%.5f" % x for x in v.ravel()), "COLOR 0.5 0.5 0.5"]
+    return "\n".join(lines) + "\n"
+
+
+def _stack_rays(n=1500, seed=11):
+    rng = np.random.default_rng(seed)
+    o = np.concatenate([rng.uniform(-0.4, 0.4, (n, 2)), rng.choice([-2.0, 6.0], (n, 1))], axis=1)
+    tgt = np.concatenate([rng.uniform(-0.3, 0.3, (n, 2)), rng.uniform(-0.5, 3.5, (n, 1))], axis=1)
+    d = tgt - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return np.concatenate([o, d], axis=1).astype(np.float32)
+
+
+@pytest.mark.parametrize("engine", ["replay", "coop"])
+def test_many_hitting_leaves_match_oracle(tmp_path, engine, monkeypatch):
+    """Rays with up to ~60 hitting leaves: the path engine's query keeps 6 per
+    pass and hands rays with 6 entered hits and another hit to the exact DFS;
+    the cooperative query holds them all.  Both give the oracle's closest hit."""
+    p = tmp_path / "stack.txt"
+    p.write_text(_stack_scene())
+    rays = _stack_rays()
+    o = U.OracleScene(str(p))
+    oids, ohits = o.ray_intersection(rays)
+    if engine == "coop":
+        monkeypatch.setenv("PT_TUNE", "qengine=coop")
+    with pt.Scene.load(str(p)) as s:
+        s.prepare()
+        ids, hits, ctr = s.selftest_ray_intersection(rays, traversal=0)
+    assert (oids >= 0).sum() > len(rays) // 2
+    assert np.array_equal(ids, oids)
+    hit = oids != -1
+    assert np.array_equal(hits[hit].view(np.uint32), ohits[hit].view(np.uint32))
+    if engine == "replay":
+        assert ctr["fallbacks"] > 0          # some rays exceed the list: the exact DFS took them
