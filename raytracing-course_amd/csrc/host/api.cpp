@@ -924,10 +924,11 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // wave per chain) to the end of the pass; it needs a wave's aux stack to hold
         // a depth-first descent below its expansion limit, and lane 0's exact DFS stack
         const uint32_t cus = (uint32_t)std::max(1, pr.multiProcessorCount);
-        // 98,304 on the 256-CU part (with the probe-first query, rank-of-8 per GPU, teams of 8:
-        // 32 k 1,620, 48 k 1,653, 65 k 1,649, 98 k 1,644, 131 k 1,580-1,587, 262 k 794 Mray/s;
-        // rank-of-2 / -4 best at 98 k)
-        ss->coop_max = cus * 384u;
+        // 49,152 on the 256-CU part (2 query waves per shade wave, hit-region query; rank-of-4 /
+        // rank-of-8 per GPU, teams of 8, two runs each: 32 k 2,758-2,782 / 2,348-2,396, 49 k
+        // 2,754-2,774 / 2,377-2,421, 65 k 2,731-2,763 / 2,318-2,338, 98 k 2,695-2,699 / 2,220-2,324,
+        // 131 k 2,599-2,603 / 2,358-2,430 Mray/s)
+        ss->coop_max = cus * 192u;
         ss->coop_max = (uint32_t)std::max(0, tune_int("coop", (int)ss->coop_max));
         ss->coop_grid = cus * 8u;
         // chains left when the first (narrow-team) launch hands over to whole-wave teams; off:
