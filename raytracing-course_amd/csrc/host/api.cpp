@@ -167,7 +167,6 @@ struct pt_scene {
     uint32_t o_nodes = 0, o_aux = 0, o_ainfo = 0, o_anc = 0, o_qprim = 0, o_prim = 0, o_bundle = 0;
     uint32_t auxw_stack = 0;    // per-lane stack words of the wide aux traversal
     uint32_t aux_rshift = 0;    // leaf-range packing of the wide aux entries (annotate_aux_ranges)
-    uint32_t n_region_leaves = 0;   // leaf entries carrying their primitives' hit region (leaf_hit_region)
     float thr[256];
     std::map<int, DevScene> dev;
     std::mutex mu;
@@ -397,7 +396,6 @@ void encode_aux_entries(pt_scene* s, std::vector<pt::AuxSL>& aux) {
             if (code & 0x80000000u) {
                 if (leaf_hit_region(s, code & 0x7FFFFFFFu, lo, hi)) {
                     b = {lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]};
-                    s->n_region_leaves++;
                 } else {
                     b = unb;
                 }
@@ -434,7 +432,6 @@ void encode_aux_entries(pt_scene* s, std::vector<pt::AuxSL>& aux) {
 void build_query_blob(pt_scene* s) {
     std::vector<pt::F4>& b = s->blob;
     b.clear();
-    s->n_region_leaves = 0;
     auto append = [&b](const void* p, size_t bytes) {
         const uint32_t o = (uint32_t)(b.size() * 16);
         const size_t n = (bytes + 15) / 16;
