@@ -307,7 +307,8 @@ def roofline(st0, st1, traffic_json, key):
     rec = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_wpath",
            "alg_bytes_per_launch": alg_bytes, "launch_ms": launch_s * 1e3, "launches": launches,
-           "rays_share": (d["rays"] - d["coop_rays"]) / max(d["rays"], 1)}
+           "rays_share": (d["rays"] - d["coop_rays"]) / max(d["rays"], 1),
+           "alg_bytes_per_ray": alg_bytes * launches / max(d["rays"] - d["coop_rays"], 1)}
     if d["coop_launches"]:
         rec["coop"] = {"kernel": "k_wcoop (end of pass)", "launches": d["coop_launches"], "ms": d["coop_ms"],
                        "rays": d["coop_rays"], "mray_s": d["coop_rays"] / max(d["coop_ms"], 1e-9) / 1e3}
@@ -327,8 +328,10 @@ def roofline(st0, st1, traffic_json, key):
             if k in prof:
                 rec[k] = prof[k]
     rec["note"] = ("algorithmic = 4-wide aux BVH nodes (128 B) + reference node records (32 B) + compact primitive "
-                   "records (48 B) per visit; the ~25 MB working set is L2/Infinity-Cache resident; what limits the "
-                   "kernel is in `limiter` (rocprofv3 SQ counters, DESIGN.md §4)")
+                   "records (48 B; a probe's 64-B leaf bundle counts its primitive) per visit; the ~30 MB working set "
+                   "is L2/Infinity-Cache resident; the query's work per ray fell from ~1.5 KB (round 1) to ~0.7 KB, so "
+                   "frac falls as Mray/s rises; what limits the kernel is in `limiter` (rocprofv3 SQ counters, "
+                   "DESIGN.md §4)")
     return rec
 
 
