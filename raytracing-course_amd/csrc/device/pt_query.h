@@ -81,7 +81,9 @@ PT_HD bool aux_entry_hit(const F4& ea, const F4& eb, const Ray& ray, f3 inv, f3 
     return tn <= tf && tf >= 0.f && (!(mt < INFINITY) || (un - mt <= uf + mt && uf + mt >= 0.f));
 }
 
-// wide aux entry (AuxSL, 32 B): a = {lo.xyz, hi.x}, b = {hi.y, hi.z, range, code}
+// wide aux entry, host form (AuxSL, 32 B; the array k_wcamera's costly-class test
+// reads): a = {lo.xyz, hi.x}, b = {hi.y, hi.z, range, code} with the own box in f32;
+// the query blob holds the dual binary16 form above with the same range and code:
 //   internal entry: range = (max reference leaf of the subtree >> S, rounded up) << 16 | (min >> S)
 //   (S = SceneView::aux_rshift; annotate_aux_ranges in host/aux_bvh.cpp)
 //   leaf entry (code = 0x80000000 | reference leaf): range = the leaf's ordinal (its bundle)
