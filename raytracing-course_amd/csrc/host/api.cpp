@@ -167,6 +167,7 @@ struct pt_scene {
     uint32_t o_nodes = 0, o_aux = 0, o_ainfo = 0, o_anc = 0, o_qprim = 0, o_prim = 0, o_bundle = 0;
     uint32_t auxw_stack = 0;    // per-lane stack words of the wide aux traversal
     uint32_t aux_rshift = 0;    // leaf-range packing of the wide aux entries (annotate_aux_ranges)
+    std::vector<float> regions;   // per reference node: its leaf's hit region {lo, hi} (lo > hi: unbounded)
     float thr[256];
     std::map<int, DevScene> dev;
     std::mutex mu;
@@ -392,13 +393,10 @@ void encode_aux_entries(pt_scene* s, std::vector<pt::AuxSL>& aux) {
             const uint32_t code = pt::f2u(e.b.w);
             if (code == 0xFFFFFFFFu) continue;
             std::array<float, 6> b;
-            float lo[3], hi[3];
             if (code & 0x80000000u) {
-                if (leaf_hit_region(s, code & 0x7FFFFFFFu, lo, hi)) {
-                    b = {lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]};
-                } else {
-                    b = unb;
-                }
+                const float* r = &s->regions.at(6ull * (code & 0x7FFFFFFFu));
+                if (r[0] <= r[3]) b = {r[0], r[1], r[2], r[3], r[4], r[5]};
+                else b = unb;
             } else {
                 if (code <= n || code >= nn) throw std::runtime_error("aux wide tree: child before its parent");
                 b = nodeB[code];
@@ -432,6 +430,9 @@ void encode_aux_entries(pt_scene* s, std::vector<pt::AuxSL>& aux) {
 void build_query_blob(pt_scene* s) {
     std::vector<pt::F4>& b = s->blob;
     b.clear();
+    // every section's 16-B pieces, reserved at once (the blob is tens of MB)
+    b.reserve(s->dnodes.size() * 2 + s->auxsl.size() * 2 + (s->anc_info.size() + s->anc.size()) / 4 +
+              s->dprims.size() * (3 + 5 + 4) + 64);
     auto append = [&b](const void* p, size_t bytes) {
         const uint32_t o = (uint32_t)(b.size() * 16);
         const size_t n = (bytes + 15) / 16;
@@ -726,6 +727,14 @@ int pt_scene_prepare(pt_scene* s) {
     if (!s) return fail(PT_E_INVALID, "null scene");
     if (s->prepared) return PT_OK;
     try {
+        // PT_TUNE prepstats=1: per-stage times on stderr
+        const bool stats = tune_int("prepstats", 0) != 0;
+        auto tick = [stats, t = std::chrono::steady_clock::now()](const char* what) mutable {
+            if (!stats) return;
+            const auto n = std::chrono::steady_clock::now();
+            fprintf(stderr, "prepare %-22s %7.1f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+            t = n;
+        };
         auto& P = s->hs.prims;
         for (const auto& p : P)
             if (p.type != pt::T_PLANE && p.type != pt::T_BOX && p.type != pt::T_ELLIPSOID && p.type != pt::T_TRIANGLE)
@@ -739,6 +748,7 @@ int pt_scene_prepare(pt_scene* s) {
         for (size_t i = 0; i < idx.size(); ++i) part[i] = P[idx[i]];
         P.swap(part);
         pth::build_reference_bvh(P, s->n_bvh, s->nodes);
+        tick("reference BVH");
         s->planes.clear();
         for (uint32_t i = s->n_bvh; i < (uint32_t)P.size(); ++i) s->planes.push_back(i);
         // InitDistribution: BOX/ELLIPSOID with emission > 0, in post-BVH order
@@ -749,13 +759,15 @@ int pt_scene_prepare(pt_scene* s) {
             if (p.type == pt::T_BOX || p.type == pt::T_ELLIPSOID) s->emitters.push_back(i);
         }
         build_device_layout(s);
+        tick("device layout");
         s->box_extent = 0.f;
         for (const auto& n : s->nodes)
             for (int a = 0; a < 3; ++a) s->box_extent = std::max({s->box_extent, fabsf(n.mn[a]), fabsf(n.mx[a])});
         if (!std::isfinite(s->box_extent)) s->box_extent = INFINITY;   // certification then never succeeds
         {
             // the leaves' hit regions, for the aux build's split choice
-            std::vector<float> reg(6 * s->dnodes.size(), 1.f);
+            std::vector<float>& reg = s->regions;
+            reg.assign(6 * s->dnodes.size(), 1.f);
             for (uint32_t i = 0; i < (uint32_t)s->dnodes.size(); ++i) {
                 float lo[3], hi[3];
                 if ((pt::f2u(s->dnodes[i].b.w) & 0x80000000u) || !leaf_hit_region(s, i, lo, hi)) {
@@ -764,14 +776,18 @@ int pt_scene_prepare(pt_scene* s) {
                 }
                 for (int a = 0; a < 3; ++a) { reg[6 * i + a] = lo[a]; reg[6 * i + 3 + a] = hi[a]; }
             }
+            tick("hit regions");
             pth::build_aux_bvh(s->nodes, reg, s->aux, s->aux_depth);
+            tick("aux BVH2");
         }
         pth::build_aux_wide(s->aux, s->dnodes, PT_AUXW, s->auxsl, s->auxsl_depth, s->auxw_stack);
         pth::annotate_aux_ranges(s->auxsl, PT_AUXW, (uint32_t)s->dnodes.size(), s->aux_rshift);
         // Query::sp (pt_query.h) counts pending aux nodes in a 7-bit field
         if (s->auxw_stack > PT_QUERY_SP_MAX)
             throw std::runtime_error("auxiliary BVH too deep for the query's stack counter");
+        tick("aux wide + ranges");
         build_query_blob(s);
+        tick("query blob");
         pth::build_gamma_thresholds(s->thr);
     } catch (const std::exception& e) {
         return fail(PT_E_SCENE, e.what());
