@@ -88,6 +88,7 @@ const Rccl& rccl() {
 //   cprof=1           per-phase cycles of the cooperative engine on stderr (-DPT_CPROF builds)
 //   qstats=FILE       per-query work counters of the host self-test render
 //   qengine=coop      host self-tests: the cooperative engine's query algorithm (pt_coop.h)
+//   prepstats=1       pt_scene_prepare's per-stage times on stderr
 std::string tune_str(const char* key) {
     const char* e = getenv("PT_TUNE");
     if (!e) return {};
