@@ -1049,13 +1049,15 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.path = 1u;
     wp.path_budget = ss->path_budget;
     wp.path_runend = ss->path_runend;
-    // Chains a workgroup may hold: PT_CMAX when the pixels outnumber that, else a
-    // little below the pixels' fair share, so the workgroups do not fill up to
-    // uneven depths and a few chains wait, costly-first, in the queue (a rank of
-    // a large N: 261 k pixels on 768 workgroups -> 320 each, +7 %).
+    // Chains a workgroup may hold: 5/8 of the pixels' fair share, within
+    // [256, PT_CMAX].  Below the share, about a third of the chains wait in the
+    // queue and go to whichever workgroup drains first, instead of every
+    // workgroup filling to its share and the costly ones finishing last
+    // (1920x1080 on 1,024 workgroups: rank of 4 -> 319 instead of 478, +1 % over
+    // three alternating pairs; ranks of 1 and 2 stay at 512, a rank of 8 at 256).
     {
         const uint64_t share = ((uint64_t)ss->n_slots + ss->path_grid - 1) / std::max(1u, ss->path_grid);
-        wp.path_cap = (uint32_t)std::min<uint64_t>(PT_CMAX, std::max<uint64_t>(256u, share * 15u / 16u));
+        wp.path_cap = (uint32_t)std::min<uint64_t>(PT_CMAX, std::max<uint64_t>(256u, share * 5u / 8u));
     }
     if (tune_has("cap")) wp.path_cap = std::min<uint32_t>(PT_CMAX, (uint32_t)std::max(64, tune_int("cap", 0)));
     wp.tile_order = tune_int("rowmajor", 0) ? nullptr : ss->tile_order;
