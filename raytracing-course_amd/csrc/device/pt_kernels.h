@@ -138,6 +138,9 @@ struct WaveParams {
 #define QC_NPL 8u                  // plane records copied to LDS per workgroup (n_planes <= QC_NPL, host-checked)
 #define QC_NEM 8u                  // emitter records copied to LDS per workgroup (n_emitters <= QC_NEM)
 #define QC_TOPN 21u                // aux BVH nodes 0..20 (BFS order: the top three levels) copied to LDS
+#ifndef QC_LPE
+#define QC_LPE 1                   // 1: the aux expansion tests one node entry per lane (else a node per lane)
+#endif
 
 struct ResolveParams {
     PixelState st;

@@ -957,11 +957,46 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
             }
             QC_TICK(1);
         }
-        // 1. breadth-first expansion of the wide aux BVH: one node per team lane
         const bool expand = run && !ovf && ns > 0u;
         if (__ballot(expand) == 0ull) break;
         uint32_t k = slim > ns ? (slim - ns) / 3u : 0u;
         k = k < 1u ? 1u : k;
+#if QC_LPE
+        // 1. breadth-first expansion of the wide aux BVH: one node per PT_AUXW team
+        //    lanes, a lane per entry (a round's instructions test one entry, not PT_AUXW)
+        constexpr uint32_t KN = T / PT_AUXW;
+        k = k > KN ? KN : k;
+        k = k > ns ? ns : k;
+        if (!expand) k = 0u;
+        if (ns + 3u * k > SCAP) { ovf = true; k = 0u; }   // cannot happen with the host's reserve (checked)
+        ns -= k;
+        {
+            const uint32_t ni = tl / PT_AUXW, e = tl % PT_AUXW;
+            const bool act = ni < k;
+            const uint32_t node = act ? L.stk[ns + ni] : 0u;
+            C.aux += act && e == 0u ? 1u : 0u;
+            F4 ea, eb;
+            if (node < QC_TOPN) {
+                ea = Q.top[node * PT_AUXW + e].a;
+                eb = Q.top[node * PT_AUXW + e].b;
+            } else {
+                const uint32_t b = S.o_aux + (node * PT_AUXW + e) * (uint32_t)sizeof(AuxSL);
+                ea = blob_piece(S, b);
+                eb = blob_piece(S, b + 16u);
+            }
+            const uint32_t code = f2u(eb.w);
+            bool h = act && code != 0xffffffffu;
+            if (h) h = aux_entry_hit(ea, eb, ray, inv, oinv, pre.w);
+            const bool leaf = h && (code & 0x80000000u) != 0u;
+            const bool inner = h && (code & 0x80000000u) == 0u;
+            const unsigned long long mi = __ballot(inner) & tmask, ml = __ballot(leaf) & tmask;
+            if (inner) L.stk[ns + lanes_below(mi)] = code;
+            if (leaf) L.cand[nc + lanes_below(ml)] = code & 0x7fffffffu;
+            ns += (uint32_t)__popcll(mi);
+            nc += (uint32_t)__popcll(ml);
+        }
+#else
+        // 1. breadth-first expansion of the wide aux BVH: one node per team lane
         k = k > T ? T : k;
         k = k > ns ? ns : k;
         if (!expand) k = 0u;
@@ -997,6 +1032,7 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
             ns += (uint32_t)__popcll(mi);
             nc += (uint32_t)__popcll(ml);
         }
+#endif
     }
     QC_TICK(0);
     if (ovf) exact = true;

@@ -14,6 +14,11 @@ for i, r in enumerate(a):
     m = re.search(r"in fresh (\d+) carry (\d+)", L[i]) if i < len(L) else None
     n = int(m.group(1)) + int(m.group(2)) if m else -1
     if i < 400:
-        print("round %3d n_in %7d span %8.0f us  WG dur p50 %6.0f max %6.0f" % (
-            i, n, span, np.median((rr[:, 1] - rr[:, 0]) / 100.0) if len(rr) else 0, ((rr[:, 1] - rr[:, 0]) / 100.0).max() if len(rr) else 0))
+        g = max(len(rr), 1)
+        print("round %3d n_in %7d span %8.0f us  WG dur p50 %6.0f max %6.0f  trips/QW %6.0f lane util %.2f sleep %.2f "
+              "pulled %7d rays(lane0) %9d budget exits %.2f" % (
+            i, n, span, np.median((rr[:, 1] - rr[:, 0]) / 100.0) if len(rr) else 0,
+            ((rr[:, 1] - rr[:, 0]) / 100.0).max() if len(rr) else 0, rr[:, 2].sum() / (2.0 * g),
+            rr[:, 3].sum() / max(64.0 * rr[:, 2].sum(), 1), rr[:, 4].sum() / max(rr[:, 2].sum(), 1),
+            rr[:, 11].sum(), rr[:, 6].sum(), rr[:, 12].sum() / (2.0 * g)))
 print("total span ms %.1f" % (tot / 1e3))
