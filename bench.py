@@ -327,6 +327,17 @@ def roofline(st0, st1, traffic_json, key):
                   "wait_frac", "vgpr", "waves_per_simd"):
             if k in prof:
                 rec[k] = prof[k]
+        if "wait_any_frac" in prof and "valu_issue_frac" in prof:
+            # what the SQ counters of that profile say bounds the kernel: the
+            # roofline is priced against HBM, but neither HBM nor VALU issue is saturated
+            hbm = rec["traffic"] / launch_s / 1e9 / HBM_PEAK_GBS if launch_s > 0 else 0.0
+            rec["limiter"] = {
+                "verdict": "latency" if max(hbm, prof["valu_issue_frac"]) < 0.6 else
+                           ("hbm" if hbm >= prof["valu_issue_frac"] else "valu_issue"),
+                "memory_side_frac_of_hbm_peak": hbm, "valu_issue_frac": prof["valu_issue_frac"],
+                "wave_wait_any_frac": prof["wait_any_frac"],
+                "source": "profiles/%s SQ_ACTIVE_INST_VALU / SQ_INSTS_VALU / SQ_WAIT_ANY per wave-cycle"
+                          % prof.get("profile", "?")}
     rec["note"] = ("algorithmic = 4-wide aux BVH nodes (128 B) + reference node records (32 B) + compact primitive "
                    "records (48 B; a probe's 64-B leaf bundle counts its primitive) per visit; the ~30 MB working set "
                    "is L2/Infinity-Cache resident; the query's work per ray fell from ~1.5 KB (round 1) to ~0.7 KB, so "

@@ -78,6 +78,8 @@ const Rccl& rccl() {
 //   sparse_steps=N    steps per loop trip of the end-of-pass kernel
 //   coop=N            a round with at most N chains runs the cooperative engine (one wave
 //                     per chain) to the end of the pass (0: never)
+//   near_budget=N     path-engine round budget once the chains are at most near_k/4 x the
+//                     cooperative hand-over (0: the usual budget); near_k=K (default 8)
 //   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
 //   coop_stop=N       the first cooperative launch hands its last N chains to whole-wave teams (0: never)
 //   cap=N             chains a workgroup may hold
@@ -190,6 +192,7 @@ struct pt_session {
     uint32_t path_grid = 0, path_budget = 1024, path_runend = 0, path_sparse = 0, sparse_steps = 8;
     uint32_t coop_max = 0, coop_grid = 0, coop_reserve = 0;   // cooperative engine (k_wcoop) at the end of a pass
     uint32_t coop_stop = 0;       // chains left when the first cooperative launch hands over to whole waves
+    uint32_t near_budget = 0, near_chains = 0;   // round budget near the cooperative hand-over
     uint32_t coop_team = 8;       // lanes per chain in the cooperative engine (pure-coop rate, teams of
                                   // 64 / 32 / 16 / 8: 283 / 392 / 572 / 815 Mray/s)
     pt::F4* qbuf = nullptr;       // 10 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd, fq0.ri, fq1.ri
@@ -965,6 +968,9 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // ... and the end-of-pass (sparse) path kernel, whose rounds are long, never runs
         // above the hand-over
         if (ss->coop_max && !tune_has("sparse")) ss->path_sparse = std::min(ss->path_sparse, ss->coop_max);
+        // round budget once the chains are at most near_k/4 x coop_max (0: the usual budget)
+        ss->near_budget = ss->coop_max ? (uint32_t)std::max(0, tune_int("near_budget", 0)) : 0u;
+        ss->near_chains = (uint32_t)((uint64_t)ss->coop_max * (uint32_t)std::max(4, tune_int("near_k", 8)) / 4u);
         if (hipMalloc(&ss->ring, (size_t)ss->path_grid * PT_RING_F4 * sizeof(pt::F4)) != hipSuccess)
             return cleanup(fail(PT_E_OOM, "device allocation failed (path rings)"));
         if (ss->n_tiles_local) {
@@ -1142,6 +1148,9 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             }
             break;
         }
+        // near the cooperative hand-over, shorter rounds: the host sees the chain count
+        // fall below coop_max sooner after it does
+        wp.path_budget = ss->near_budget && chains <= ss->near_chains ? ss->near_budget : ss->path_budget;
         for (uint32_t r = 0; r < batch; ++r) {
             wp.parity = p;
             const std::string wgps = tune_str("wgprof");
