@@ -51,6 +51,13 @@ IMAGES = {
     "c3s4_win_944_520_16x16": ("c3", (1920, 1080, 4, True, "diffuse"), (944, 520, 16, 16)),
     "c4glass_s4_win_900_560_16x16": ("c4_glass", (1920, 1080, 4, True, "glass"), (900, 560, 16, 16)),
     "c4metal_s4_win_900_560_16x16": ("c4_metal", (1920, 1080, 4, True, "metal"), (900, 560, 16, 16)),
+    # more windows of configs 3/4: the frame's corners (edge tiles), a window off the
+    # 16x16 tile grid, and further regions of the metal and glass variants
+    "c3s4_win_0_0_16x16": ("c3", (1920, 1080, 4, True, "diffuse"), (0, 0, 16, 16)),
+    "c3s4_win_1896_1064_24x16": ("c3", (1920, 1080, 4, True, "diffuse"), (1896, 1064, 24, 16)),
+    "c3s4_win_1001_537_24x12": ("c3", (1920, 1080, 4, True, "diffuse"), (1001, 537, 24, 12)),
+    "c4metal_s4_win_1010_470_16x16": ("c4_metal", (1920, 1080, 4, True, "metal"), (1010, 470, 16, 16)),
+    "c4glass_s4_win_830_610_16x16": ("c4_glass", (1920, 1080, 4, True, "glass"), (830, 610, 16, 16)),
     # config 5 (3840x2160, pixel-tiled over 8 GPUs): windows whose 16x16 tiles belong to
     # ranks 0, 2+3, 6 and 7 of 8 (global tile ty*240+tx, rank = tile % 8); seeds y*3840+x
     "c5s4_win_1920_1072_16x16": ("c5", (3840, 2160, 4, True, "diffuse"), (1920, 1072, 16, 16)),
