@@ -270,9 +270,9 @@ def wall_to_ppm(config, ngpu):
     if ngpu > 1:
         env["PT_GATHER"] = "rccl"
     t0 = time.perf_counter()
-    # bounded: a hung CLI (e.g. RCCL initialisation) must not hold back the bench line
+    # bounded (120 s; c3 takes ~1 s): a hung CLI (e.g. RCCL initialisation) must not hold back the bench line
     r = subprocess.run([os.path.join(REPO, "run.sh"), src, out], env=env, capture_output=True, text=True,
-                       timeout=240)
+                       timeout=120)
     dt = time.perf_counter() - t0
     if r.returncode != 0:
         raise RuntimeError(r.stderr.strip()[-300:])
