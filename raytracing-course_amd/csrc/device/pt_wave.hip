@@ -271,6 +271,12 @@ struct PathRing {
 #ifndef PT_PATH_REFILL_MIN
 #define PT_PATH_REFILL_MIN 8u      // idle lanes before a query wave refills (any, once the round's work is out)
 #endif
+#ifndef PT_SHADE_PRIO
+#define PT_SHADE_PRIO 0            // issue priority (s_setprio 0-3) of the shade wave ...
+#endif
+#ifndef PT_QUERY_PRIO
+#define PT_QUERY_PRIO 0            // ... and of the query waves, against the other waves of their SIMD
+#endif
 #define PT_NOWORK 0xffffffffu
 #define PT_CAPPED 0xfffffffeu
 
@@ -798,8 +804,13 @@ __global__ void __launch_bounds__(PT_PATH_WG) __attribute__((amdgpu_waves_per_eu
     // which wave shades: rotated over the workgroups (PT_ROTATE_SHADE), so the
     // shade waves of a CU's workgroups do not all sit on one SIMD
     const uint32_t wave = threadIdx.x >> 6, sw = PT_ROTATE_SHADE ? blockIdx.x % (PT_NQ + 1u) : PT_NQ;
-    if (wave == sw) path_shade_wave(P, L, G);
-    else path_query_wave<SPARSE>(P, L, G, lds_stack, wave < sw ? wave : wave - 1u);
+    if (wave == sw) {
+        if (PT_SHADE_PRIO) __builtin_amdgcn_s_setprio(PT_SHADE_PRIO);
+        path_shade_wave(P, L, G);
+    } else {
+        if (PT_QUERY_PRIO) __builtin_amdgcn_s_setprio(PT_QUERY_PRIO);
+        path_query_wave<SPARSE>(P, L, G, lds_stack, wave < sw ? wave : wave - 1u);
+    }
 #elif PT_PATH_ONLY == 1
     path_query_wave<SPARSE>(P, L, G, lds_stack, threadIdx.x >> 6);
 #else
