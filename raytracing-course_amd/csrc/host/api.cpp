@@ -80,6 +80,8 @@ const Rccl& rccl() {
 //                     per chain) to the end of the pass (0: never)
 //   near_budget=N     path-engine round budget once the chains are at most near_k/4 x the
 //                     cooperative hand-over (0: the usual budget); near_k=K (default 8)
+//   round_batch=N     path rounds launched per chain count while the chains are far above
+//                     the hand-over (default 1)
 //   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
 //   coop_stop=N       the first cooperative launch hands its last N chains to whole-wave teams (0: never)
 //   cap=N             chains a workgroup may hold
@@ -193,6 +195,7 @@ struct pt_session {
     uint32_t coop_max = 0, coop_grid = 0, coop_reserve = 0;   // cooperative engine (k_wcoop) at the end of a pass
     uint32_t coop_stop = 0;       // chains left when the first cooperative launch hands over to whole waves
     uint32_t near_budget = 0, near_chains = 0;   // round budget near the cooperative hand-over
+    uint32_t round_batch = 1;     // rounds launched per count while the chains are far above the hand-over
     uint32_t coop_team = 8;       // lanes per chain in the cooperative engine (pure-coop rate, teams of
                                   // 64 / 32 / 16 / 8: 283 / 392 / 572 / 815 Mray/s)
     pt::F4* qbuf = nullptr;       // 10 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd, fq0.ri, fq1.ri
@@ -971,6 +974,7 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // round budget once the chains are at most near_k/4 x coop_max (0: the usual budget)
         ss->near_budget = ss->coop_max ? (uint32_t)std::max(0, tune_int("near_budget", 0)) : 0u;
         ss->near_chains = (uint32_t)((uint64_t)ss->coop_max * (uint32_t)std::max(4, tune_int("near_k", 8)) / 4u);
+        ss->round_batch = (uint32_t)std::max(1, tune_int("round_batch", (int)ss->round_batch));
         if (hipMalloc(&ss->ring, (size_t)ss->path_grid * PT_RING_F4 * sizeof(pt::F4)) != hipSuccess)
             return cleanup(fail(PT_E_OOM, "device allocation failed (path rings)"));
         if (ss->n_tiles_local) {
@@ -1215,7 +1219,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
         if (guard > 100000u) return fail(PT_E_HIP, "wavefront rounds did not drain");
         chains = ss->ctl_host[pt::C_FRESH] + ss->ctl_host[pt::C_CARRY];
         // near the cooperative hand-over every round is counted (the tail's rounds take ms)
-        batch = chains > 4096u && chains > 4u * ss->coop_max ? 4u : (chains > 4096u ? 1u : 2u);
+        batch = chains > 4096u && chains > 4u * ss->coop_max ? ss->round_batch : (chains > 4096u ? 1u : 2u);
         sparse = chains < ss->path_sparse;
     }
     HIP_TRY(hipEventRecord(e1, ss->stream));
