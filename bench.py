@@ -115,12 +115,15 @@ def gather_tiles(dist, packed, rank, world, width, height, device):
     un-interleave into the H x W x 3 framebuffer on rank 0's device, and one
     copy of it to the host (rank 0 returns it as a numpy array).
 
-    Rank r holds global tiles r, r + world, ... (16 x 16 x 3 bytes each), so
-    the gathered [world, tiles, 16, 16, 3] block transposed to [tiles, world]
-    lists the tiles in global order."""
+    Rank r holds the tiles (tx, ty) with (tx + ty) % world == r, in ascending
+    order (include/pt.h sessions), 16 x 16 x 3 bytes each; the gathered
+    [world, cap_tiles] blocks are put in global tile order by one index gather."""
     import torch
-    n_tiles = (width + 15) // 16 * ((height + 15) // 16)
-    cap_tiles = (n_tiles + world - 1) // world
+    tiles_x, tiles_y = (width + 15) // 16, (height + 15) // 16
+    n_tiles = tiles_x * tiles_y
+    t_all = np.arange(n_tiles)
+    owner = (t_all % tiles_x + t_all // tiles_x) % world
+    cap_tiles = int(np.bincount(owner, minlength=world).max())
     cap = cap_tiles * 768
     if packed.numel() == cap:
         buf = packed.contiguous()
@@ -134,8 +137,13 @@ def gather_tiles(dist, packed, rank, world, width, height, device):
         dist.gather(buf, list(parts.unbind(0)) if rank == 0 else None, dst=0)
     if rank != 0:
         return None
-    tiles_x, tiles_y = (width + 15) // 16, (height + 15) // 16
-    t = parts.view(world, cap_tiles, 16, 16, 3).transpose(0, 1).reshape(world * cap_tiles, 16, 16, 3)[:n_tiles]
+    # source block of every global tile: owner * cap_tiles + its rank in the owner's list
+    local = np.zeros(n_tiles, np.int64)
+    for r in range(world):
+        m = owner == r
+        local[m] = np.arange(int(m.sum()))
+    src = torch.from_numpy(owner.astype(np.int64) * cap_tiles + local).to(parts.device)
+    t = parts.view(world * cap_tiles, 16, 16, 3).index_select(0, src)
     img = t.view(tiles_y, tiles_x, 16, 16, 3).permute(0, 2, 1, 3, 4).reshape(tiles_y * 16, tiles_x * 16, 3)
     return img[:height, :width].cpu().numpy()
 

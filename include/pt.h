@@ -25,7 +25,8 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 3   /* 2: pt_render_opts.gather; 3: pt_stats per-engine (coop_*) fields */
+#define PT_ABI_VERSION 4   /* 2: pt_render_opts.gather; 3: pt_stats per-engine (coop_*) fields;
+                              4: pt_gather_init */
 
 enum {
     PT_OK = 0,
@@ -60,6 +61,13 @@ int pt_scene_prepare(pt_scene* s);
  * CPU, so the runtime's start-up does not add to the wall-clock (cli/main.cpp).
  * pt_render does the same work itself when it has not been done. */
 int pt_device_init(int device);
+
+/* Optional creation of the RCCL communicator that pt_render(ngpu = n, gather RCCL)
+ * uses over devices device .. device+n-1 (ncclCommInitAll, cached per process).  No
+ * reference counterpart (the reference renders on one host): the CLI runs it on its
+ * start-up thread beside Scene::Load / InitScene, so the communicator's set-up is not
+ * paid between the render and the PPM.  pt_render creates it itself otherwise. */
+int pt_gather_init(int device, int ngpu);
 
 typedef struct pt_scene_info {
     uint32_t width, height, samples, ray_depth;
@@ -149,7 +157,9 @@ int pt_write_ppm(const char* path, uint32_t width, uint32_t height, const uint8_
 /* ------------------------------------------------------- sessions (tiles)
  * Progressive / sharded rendering on ONE device, used by pt_render and by
  * multi-process drivers (one process per GPU): the image is cut into 16x16
- * tiles, tile t belongs to rank t % world; the session keeps every owned
+ * tiles, tile (tx, ty) belongs to rank (tx + ty) % world (diagonal stripes: every
+ * rank gets every row and column of the image); a rank's tiles are kept in
+ * ascending tile order (t = ty * tiles_x + tx).  The session keeps every owned
  * pixel's RNG stream and f32 sum resident in HBM, so pt_session_trace(spp)
  * continues each pixel's stream exactly as the reference's sequential spp loop. */
 typedef struct pt_session_opts {

@@ -33,12 +33,17 @@ int main(int argc, char** argv) {
     const auto t_main = std::chrono::steady_clock::now();
     auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_main).count(); };
     const int ngpu = env_int("PT_NGPU", 1), dev0 = env_int("PT_DEVICE", 0);
-    double t_warm = 0, t_load = 0, t_join = 0, t_render = 0, t_write = 0;
+    double t_warm = 0, t_comm = 0, t_load = 0, t_join = 0, t_render = 0, t_write = 0;
+    const char* gather = getenv("PT_GATHER");
+    const bool host_gather = gather && !strcmp(gather, "host");
     // the HIP runtime starts on a second thread while the scene is parsed and its
-    // BVH built (errors surface again, from pt_render)
+    // BVH built, and with several GPUs the RCCL communicator of the framebuffer
+    // gather is created there too (errors surface again, from pt_render)
     std::thread warm([&] {
         for (int g = 0; g < ngpu; ++g) (void)pt_device_init(dev0 + g);
         t_warm = ms();
+        if (ngpu > 1 && !host_gather) (void)pt_gather_init(dev0, ngpu);
+        t_comm = ms();
     });
     pt_scene* s = nullptr;
     const bool ok = pt_scene_load(argv[1], &s) == PT_OK && pt_scene_prepare(s) == PT_OK;
@@ -58,9 +63,9 @@ int main(int argc, char** argv) {
     o.device = dev0;
     o.spp_per_launch = (uint32_t)env_int("PT_SPP_LAUNCH", 0);
     o.progress = env_int("PT_QUIET", 0) ? 0 : 1;
-    if (const char* g = getenv("PT_GATHER")) {
-        if (!strcmp(g, "rccl")) o.gather = PT_GATHER_RCCL;
-        else if (!strcmp(g, "host")) o.gather = PT_GATHER_HOST;
+    if (gather) {
+        if (!strcmp(gather, "rccl")) o.gather = PT_GATHER_RCCL;
+        else if (host_gather) o.gather = PT_GATHER_HOST;
     }
     std::vector<uint8_t> rgb((size_t)info.width * info.height * 3);
     pt_stats st;
@@ -77,8 +82,8 @@ int main(int argc, char** argv) {
     }
     t_write = ms();
     if (env_int("PT_STATS", 0) >= 2)
-        fprintf(stderr, "phases_ms: device_init=%.1f load_prepare=%.1f join=%.1f render=%.1f write=%.1f\n", t_warm,
-                t_load, t_join, t_render, t_write);
+        fprintf(stderr, "phases_ms: device_init=%.1f comm_init=%.1f load_prepare=%.1f join=%.1f render=%.1f write=%.1f\n",
+                t_warm, t_comm, t_load, t_join, t_render, t_write);
     if (env_int("PT_STATS", 0)) {
         fprintf(stderr, "rays=%llu samples=%llu kernel_ms=%.3f wall_ms=%.3f Mray/s=%.3f ngpu=%d gather_rccl=%llu "
                 "fallbacks=%llu rounds=%llu\n",

@@ -53,7 +53,7 @@ __device__ __forceinline__ HbmVStore fold_store(const PixelState& st, uint32_t s
 // the RNG / progress piece of a slot's record
 struct PixelHot {
     Rng R;
-    uint32_t nv;      // vertices of the current path (fold records written)
+    uint32_t nv;      // vertices of the current path (fold records written; 24 bits: RAY_DEPTH < 2^24)
     uint32_t done;    // samples completed in this session
 };
 __device__ __forceinline__ PixelHot load_hot(const PixelState& st, uint32_t slot) {
@@ -62,7 +62,7 @@ __device__ __forceinline__ PixelHot load_hot(const PixelState& st, uint32_t slot
     h.R.x = v.x;
     h.R.saved = u2f(v.y);
     h.R.saved_ok = v.z & 1u;
-    h.nv = (v.z >> 8) & 0xffu;
+    h.nv = v.z >> 8;
     h.done = v.w;
     return h;
 }
@@ -73,14 +73,20 @@ __device__ __forceinline__ f3 load_sum(const PixelState& st, uint32_t slot) {
     const uint4 v = st.rec[2u * slot + 1u];
     return mk3(u2f(v.x), u2f(v.y), u2f(v.z));
 }
-__device__ __forceinline__ void store_sum(const PixelState& st, uint32_t slot, f3 s) {
-    st.rec[2u * slot + 1u] = make_uint4(f2u(s.x), f2u(s.y), f2u(s.z), 0u);
+// the sum and the slot's global pixel index (one 16-B load)
+__device__ __forceinline__ f3 load_sum_pix(const PixelState& st, uint32_t slot, uint32_t& pix) {
+    const uint4 v = st.rec[2u * slot + 1u];
+    pix = v.w;
+    return mk3(u2f(v.x), u2f(v.y), u2f(v.z));
+}
+__device__ __forceinline__ void store_sum(const PixelState& st, uint32_t slot, f3 s, uint32_t pix) {
+    st.rec[2u * slot + 1u] = make_uint4(f2u(s.x), f2u(s.y), f2u(s.z), pix);
 }
 
-// owned slot -> global pixel (16x16 tiles of the window dealt round-robin to ranks)
+// owned slot -> global pixel (16x16 tiles of the window, dealt to ranks by tile_owner)
 __device__ __forceinline__ bool slot_pixel(const TileMap& tm, uint32_t tile_local, uint32_t lane, uint32_t& x,
                                            uint32_t& y) {
-    const uint32_t gt = tile_local * tm.world + tm.rank;
+    const uint32_t gt = tm.gtile[tile_local];
     const uint32_t tx = gt % tm.tiles_x, ty = gt / tm.tiles_x;
     const uint32_t wx = tx * 16u + (lane & 15u), wy = ty * 16u + (lane >> 4);
     x = tm.x0 + wx;

@@ -16,14 +16,28 @@ struct TileMap {
     uint32_t ww, wh;      // rendered window size (= W, H for a full render)
     uint32_t tiles_x;     // ceil(ww/16)
     uint32_t n_tiles;     // ceil(ww/16)*ceil(wh/16)
-    uint32_t rank, world; // window tile t belongs to rank t % world
+    uint32_t rank, world; // window tile t belongs to rank tile_owner(t, tiles_x, world)
+    const uint32_t* gtile;   // device: this rank's window tiles in ascending order (local -> window tile)
 };
+
+// The deal of a window's 16x16 tiles to the ranks of a multi-GPU render: tile
+// (tx, ty) belongs to rank (tx + ty) % world.  Diagonal stripes give every rank
+// every column and every row of the image in equal parts; the plain t % world
+// deals whole tile columns whenever tiles_x % world == 0 (1080p: 120 tiles per
+// row), and the dragon's columns cost more than the walls' (rank-of-8 spread 7 %).
+// A rank's local tiles are its window tiles in ascending order.
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline uint32_t tile_owner(uint32_t t, uint32_t tiles_x, uint32_t world) {
+    return (t % tiles_x + t / tiles_x) % world;
+}
 
 // Per owned slot (256 per owned tile) one 32-B record, read and written as two
 // 16-B pieces: a shade touches ONE piece (one vector load + one store instead of
 // five scattered dwords), the path end the second one as well.
-//   rec[2 slot]     = {rng x, rng saved (f32 bits), rng flag | vertices << 8, samples done}
-//   rec[2 slot + 1] = {sum.r, sum.g, sum.b, -}
+//   rec[2 slot]     = {rng x, rng saved (f32 bits), rng flag | vertices << 8 (24 bits), samples done}
+//   rec[2 slot + 1] = {sum.r, sum.g, sum.b, global pixel index y*W + x (its seed)}
 // Fold records (one 16-B record per path vertex: {idm, s1, s2, -}) are slot-major,
 // fold[slot * depth + k], so a path's records share lines.
 struct PixelState {
@@ -68,8 +82,7 @@ enum : uint32_t { PE_LIVE = 0u, PE_MISS = 1u, PE_CUT = 2u, PE_TERM = 3u };
 
 // round counters: set p = ctl + PT_CTL_SET * p; the work-batch heads are one per
 // XCD, each on its own 128-B line (C_HEADS + 32 x)
-enum : uint32_t { C_FRESH = 0u, C_CARRY = 1u, C_DONE = 3u, C_EXACT = 4u, C_FRONT = 5u, C_BACK = 6u, C_LIVE = 8u,
-                  C_HEADS = 32u };
+enum : uint32_t { C_FRESH = 0u, C_CARRY = 1u, C_DONE = 3u, C_EXACT = 4u, C_FRONT = 5u, C_BACK = 6u, C_HEADS = 32u };
 #define PT_CTL_SET 288u          // words per counter set (C_HEADS + 8 x 32)
 // statistics counters: one copy per XCD (PT_CTR_COPIES x PT_CTR_STRIDE u64), summed by the host
 #define PT_CTR_COPIES 8u
@@ -106,8 +119,6 @@ struct WaveParams {
     uint32_t sparse_steps;        // steps per loop trip of the end-of-pass (sparse) kernel
     F4* ring;                     // per-workgroup ray/done rings, PT_RING_F4 F4 per workgroup
     uint32_t coop_reserve;        // k_wcoop: aux stack words kept free for a depth-first descent (3 (aux depth + 2))
-    uint32_t coop_stop;           // k_wcoop: once the queue is empty and at most this many chains are held,
-                                  // they leave for the next launch (0: run to the end)
 };
 
 // path engine geometry: PT_NQ query waves + 1 shade wave per workgroup; at most
@@ -134,13 +145,10 @@ struct WaveParams {
 #define QC_WAVES 4u
 #endif
 #define QC_SCAP_MIN 128u           // aux stack words per team (the smallest; also the exact DFS stack)
-#define QC_FOLD 6u                 // fold records held in LDS per chain (RAY_DEPTH <= QC_FOLD, host-checked)
-#define QC_NPL 8u                  // plane records copied to LDS per workgroup (n_planes <= QC_NPL, host-checked)
-#define QC_NEM 8u                  // emitter records copied to LDS per workgroup (n_emitters <= QC_NEM)
+#define QC_FOLD 6u                 // fold records held in LDS per chain (deeper vertices: HBM fold records)
+#define QC_NPL 8u                  // plane records copied to LDS per workgroup (further planes: from HBM)
+#define QC_NEM 8u                  // emitter records copied to LDS per workgroup (further emitters: from HBM)
 #define QC_TOPN 21u                // aux BVH nodes 0..20 (BFS order: the top three levels) copied to LDS
-#ifndef QC_LPE
-#define QC_LPE 1                   // 1: the aux expansion tests one node entry per lane (else a node per lane)
-#endif
 
 struct ResolveParams {
     PixelState st;
@@ -165,7 +173,8 @@ hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s);
 hipError_t pt_launch_path_round(pt::WaveParams p, uint32_t path_grid, uint32_t shade_grid, hipStream_t s, bool sparse,
                                 hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 // cooperative engine: one launch runs every remaining chain of the pass to its end
-// team = lanes per chain (16, 32 or 64)
-hipError_t pt_launch_coop(pt::WaveParams p, uint32_t grid, uint32_t team, hipStream_t s, hipEvent_t e0 = nullptr,
-                          hipEvent_t e1 = nullptr);
+// team = lanes per chain (8 -- the default --, 16, 32 or 64)
+// big: the scene exceeds the LDS tables (QC_FOLD / QC_NPL / QC_NEM; team 8 or 64 then)
+hipError_t pt_launch_coop(pt::WaveParams p, uint32_t grid, uint32_t team, bool big, hipStream_t s,
+                          hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t pt_launch_resolve(const pt::ResolveParams& p, uint32_t n_tiles, hipStream_t s);

@@ -28,7 +28,7 @@ __global__ void __launch_bounds__(256) k_init(InitParams P) {
     h.nv = 0u;
     h.done = 0u;
     store_hot(P.st, slot, h);
-    store_sum(P.st, slot, mk3(0.f, 0.f, 0.f));
+    store_sum(P.st, slot, mk3(0.f, 0.f, 0.f), ok ? y * P.tm.W + x : 0u);
 }
 
 // V bit 0: filtered node tests + flat replay loop (FAST); bit 1: XCD-banded
@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(256) k_trace(TraceParams P) {
         hot.R = R;
         hot.done += P.spp;
         store_hot(P.st, slot, hot);
-        store_sum(P.st, slot, sum);
+        store_sum(P.st, slot, sum, y * P.tm.W + x);
     }
     unsigned long long* ctr = ctr_copy(P.counters);
     wave_add_u64(ctr + 0, C.rays);

@@ -694,25 +694,16 @@ PT_HD F4 blob_piece(const SceneView& S, uint32_t off) {
 
 // Advance one step.  Precondition: phase is Q_AUX or Q_REPLAY.
 // `stk` = per-lane word memory for the pending aux nodes (set/get).
-#ifndef PT_MASKED_PIECES
-#define PT_MASKED_PIECES 0   // 1: a lane loads only the distinct pieces its step reads
-#endif
+// Every lane loads 8 pieces (q_addr repeats a step's last piece): loading only
+// the distinct ones measured -5 % (the exec-mask branches cost more than the
+// repeated loads, which hit the same line).
 template <class Mem>
 PT_HD void q_step(const SceneView& S, Query& q, QCounts& C, Mem& stk) {
     uint32_t off[8];
     q_addr(S, q, off);
     F4 r[8];
-#if PT_MASKED_PIECES
-    // pieces this step reads (q_addr repeats the last one up to 8)
-    const uint32_t np = q.phase == Q_AUX ? (!(q.node & PT_LEAFQ) ? 8u : q.li == 0u ? 4u : (q.li & 0x80000000u) ? 5u : 3u)
-                                         : q.walk == R_CAND ? 3u : q.walk == R_WALK_E ? 1u : 8u;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        if ((uint32_t)k < np) r[k] = blob_piece(S, off[k]);
-#else
 #pragma unroll
     for (int k = 0; k < 8; ++k) r[k] = blob_piece(S, off[k]);
-#endif
     q_exec(S, q, C, stk, r);
 }
 

@@ -31,10 +31,21 @@
 
 namespace pt {
 
-// the pixel of an owned slot (slot = local tile * 256 + lane)
-__device__ __forceinline__ void slot_xy(const TileMap& tm, uint32_t slot, uint32_t& x, uint32_t& y) {
-    slot_pixel(tm, slot >> 8, slot & 255u, x, y);
+#ifdef PT_WPROF
+// diagnostics builds: shader-clock stamp that no memory operation crosses
+__device__ __forceinline__ uint64_t pf_now() {
+    uint64_t t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
 }
+#define PF_WAIT4(a) asm volatile("" ::"v"((a).x), "v"((a).y), "v"((a).z), "v"((a).w) : "memory")
+#define PF_ARGS , uint64_t* pf
+#define PF_PASS , pf
+#else
+#define PF_ARGS
+#define PF_PASS
+#endif
+
 
 // enqueue a fresh ray with its plane result (RayIntersection's plane loop)
 __device__ __forceinline__ void push_ray(const WaveParams& P, const RayQ& Q, uint32_t qi, const Ray& ray,
@@ -61,8 +72,15 @@ __device__ __forceinline__ Ray camera_sample(const CamView& cam, Rng& R, uint32_
 // to the chain's next ray (the child, or the next sample's camera ray); false
 // when the pixel has reached this pass's target.  `ray` enters as the query ray.
 // `sdone` returns whether a sample of the pixel ended here.
-__device__ __forceinline__ bool shade_item(const WaveParams& P, uint32_t slot, Ray& ray, uint32_t hid, bool& sdone) {
+__device__ __forceinline__ bool shade_item(const WaveParams& P, uint32_t slot, Ray& ray, uint32_t hid,
+                                           bool& sdone PF_ARGS) {
     bool emit = false;
+#ifdef PT_WPROF
+    uint64_t pt0 = pf_now();
+#define PF_MARK(i) do { const uint64_t n_ = pf_now(); pf[i] += n_ - pt0; pt0 = n_; } while (0)
+#else
+#define PF_MARK(i) (void)0
+#endif
     PixelHot hot = load_hot(P.st, slot);     // one 16-B load: RNG, vertex count, samples done
     uint32_t nv = hot.nv;
     uint32_t end = PE_LIVE;
@@ -74,9 +92,11 @@ __device__ __forceinline__ bool shade_item(const WaveParams& P, uint32_t slot, R
         // (the query's own test, same operations -> same bits)
         Hit h;
         (void)prim_intersect(P.S.prims[hid], ray, h);
+        PF_MARK(0);   // pixel record + prim loads, the hit recomputed
         uint32_t idm;
         float s1, s2;
         const bool cont = shade_vertex(P.S, R, ray, h, (int)hid, idm, s1, s2);
+        PF_MARK(1);   // the vertex: material, sampling, pdfs
         HbmVStore vs = fold_store(P.st, slot);
         vs.put(nv, idm, s1, s2);
         ++nv;
@@ -95,27 +115,27 @@ __device__ __forceinline__ bool shade_item(const WaveParams& P, uint32_t slot, R
             vs.get(k - 1u, idm, s1, s2);
             L = fold_vertex(P.S, L, idm, s1, s2);
         }
-        store_sum(P.st, slot, load_sum(P.st, slot) + L);   // src/scene.cpp:198 sum += RayTrace(...)
+        uint32_t pix;
+        const f3 sum = load_sum_pix(P.st, slot, pix);
+        store_sum(P.st, slot, sum + L, pix);   // src/scene.cpp:198 sum += RayTrace(...)
+        PF_MARK(2);   // backward fold + sum
         const uint32_t done = hot.done + 1u;
         hot.done = done;
         nv = 0u;
         if (done < P.target) {
             // the pixel's next sample: jitter draws + camera ray
-            uint32_t x, y;
-            slot_xy(P.tm, slot, x, y);
-            ray = camera_sample(P.cam, R, x, y);
+            ray = camera_sample(P.cam, R, pix % P.tm.W, pix / P.tm.W);
             emit = true;
         }
     }
     hot.nv = nv;
     hot.R = R;
     store_hot(P.st, slot, hot);               // one 16-B store
+    PF_MARK(3);   // next sample's camera ray, record store
     return emit;
 }
+#undef PF_MARK
 
-#ifndef PT_SEED_DEPTH
-#define PT_SEED_DEPTH 2               // k_wcamera: aux BVH levels of the costly-class test
-#endif
 __global__ void __launch_bounds__(256) k_wcamera(WaveParams P) {
     // blocks append in about block order: the queue follows tile_order (Z-order of
     // the tiles, so the pixels resident together form compact image regions)
@@ -136,7 +156,7 @@ __global__ void __launch_bounds__(256) k_wcamera(WaveParams P) {
                 (void)camera_sample(P.cam, R, x, y);
                 sum = sum + mk3(0.f, 0.f, 0.f);
             }
-            store_sum(P.st, slot, sum);
+            store_sum(P.st, slot, sum, y * P.tm.W + x);
         } else if (done < P.target) {
             ray = camera_sample(P.cam, R, x, y);
             want = true;
@@ -157,7 +177,6 @@ __global__ void __launch_bounds__(256) k_wcamera(WaveParams P) {
         const f3 oinv = mk3(ray.o.x * rinv.x, ray.o.y * rinv.y, ray.o.z * rinv.z);
         for (uint32_t k = 0; k < PT_AUXW && k < P.n_aux; ++k) {
             const AuxSL e = P.aux[k];
-#if PT_SEED_DEPTH > 1
             const uint32_t code = f2u(e.b.w);
             if (code == 0xffffffffu || !aux_box(e.a.x, e.a.y, e.a.z, e.a.w, e.b.x, e.b.y, rinv, oinv)) continue;
             if (code & 0x80000000u) {
@@ -168,9 +187,6 @@ __global__ void __launch_bounds__(256) k_wcamera(WaveParams P) {
                 const AuxSL c = P.aux[code * PT_AUXW + j];
                 front = front || (f2u(c.b.w) != 0xffffffffu && aux_box(c.a.x, c.a.y, c.a.z, c.a.w, c.b.x, c.b.y, rinv, oinv));
             }
-#else
-            front = front || aux_box(e.a.x, e.a.y, e.a.z, e.a.w, e.b.x, e.b.y, rinv, oinv);
-#endif
         }
     }
     __shared__ uint32_t agg[5];
@@ -194,15 +210,9 @@ __global__ void __launch_bounds__(256) k_wcamera_merge(WaveParams P) {
     if (blockIdx.x == 0u && threadIdx.x == 0u) ctl[C_FRESH] = nf + nb;
 }
 
-#ifndef PT_VOTE
-#define PT_VOTE 0
-#endif
 #define PT_SUSPENDED 0xfffffffeu   // done.id of a query suspended to the next round
 #ifndef PT_BATCH
 #define PT_BATCH 64u        // queue indices a wave takes per atomic
-#endif
-#ifndef PT_REFILL_MIN
-#define PT_REFILL_MIN 4u    // idle lanes before a wave refills
 #endif
 
 // ---- path engine -------------------------------------------------------------
@@ -247,36 +257,7 @@ struct PathRing {
     F4* dq_rd;                    //                               {d.xyz, u32 closest prim | 0xffffffff}
 };
 
-#ifndef PT_PVOTE
-#define PT_PVOTE 1                 // one replay step kind per trip, round-robin over the kinds present
-#endif
-#ifndef PT_SHADE_MIN
-#define PT_SHADE_MIN 1u            // shade batches smaller than this may be held back ...
-#endif
-#ifndef PT_SHADE_DIV
-#define PT_SHADE_DIV 4u            // ... while more than PT_SHADE_DIV x the batch chains are resident ...
-#endif
-#ifndef PT_SHADE_WAIT
-#define PT_SHADE_WAIT 2000u        // ... for at most this many shader clocks
-#endif
-#ifndef PT_ROTATE_SHADE
-#define PT_ROTATE_SHADE 0          // 1: the shade wave's index rotates with blockIdx.x
-#endif
-#ifndef PT_PVOTE_K
-#define PT_PVOTE_K 1               // replay step kinds served per trip (round-robin)
-#endif
-#ifndef PT_PVOTE_SPARSE
-#define PT_PVOTE_SPARSE 0u         // running queries at or below which a wave runs every step kind
-#endif
-#ifndef PT_PATH_REFILL_MIN
 #define PT_PATH_REFILL_MIN 8u      // idle lanes before a query wave refills (any, once the round's work is out)
-#endif
-#ifndef PT_SHADE_PRIO
-#define PT_SHADE_PRIO 0            // issue priority (s_setprio 0-3) of the shade wave ...
-#endif
-#ifndef PT_QUERY_PRIO
-#define PT_QUERY_PRIO 0            // ... and of the query waves, against the other waves of their SIMD
-#endif
 #define PT_NOWORK 0xffffffffu
 #define PT_CAPPED 0xfffffffeu
 
@@ -309,9 +290,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     uint32_t wpost = 0u;              // trips since the round's work ran out
     uint32_t trip = 0u;
     const uint32_t wq = qw;                 // this query wave's done ring
-#if PT_PVOTE
     uint32_t rr = 0u;                       // replay step kind served last
-#endif
     const uint32_t dq_base = wq * PT_CMAX;
     uint32_t dq_res = 0u;                   // done-ring entries reserved (and written)
     uint32_t dq_pend = 0u, dq_pub = 0u;     // ... written before this trip / published
@@ -324,6 +303,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     uint64_t pf_trips = 0, pf_act = 0, pf_sleep = 0, pf_ring = 0, pf_pulled = 0, pf_exit_budget = 0, pf_res = 0,
              pf_dq = 0, pf_rq = 0, pf_tripcyc = 0, pf_qlat = 0, pf_qn = 0, pf_qsteps = 0, pf_refillcyc = 0;
     uint64_t pf_stepcyc = 0, pf_auxtrips = 0, pf_picktrips = 0, pf_stepped = 0, pf_donecyc = 0;
+    uint64_t pf_ldcyc = 0, pf_excyc = 0, pf_rfdata = 0, pf_rftrips = 0;
     uint64_t pf_t0 = __builtin_amdgcn_s_memtime(), pf_qstart = 0;
     uint32_t pf_qs = 0;
 #endif
@@ -442,6 +422,9 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 given += take;
             }
             if (src == 2u) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#ifdef PT_WPROF
+            const uint64_t pf_r0 = __ballot(src != 0u) ? pf_now() : 0;
+#endif
             if (src == 1u && gi < n_carry) {
                 // resume a suspended query: state, slot, then its aux stack into LDS
                 const uint32_t* w = CQ + (size_t)gi * P.carry_words;
@@ -466,6 +449,9 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                     pid = G.rq_pid[gi];
                     pre = G.rq_ri[gi];
                 }
+#ifdef PT_WPROF
+                PF_WAIT4(o); PF_WAIT4(d); PF_WAIT4(pre);
+#endif
                 Ray ray;
                 ray.o = mk3(o.x, o.y, o.z);
                 ray.d = mk3(d.x, d.y, d.z);
@@ -480,6 +466,12 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 if (q.phase == Q_EXACT) init_exact++;
                 active = true;
             }
+#ifdef PT_WPROF
+            if (pf_r0) {
+                pf_rfdata += pf_now() - pf_r0;
+                pf_rftrips++;
+            }
+#endif
         }
         if (__ballot(active) == 0ull) {
 #ifdef PT_WPROF
@@ -494,7 +486,6 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
 #ifdef PT_WPROF
         const uint64_t pf_s0 = __builtin_amdgcn_s_memtime();
 #endif
-#if PT_PVOTE
         if constexpr (SPARSE) {
 #pragma unroll 1
             for (uint32_t it = 0; it < P.sparse_steps; ++it) {
@@ -510,30 +501,38 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
 #pragma unroll
             for (uint32_t k = 1; k <= PT_RKINDS; ++k)
                 if (__ballot(kind == k) != 0ull) present |= 1u << k;
-            uint32_t pick = 0u, pick2 = 0u;
+            uint32_t pick = 0u;
 #pragma unroll
             for (uint32_t j = 1; j <= PT_RKINDS; ++j) {
                 const uint32_t c = (rr + j - 1u) % PT_RKINDS + 1u;
-                if ((present >> c) & 1u) {
-                    if (pick == 0u) pick = c;
-                    else if (PT_PVOTE_K > 1 && pick2 == 0u) pick2 = c;
-                }
+                if (pick == 0u && ((present >> c) & 1u)) pick = c;
             }
-            if (pick) rr = pick2 ? pick2 : pick;
+            if (pick) rr = pick;
 #ifdef PT_WPROF
             if (__ballot(kind == 0u) != 0ull) pf_auxtrips++;
             if (pick) pf_picktrips++;
             pf_stepped += (uint64_t)__popcll(__ballot(kind == 0u || kind == pick));
 #endif
-            // a sparse wave (few running queries) is bound by its chains' latency, not by
-            // issue: it runs every kind present
-            const bool run = 64u - nidle <= PT_PVOTE_SPARSE ? kind != 7u
-                                                            : (kind == 0u || kind == pick || (pick2 && kind == pick2));
-            if (run) q_step(P.S, q, C, stk);
-        }
+#ifdef PT_WPROF
+            if (kind == 0u || kind == pick) {
+                const uint64_t ta = pf_now();
+                uint32_t off[8];
+                q_addr(P.S, q, off);
+                F4 r[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) r[k] = blob_piece(P.S, off[k]);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) PF_WAIT4(r[k]);
+                const uint64_t tb = pf_now();
+                q_exec(P.S, q, C, stk, r);
+                const uint64_t tc = pf_now();
+                pf_ldcyc += tb - ta;
+                pf_excyc += tc - tb;
+            }
 #else
-        if (active && (q.phase == Q_AUX || q.phase == Q_REPLAY)) q_step(P.S, q, C, stk);
+            if (kind == 0u || kind == pick) q_step(P.S, q, C, stk);
 #endif
+        }
 #ifdef PT_WPROF
         const uint64_t pf_s1 = __builtin_amdgcn_s_memtime();
         pf_stepcyc += pf_s1 - pf_s0;
@@ -592,7 +591,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     wave_add_u64(ctr + 7, init_exact);
 #ifdef PT_WPROF
     if (P.wg_prof && lane_id() == 0u) {
-        unsigned long long* w = P.wg_prof + 32ull * blockIdx.x;
+        unsigned long long* w = P.wg_prof + 64ull * blockIdx.x;
         atomicAdd(w + 2, pf_trips);
         atomicAdd(w + 3, pf_act);
         atomicAdd(w + 4, pf_sleep);
@@ -610,9 +609,13 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
         atomicAdd(w + 24, pf_picktrips);
         atomicAdd(w + 25, pf_stepped);
         atomicAdd(w + 26, pf_donecyc);
+        atomicAdd(w + 32, pf_ldcyc);
+        atomicAdd(w + 33, pf_excyc);
+        atomicAdd(w + 34, pf_rfdata);
+        atomicAdd(w + 35, pf_rftrips);
     }
     if (P.wg_prof) {
-        unsigned long long* w = P.wg_prof + 32ull * blockIdx.x;
+        unsigned long long* w = P.wg_prof + 64ull * blockIdx.x;
         wave_add_u64(w + 17, pf_qlat);
         wave_add_u64(w + 18, pf_qn);
         wave_add_u64(w + 19, pf_qsteps);
@@ -632,11 +635,10 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
     for (uint32_t w = 0; w < PT_NQ; ++w) head[w] = 0u;
     uint32_t tail = 0u;               // ray ring published
 #ifdef PT_WPROF
-    uint64_t pf_batches = 0, pf_items = 0, pf_spin = 0, pf_cyc = 0, pf_shc = 0, pf_pushc = 0;
+    uint64_t pf_batches = 0, pf_items = 0, pf_spin = 0, pf_cyc = 0, pf_shc = 0, pf_pushc = 0, pf_rdc = 0;
+    uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // shade_item phases
 #endif
     uint32_t prog = 0u;               // finished samples not yet added to P.progress
-    bool waiting = false;             // holding back a small batch (since wait_t0)
-    uint64_t wait_t0 = 0;
     for (;;) {
         // published entries of the done rings (ring indices are compile-time: no scratch)
         uint32_t av[PT_NQ], total = 0u;
@@ -660,21 +662,6 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
-        // A shade batch costs about the same for 1 or 64 items.  With many chains in
-        // flight (more results are on their way) hold a small batch back briefly.
-        if (total < PT_SHADE_MIN && lds_read(L.qw_done) != PT_NQ &&
-            total * PT_SHADE_DIV < (uint32_t)__builtin_amdgcn_readfirstlane(lds_read(L.resident))) {
-            const uint64_t now = __builtin_amdgcn_s_memtime();
-            if (!waiting) {
-                waiting = true;
-                wait_t0 = now;
-            }
-            if (now - wait_t0 < PT_SHADE_WAIT) {
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-        }
-        waiting = false;
         // up to 64 of them, rings in order (a ring is never starved for long: its
         // producer's chains are the ones the other rings are not holding)
         uint32_t take[PT_NQ], n = 0u;
@@ -707,10 +694,14 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
 #endif
         if (have) {
             const F4 o = G.dq_ro[j], d = G.dq_rd[j];
+#ifdef PT_WPROF
+            PF_WAIT4(o); PF_WAIT4(d);
+            pf_rdc += pf_now() - c1;
+#endif
             slot = f2u(o.w);
             ray.o = mk3(o.x, o.y, o.z);
             ray.d = mk3(d.x, d.y, d.z);
-            emit = shade_item(P, slot, ray, f2u(d.w), sdone);
+            emit = shade_item(P, slot, ray, f2u(d.w), sdone PF_PASS);
         }
 #ifdef PT_WPROF
         const uint64_t c2 = __builtin_amdgcn_s_memtime();
@@ -748,13 +739,15 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
     }
 #ifdef PT_WPROF
     if (P.wg_prof && lane == 0u) {
-        unsigned long long* w = P.wg_prof + 32ull * blockIdx.x;
+        unsigned long long* w = P.wg_prof + 64ull * blockIdx.x;
         w[7] = pf_batches;
         w[8] = pf_items;
         w[9] = pf_spin;
         w[10] = pf_cyc;
         w[27] = pf_shc;
         w[28] = pf_pushc;
+        w[36] = pf_rdc;
+        for (int i = 0; i < 8; ++i) w[40 + i] = pf[i];
 
         w[1] = __builtin_amdgcn_s_memrealtime();
     }
@@ -766,21 +759,14 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
     for (uint32_t b = h; b < tail; b += 64u) {
         const uint32_t i = b + lane;
         const bool has = i < tail;
-        F4 o, d, pre;
-        int pid = -1;
-        if (has) {
-            const uint32_t e = i % PT_CMAX;
-            o = G.rq_ro[e];
-            d = G.rq_rd[e];
-            pid = G.rq_pid[e];
-            pre = G.rq_ri[e];
-        }
+        // (the append first: ring values held across its atomic would live in scratch)
         const uint32_t k = wave_append(out + C_FRESH, has);
         if (has) {
-            N.ro[k] = o;
-            N.rd[k] = d;
-            N.pid[k] = pid;
-            N.ri[k] = pre;
+            const uint32_t e = i % PT_CMAX;
+            N.ro[k] = G.rq_ro[e];
+            N.rd[k] = G.rq_rd[e];
+            N.pid[k] = G.rq_pid[e];
+            N.ri[k] = G.rq_ri[e];
         }
     }
 }
@@ -797,25 +783,13 @@ __global__ void __launch_bounds__(PT_PATH_WG) __attribute__((amdgpu_waves_per_eu
     }
     if (threadIdx.x < PT_NQ) L.dq_tail[threadIdx.x] = L.dq_head[threadIdx.x] = 0u;
 #ifdef PT_WPROF
-    if (P.wg_prof && threadIdx.x == 0u) P.wg_prof[32ull * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    if (P.wg_prof && threadIdx.x == 0u) P.wg_prof[64ull * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
 #endif
     __syncthreads();
-#ifndef PT_PATH_ONLY
-    // which wave shades: rotated over the workgroups (PT_ROTATE_SHADE), so the
-    // shade waves of a CU's workgroups do not all sit on one SIMD
-    const uint32_t wave = threadIdx.x >> 6, sw = PT_ROTATE_SHADE ? blockIdx.x % (PT_NQ + 1u) : PT_NQ;
-    if (wave == sw) {
-        if (PT_SHADE_PRIO) __builtin_amdgcn_s_setprio(PT_SHADE_PRIO);
-        path_shade_wave(P, L, G);
-    } else {
-        if (PT_QUERY_PRIO) __builtin_amdgcn_s_setprio(PT_QUERY_PRIO);
-        path_query_wave<SPARSE>(P, L, G, lds_stack, wave < sw ? wave : wave - 1u);
-    }
-#elif PT_PATH_ONLY == 1
-    path_query_wave<SPARSE>(P, L, G, lds_stack, threadIdx.x >> 6);
-#else
-    path_shade_wave(P, L, G);
-#endif
+    // waves 0 .. PT_NQ-1 query, wave PT_NQ shades
+    const uint32_t wave = threadIdx.x >> 6;
+    if (wave == PT_NQ) path_shade_wave(P, L, G);
+    else path_query_wave<SPARSE>(P, L, G, lds_stack, wave);
 }
 
 // ---- cooperative engine (end of a pass) ---------------------------------------
@@ -853,13 +827,26 @@ struct QcScene {
     AuxSL top[QC_TOPN * PT_AUXW];  // aux nodes 0..QC_TOPN-1
     uint32_t pl_id[QC_NPL];
 };
+// the first QC_NPL planes / QC_NEM emitters from the LDS copy, any further ones
+// (BIG: a scene beyond the tables) from HBM
+template <bool BIG>
 struct PlanesLds {
     const QcScene& Q;
-    __device__ Prim operator()(uint32_t k, uint32_t& pi) const { pi = Q.pl_id[k]; return Q.pl[k]; }
+    const SceneView& S;
+    __device__ Prim operator()(uint32_t k, uint32_t& pi) const {
+        if (!BIG || k < QC_NPL) {
+            pi = Q.pl_id[k];
+            return Q.pl[k];
+        }
+        pi = S.planes[k];
+        return S.prims[pi];
+    }
 };
+template <bool BIG>
 struct EmitLds {
     const QcScene& Q;
-    __device__ Prim operator()(uint32_t k) const { return Q.em[k]; }
+    const SceneView& S;
+    __device__ Prim operator()(uint32_t k) const { return !BIG || k < QC_NEM ? Q.em[k] : S.prims[S.emitters[k]]; }
 };
 
 // bvh_prim_intersect from the compact record (pt_query.h): a plain triangle (pos = +0,
@@ -897,7 +884,7 @@ __device__ __forceinline__ bool qc_prim_hit(const SceneView& S, uint32_t i, cons
 #endif
 
 // The query of one ray per team (every argument team-uniform; `on` = this team has
-// a query).  `reserve` = 4 (aux depth + 2): above SCAP - reserve pending nodes the
+// a query).  `reserve` = 3 (aux depth + 2): above SCAP - reserve pending nodes the
 // expansion takes fewer nodes per round, so a depth-first descent still fits.
 // Returns the closest prim (-1 none) and, for a BVH result, `hit` = its intersection
 // (t, n, side, from the same bvh_prim_intersect the consumer would repeat); `bvh`
@@ -972,7 +959,6 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
         if (__ballot(expand) == 0ull) break;
         uint32_t k = slim > ns ? (slim - ns) / 3u : 0u;
         k = k < 1u ? 1u : k;
-#if QC_LPE
         // 1. breadth-first expansion of the wide aux BVH: one node per PT_AUXW team
         //    lanes, a lane per entry (a round's instructions test one entry, not PT_AUXW)
         constexpr uint32_t KN = T / PT_AUXW;
@@ -1006,44 +992,6 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
             ns += (uint32_t)__popcll(mi);
             nc += (uint32_t)__popcll(ml);
         }
-#else
-        // 1. breadth-first expansion of the wide aux BVH: one node per team lane
-        k = k > T ? T : k;
-        k = k > ns ? ns : k;
-        if (!expand) k = 0u;
-        if (ns + 3u * k > SCAP) { ovf = true; k = 0u; }   // cannot happen with the host's reserve (checked)
-        ns -= k;
-        const bool act = tl < k;
-        const uint32_t node = act ? L.stk[ns + tl] : 0u;
-        C.aux += act ? 1u : 0u;
-        F4 r[2 * PT_AUXW];
-        if (node < QC_TOPN) {
-            // the top levels: the workgroup's LDS copy
-#pragma unroll
-            for (uint32_t e = 0; e < PT_AUXW; ++e) {
-                r[2 * e] = Q.top[node * PT_AUXW + e].a;
-                r[2 * e + 1] = Q.top[node * PT_AUXW + e].b;
-            }
-        } else {
-            const uint32_t b = S.o_aux + node * (uint32_t)(PT_AUXW * sizeof(AuxSL));
-#pragma unroll
-            for (uint32_t e = 0; e < 2u * PT_AUXW; ++e) r[e] = blob_piece(S, b + 16u * e);
-        }
-#pragma unroll
-        for (uint32_t e = 0; e < PT_AUXW; ++e) {
-            const F4 ea = r[2 * e], eb = r[2 * e + 1];
-            const uint32_t code = f2u(eb.w);
-            bool h = act && code != 0xffffffffu;
-            if (h) h = aux_entry_hit(ea, eb, ray, inv, oinv, pre.w);
-            const bool leaf = h && (code & 0x80000000u) != 0u;
-            const bool inner = h && (code & 0x80000000u) == 0u;
-            const unsigned long long mi = __ballot(inner) & tmask, ml = __ballot(leaf) & tmask;
-            if (inner) L.stk[ns + lanes_below(mi)] = code;
-            if (leaf) L.cand[nc + lanes_below(ml)] = code & 0x7fffffffu;
-            ns += (uint32_t)__popcll(mi);
-            nc += (uint32_t)__popcll(ml);
-        }
-#endif
     }
     QC_TICK(0);
     if (ovf) exact = true;
@@ -1161,12 +1109,13 @@ struct CoopPixel {
     Rng R;
     uint32_t nv, done;
     f3 sum;
+    uint32_t pix;   // global pixel index y*W + x
 };
 
 // shade_item for the cooperative engine (a team's first lane): the same vertex /
 // fold / next sample logic (src/scene.cpp:91-203), with the pixel state in
 // registers, the fold records in LDS and the hit handed over by the query
-template <class TL>
+template <bool BIG, class TL>
 __device__ __forceinline__ bool coop_shade(const WaveParams& P, const QcScene& Q, TL& L, CoopPixel& px,
                                            uint32_t slot, Ray& ray, int id, const Hit& h, bool& sdone) {
     bool emit = false;
@@ -1177,9 +1126,14 @@ __device__ __forceinline__ bool coop_shade(const WaveParams& P, const QcScene& Q
         uint32_t idm;
         float s1, s2;
         const Shade sh = P.S.shade[id];
-        const bool cont = shade_vertex_e(P.S, EmitLds{Q}, sh, px.R, ray, h, id, idm, s1, s2);
-        L.fold_sh[px.nv] = sh;
-        L.fold[px.nv] = make_uint4(idm, f2u(s1), f2u(s2), 0u);
+        const bool cont = shade_vertex_e(P.S, EmitLds<BIG>{Q, P.S}, sh, px.R, ray, h, id, idm, s1, s2);
+        if (!BIG || px.nv < QC_FOLD) {
+            L.fold_sh[px.nv] = sh;
+            L.fold[px.nv] = make_uint4(idm, f2u(s1), f2u(s2), 0u);
+        } else {
+            // a path deeper than the LDS records: the rest in the slot's HBM fold records
+            P.st.fold[(size_t)slot * P.st.depth + px.nv] = make_uint4(idm, f2u(s1), f2u(s2), 0u);
+        }
         ++px.nv;
         if (!cont) end = PE_TERM;
         else if (px.nv >= P.depth) end = PE_CUT;   // RayTrace(.., 0) = 0
@@ -1190,16 +1144,19 @@ __device__ __forceinline__ bool coop_shade(const WaveParams& P, const QcScene& Q
         // path over: backward fold (deepest vertex first), src/scene.cpp:198 sum += ...
         f3 Lr = end == PE_MISS ? P.S.bg : mk3(0.f, 0.f, 0.f);
         for (uint32_t k = px.nv; k > 0u; --k) {
-            const uint4 f = L.fold[k - 1u];
-            Lr = fold_vertex_sh(L.fold_sh[k - 1u], Lr, f.x, u2f(f.y), u2f(f.z));
+            if (!BIG || k - 1u < QC_FOLD) {
+                const uint4 f = L.fold[k - 1u];
+                Lr = fold_vertex_sh(L.fold_sh[k - 1u], Lr, f.x, u2f(f.y), u2f(f.z));
+            } else {
+                const uint4 f = P.st.fold[(size_t)slot * P.st.depth + (k - 1u)];
+                Lr = fold_vertex_sh(P.S.shade[f.x & 0x3fffffffu], Lr, f.x, u2f(f.y), u2f(f.z));
+            }
         }
         px.sum = px.sum + Lr;
         px.done += 1u;
         px.nv = 0u;
         if (px.done < P.target) {
-            uint32_t x, y;
-            slot_xy(P.tm, slot, x, y);
-            ray = camera_sample(P.cam, px.R, x, y);
+            ray = camera_sample(P.cam, px.R, px.pix % P.tm.W, px.pix / P.tm.W);
             emit = true;
         }
     }
@@ -1209,7 +1166,10 @@ __device__ __forceinline__ bool coop_shade(const WaveParams& P, const QcScene& Q
 #ifndef QC_WAVES_PER_EU
 #define QC_WAVES_PER_EU 3
 #endif
-template <uint32_t T>
+// BIG: a scene beyond the LDS tables (RAY_DEPTH > QC_FOLD, more than QC_NPL planes
+// or QC_NEM emitters): the rest of them from HBM (a separate instantiation, so the
+// common case carries none of that code)
+template <uint32_t T, bool BIG>
 __global__ void __launch_bounds__(64u * QC_WAVES) __attribute__((amdgpu_waves_per_eu(QC_WAVES_PER_EU, QC_WAVES_PER_EU)))
 k_wcoop(WaveParams P) {
     __shared__ QcTeamLds<T> Ls[QC_WAVES * (64u / T)];
@@ -1217,9 +1177,10 @@ k_wcoop(WaveParams P) {
     const uint32_t lane = lane_id(), tl = lane % T, tbase = lane - tl;
     QcTeamLds<T>& L = Ls[(threadIdx.x >> 6) * (64u / T) + lane / T];
     {
-        // this launch's copies: planes, emitters, the aux BVH's top nodes (counts host-checked)
+        // this launch's copies: the first planes and emitters, the aux BVH's top nodes
         F4* q = reinterpret_cast<F4*>(&Q);
-        const uint32_t npl = P.S.n_planes * 5u, nem = P.S.n_emitters * 5u;
+        const uint32_t npl = (P.S.n_planes < QC_NPL ? P.S.n_planes : QC_NPL) * 5u;
+        const uint32_t nem = (P.S.n_emitters < QC_NEM ? P.S.n_emitters : QC_NEM) * 5u;
         const uint32_t ntop = (P.n_aux < QC_TOPN * PT_AUXW ? P.n_aux : QC_TOPN * PT_AUXW) * 2u;
         for (uint32_t i = threadIdx.x; i < npl; i += blockDim.x)
             q[i] = reinterpret_cast<const F4*>(P.S.prims + P.S.planes[i / 5u])[i % 5u];
@@ -1227,7 +1188,7 @@ k_wcoop(WaveParams P) {
             q[QC_NPL * 5u + i] = reinterpret_cast<const F4*>(P.S.prims + P.S.emitters[i / 5u])[i % 5u];
         for (uint32_t i = threadIdx.x; i < ntop; i += blockDim.x)
             q[(QC_NPL + QC_NEM) * 5u + i] = P.S.blob[P.S.o_aux / 16u + i];   // (the query-blob form)
-        if (threadIdx.x < P.S.n_planes) Q.pl_id[threadIdx.x] = P.S.planes[threadIdx.x];
+        if (threadIdx.x < P.S.n_planes && threadIdx.x < QC_NPL) Q.pl_id[threadIdx.x] = P.S.planes[threadIdx.x];
         __syncthreads();
     }
     const uint32_t* in = P.ctl + PT_CTL_SET * P.parity;
@@ -1254,17 +1215,13 @@ k_wcoop(WaveParams P) {
     px.R.saved_ok = 0u;
     px.nv = px.done = 0u;
     px.sum = mk3(0.f, 0.f, 0.f);
+    px.pix = 0u;
     for (;;) {
         // teams without a chain take the next one (queue order: carry, then fresh)
         const bool need = !have && !exhausted;
         if (__ballot(need) != 0ull) {
             uint32_t gi = wave_append(out + C_HEADS, need && tl == 0u);
             gi = __shfl(gi, (int)tbase, 64);
-            if (P.coop_stop) {
-                // chains held, for the hand-over to the next launch (coop_stop)
-                const uint32_t got = (uint32_t)__popcll(__ballot(need && tl == 0u && gi < n_total));
-                if (lane == 0u && got) atomicAdd(out + C_LIVE, got);
-            }
             if (need) {
                 if (gi >= n_total) {
                     exhausted = true;
@@ -1279,7 +1236,7 @@ k_wcoop(WaveParams P) {
                         const uint32_t* w = P.cq[P.parity] + (size_t)gi * P.carry_words;
                         ray = reinterpret_cast<const Query*>(w)->ray;
                         slot = w[sizeof(Query) / 4u];
-                        q_planes_e(P.S, PlanesLds{Q}, ray, Pt, pid);
+                        q_planes_e(P.S, PlanesLds<BIG>{Q, P.S}, ray, Pt, pid);
                         pre = q_prep(P.S, ray);
                     } else {
                         const uint32_t fi = gi - n_carry;
@@ -1298,9 +1255,10 @@ k_wcoop(WaveParams P) {
                     px.R = hot.R;
                     px.nv = hot.nv;
                     px.done = hot.done;
-                    px.sum = load_sum(P.st, slot);
-                    if (tl < hot.nv) {
-                        // the current path's vertices so far (written by the path engine)
+                    px.sum = load_sum_pix(P.st, slot, px.pix);
+                    if (tl < hot.nv && (!BIG || tl < QC_FOLD)) {
+                        // the current path's vertices so far (written by the path engine; any
+                        // beyond QC_FOLD stay in HBM)
                         const uint4 f = P.st.fold[(size_t)slot * P.st.depth + tl];
                         L.fold[tl] = f;
                         L.fold_sh[tl] = P.S.shade[f.x & 0x3fffffffu];
@@ -1323,66 +1281,34 @@ k_wcoop(WaveParams P) {
             } else if (id >= 0 && !bvh) {
                 // the plane hit (its record from the LDS copy)
                 Prim pr = P.S.prims[id];
-                for (uint32_t k = 0; k < P.S.n_planes; ++k)
+                for (uint32_t k = 0; k < P.S.n_planes && (!BIG || k < QC_NPL); ++k)
                     if (Q.pl_id[k] == (uint32_t)id) pr = Q.pl[k];
                 (void)prim_intersect(pr, ray, h);
             }
-            emit = coop_shade(P, Q, L, px, slot, ray, id, h, sdone);
+            emit = coop_shade<BIG>(P, Q, L, px, slot, ray, id, h, sdone);
             prog += sdone ? 1u : 0u;
             if (emit) { rays++; C.planes += P.S.n_planes; }
         }
         emit = __shfl(emit ? 1 : 0, (int)tbase, 64) != 0;
         QC_TICK(3);
-        // hand-over: once every chain has been taken and few are left, they leave for the
-        // next launch (whole-wave teams: a shorter chain cycle) at this cycle boundary
-        bool leave = false;
-        if (P.coop_stop && __ballot(have) != 0ull) {
-            uint32_t lv = 0u, hd = 0u;
-            const uint32_t fin = (uint32_t)__popcll(__ballot(have && !emit && tl == 0u));
-            if (lane == 0u) {
-                if (fin) atomicSub(out + C_LIVE, fin);
-                lv = __hip_atomic_load(out + C_LIVE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                hd = __hip_atomic_load(out + C_HEADS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            lv = __builtin_amdgcn_readfirstlane(lv);
-            hd = __builtin_amdgcn_readfirstlane(hd);
-            leave = hd >= n_total && lv <= P.coop_stop;
-        }
-        if (have && (!emit || leave)) {
-            // the pixel's state back to HBM: at the pass target, or (leave) mid-path with its
-            // fold records, its next ray going to the next round's fresh queue
+        if (have && !emit) {
+            // the pixel has reached the pass target: its state back to HBM
             if (tl == 0u) {
                 PixelHot hot;
                 hot.R = px.R;
                 hot.nv = px.nv;
                 hot.done = px.done;
                 store_hot(P.st, slot, hot);
-                store_sum(P.st, slot, px.sum);
+                store_sum(P.st, slot, px.sum, px.pix);
             }
-            if (emit) {
-                const uint32_t nv = (uint32_t)__shfl((int)px.nv, (int)tbase, 64);
-                if (tl < nv) P.st.fold[(size_t)slot * P.st.depth + tl] = L.fold[tl];
-            }
+            have = false;
         }
-        if (leave) {
-            const bool go = have && emit && tl == 0u;
-            const uint32_t k = wave_append(out + C_FRESH, go);
-            if (go) {
-                push_ray(P, P.fq[1u - P.parity], k, ray, slot);
-                rays--;                          // counted again when the next launch takes it
-                C.planes -= P.S.n_planes;
-            }
-            const uint32_t ng = (uint32_t)__popcll(__ballot(go));
-            if (lane == 0u && ng) atomicSub(out + C_LIVE, ng);
-            emit = false;
-        }
-        if (have && !emit) have = false;
         if (__ballot(have) != 0ull) {
             // the chains' next rays (the first lanes'), plane tests and query set-up on every lane
             ray.o = mk3(__shfl(ray.o.x, (int)tbase, 64), __shfl(ray.o.y, (int)tbase, 64), __shfl(ray.o.z, (int)tbase, 64));
             ray.d = mk3(__shfl(ray.d.x, (int)tbase, 64), __shfl(ray.d.y, (int)tbase, 64), __shfl(ray.d.z, (int)tbase, 64));
             if (have) {
-                q_planes_e(P.S, PlanesLds{Q}, ray, Pt, pid);
+                q_planes_e(P.S, PlanesLds<BIG>{Q, P.S}, ray, Pt, pid);
                 pre = q_prep(P.S, ray);
             }
 #ifdef PT_CPROF
@@ -1449,6 +1375,9 @@ __global__ void __launch_bounds__(64) k_wexact(WaveParams P) {
 
 __global__ void __launch_bounds__(256) k_wshade(WaveParams P) {
     __shared__ uint32_t agg[5];
+#ifdef PT_WPROF
+    uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     uint32_t* out = P.ctl + PT_CTL_SET * (1u - P.parity);
     // the exact-DFS results of this round (the path engine shades everything else itself)
     const uint32_t n = out[C_EXACT];
@@ -1466,7 +1395,7 @@ __global__ void __launch_bounds__(256) k_wshade(WaveParams P) {
             slot = f2u(o.w);
             ray.o = mk3(o.x, o.y, o.z);
             ray.d = mk3(d.x, d.y, d.z);
-            emit = shade_item(P, slot, ray, hid, sdone);
+            emit = shade_item(P, slot, ray, hid, sdone PF_PASS);
         }
         if (P.progress) {
             const uint32_t nd = (uint32_t)__popcll(__ballot(sdone));
@@ -1496,16 +1425,20 @@ hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t pt_launch_coop(pt::WaveParams p, uint32_t grid, uint32_t team, hipStream_t s, hipEvent_t e0,
+hipError_t pt_launch_coop(pt::WaveParams p, uint32_t grid, uint32_t team, bool big, hipStream_t s, hipEvent_t e0,
                           hipEvent_t e1) {
     hipError_t e = hipMemsetAsync(p.ctl + PT_CTL_SET * (1u - p.parity), 0, 4u * PT_CTL_SET, s);
     if (e != hipSuccess) return e;
     p.path = 1u;
     if (e0 && (e = hipEventRecord(e0, s)) != hipSuccess) return e;
-    if (team == 8u) hipLaunchKernelGGL(pt::k_wcoop<8u>, dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
-    else if (team == 16u) hipLaunchKernelGGL(pt::k_wcoop<16u>, dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
-    else if (team == 32u) hipLaunchKernelGGL(pt::k_wcoop<32u>, dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
-    else hipLaunchKernelGGL(pt::k_wcoop<64u>, dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
+    if (big) {
+        // (a scene beyond the LDS tables: teams of 8, or whole waves for deep trees)
+        if (team == 64u) hipLaunchKernelGGL((pt::k_wcoop<64u, true>), dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
+        else hipLaunchKernelGGL((pt::k_wcoop<8u, true>), dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
+    } else if (team == 8u) hipLaunchKernelGGL((pt::k_wcoop<8u, false>), dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
+    else if (team == 16u) hipLaunchKernelGGL((pt::k_wcoop<16u, false>), dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
+    else if (team == 32u) hipLaunchKernelGGL((pt::k_wcoop<32u, false>), dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
+    else hipLaunchKernelGGL((pt::k_wcoop<64u, false>), dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
     if (e1 && (e = hipEventRecord(e1, s)) != hipSuccess) return e;
     return hipGetLastError();
 }

@@ -78,12 +78,9 @@ const Rccl& rccl() {
 //   sparse_steps=N    steps per loop trip of the end-of-pass kernel
 //   coop=N            a round with at most N chains runs the cooperative engine (one wave
 //                     per chain) to the end of the pass (0: never)
-//   near_budget=N     path-engine round budget once the chains are at most near_k/4 x the
-//                     cooperative hand-over (0: the usual budget); near_k=K (default 8)
 //   round_batch=N     path rounds launched per chain count while the chains are far above
 //                     the hand-over (default 1)
 //   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
-//   coop_stop=N       the first cooperative launch hands its last N chains to whole-wave teams (0: never)
 //   cap=N             chains a workgroup may hold
 //   rowmajor=1        seed a pass in row-major tile order instead of Z-order
 //   variant=V         megakernel variant bits (1 filtered tests, 2 XCD-banded tiles)
@@ -94,6 +91,13 @@ const Rccl& rccl() {
 //   qengine=coop      host self-tests: the cooperative engine's query algorithm (pt_coop.h)
 //   prepstats=1       pt_scene_prepare's per-stage times on stderr
 std::string tune_str(const char* key) {
+    // the single-variable switches of earlier builds are ignored now: say so once
+    static const bool warned = [] {
+        for (const char* old : {"PT_ENGINE", "PT_PATH_BUDGET", "PT_STRAGGLER", "PT_QSTATS", "PT_WGPROF", "PT_COOP"})
+            if (getenv(old)) fprintf(stderr, "libpt: %s is ignored; use PT_TUNE=\"key=value,...\" (INTEGRATION.md)\n", old);
+        return true;
+    }();
+    (void)warned;
     const char* e = getenv("PT_TUNE");
     if (!e) return {};
     const std::string k = std::string(key) + "=";
@@ -193,8 +197,6 @@ struct pt_session {
     pt::F4* ring = nullptr;       // path engine: path_grid * PT_RING_F4
     uint32_t path_grid = 0, path_budget = 1024, path_runend = 0, path_sparse = 0, sparse_steps = 8;
     uint32_t coop_max = 0, coop_grid = 0, coop_reserve = 0;   // cooperative engine (k_wcoop) at the end of a pass
-    uint32_t coop_stop = 0;       // chains left when the first cooperative launch hands over to whole waves
-    uint32_t near_budget = 0, near_chains = 0;   // round budget near the cooperative hand-over
     uint32_t round_batch = 1;     // rounds launched per count while the chains are far above the hand-over
     uint32_t coop_team = 8;       // lanes per chain in the cooperative engine (pure-coop rate, teams of
                                   // 64 / 32 / 16 / 8: 283 / 392 / 572 / 815 Mray/s)
@@ -214,6 +216,8 @@ struct pt_session {
     uint64_t samples_done = 0;
     uint32_t deferred_spp = 0;    // wavefront engine: trace() calls not yet run (one pass at the next sync point)
     uint32_t* tile_order = nullptr;   // local tiles in Z-order of their image position (k_wcamera)
+    std::vector<uint32_t> gtiles;     // this rank's window tiles (local -> window tile), tm.gtile on the device
+    uint32_t* gtile_dev = nullptr;
     // optional progress report during a pass (pt_render's bar): finished samples,
     // counted by the kernels into host-mapped memory and polled at the round syncs
     std::function<void(uint64_t)> on_progress;
@@ -636,10 +640,19 @@ int finish_pending(pt_session* ss) {
     return PT_OK;
 }
 
+// the window tiles dealt to `rank` (pt_kernels.h tile_owner), ascending
+std::vector<uint32_t> rank_tiles(uint32_t n_tiles, uint32_t tiles_x, uint32_t rank, uint32_t world) {
+    std::vector<uint32_t> v;
+    v.reserve(n_tiles / world + 1);
+    for (uint32_t t = 0; t < n_tiles; ++t)
+        if (pt::tile_owner(t, tiles_x, world) == rank) v.push_back(t);
+    return v;
+}
+
 uint64_t owned_pixels(const pt_session* ss) {
     uint64_t px = 0;
     for (uint32_t t = 0; t < ss->n_tiles_local; ++t) {
-        const uint32_t gt = t * ss->tm.world + ss->tm.rank;
+        const uint32_t gt = ss->gtiles[t];
         const uint32_t tx = gt % ss->tm.tiles_x, ty = gt / ss->tm.tiles_x;
         const uint32_t w = std::min(16u, ss->tm.ww - tx * 16u), h = std::min(16u, ss->tm.wh - ty * 16u);
         px += (uint64_t)w * h;
@@ -866,6 +879,8 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
     if (o->world == 0 || o->rank >= o->world) return fail(PT_E_INVALID, "bad rank/world");
     if (s->hs.W == 0 || s->hs.H == 0) return fail(PT_E_SCENE, "zero image size");
     if ((uint64_t)s->hs.W * s->hs.H >= 2147483647ull) return fail(PT_E_SCENE, "image too large for per-pixel seeds");
+    // the slot record keeps the current path's vertex count in 24 bits (pt_devutil.h PixelHot)
+    if (s->hs.depth >= (1u << 24)) return fail(PT_E_SCENE, "RAY_DEPTH too large (at most 16777215)");
     int rc = check_device(o->device);
     if (rc) return rc;
     DevScene* ds = nullptr;
@@ -890,7 +905,8 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
     ss->tm.n_tiles = ss->tm.tiles_x * ((ss->tm.wh + 15u) / 16u);
     ss->tm.rank = o->rank;
     ss->tm.world = o->world;
-    ss->n_tiles_local = ss->tm.n_tiles > o->rank ? (ss->tm.n_tiles - o->rank + o->world - 1u) / o->world : 0u;
+    ss->gtiles = rank_tiles(ss->tm.n_tiles, ss->tm.tiles_x, o->rank, o->world);
+    ss->n_tiles_local = (uint32_t)ss->gtiles.size();
     ss->n_slots = ss->n_tiles_local * 256u;
     ss->cam = make_cam(s);
     auto cleanup = [&](int code) {
@@ -900,6 +916,11 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
     if (hipSetDevice(ss->dev) != hipSuccess) return cleanup(fail(PT_E_HIP, "hipSetDevice failed"));
     const size_t n = std::max<size_t>(ss->n_slots, 1);
     ss->st.depth = std::max<uint32_t>(ss->depth, 1u);
+    if (!ss->gtiles.empty() &&
+        (hipMalloc(&ss->gtile_dev, ss->gtiles.size() * 4) != hipSuccess ||
+         hipMemcpy(ss->gtile_dev, ss->gtiles.data(), ss->gtiles.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
+        return cleanup(fail(PT_E_OOM, "device allocation failed (tile list)"));
+    ss->tm.gtile = ss->gtile_dev;
     if (take_stream(ss->dev, &ss->stream) != hipSuccess ||
         hipMalloc(&ss->st.rec, 2 * n * sizeof(uint4)) != hipSuccess ||
         hipMalloc(&ss->st.fold, (size_t)ss->st.depth * n * sizeof(uint4)) != hipSuccess ||
@@ -908,7 +929,7 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         return cleanup(fail(PT_E_OOM, "device allocation failed"));
     ss->st.n_slots = ss->n_slots;
     // engine: the wavefront pipeline for the (filtered) replay traversal; the
-    // megakernel for the exact DFS and the division-form replay (PT_ENGINE=mega forces it)
+    // megakernel for the exact DFS and the division-form replay (PT_TUNE engine=mega forces it)
     ss->wave = o->traversal == PT_TRAVERSAL_REPLAY;
     if (tune_str("engine") == "mega") ss->wave = false;
     if (ss->wave) {
@@ -951,18 +972,15 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         ss->coop_max = cus * 192u;
         ss->coop_max = (uint32_t)std::max(0, tune_int("coop", (int)ss->coop_max));
         ss->coop_grid = cus * 8u;
-        // chains left when the first (narrow-team) launch hands over to whole-wave teams; off:
-        // letting the teams of 8 finish measured faster (1 / 4 / 12 / 32 / 64 k chains: rank-of-1
-        // 1,643 -> 1,592 / 1,543 / 1,555 / 1,605, rank-of-8 1,290 -> 1,267-1,283 Mray/s)
-        ss->coop_stop = (uint32_t)std::max(0, tune_int("coop_stop", 0));
         // (a depth-first descent below the expansion limit adds at most 3 entries per level)
         const uint32_t reserve = 3u * (s->auxsl_depth + 2u);
         ss->coop_team = (uint32_t)tune_int("coop_team", (int)ss->coop_team);
         if (ss->coop_team != 8u && ss->coop_team != 16u && ss->coop_team != 32u) ss->coop_team = 64u;
         const uint32_t scap = ss->coop_team == 64u ? 448u : ss->coop_team == 32u ? 192u : QC_SCAP_MIN;
         if (scap < reserve + 64u || s->max_stack > scap) ss->coop_team = 64u;   // deep trees: whole-wave teams
-        if (448u < reserve + 64u || s->max_stack > 448u || ss->depth > QC_FOLD || s->planes.size() > QC_NPL ||
-            s->emitters.size() > QC_NEM)
+        // (paths deeper than QC_FOLD keep their further fold records in HBM, planes and
+        // emitters beyond QC_NPL / QC_NEM come from HBM: no scene limit besides the stacks)
+        if (448u < reserve + 64u || s->max_stack > 448u)
             ss->coop_max = 0;
         else ss->coop_reserve = reserve;
         // with the cooperative engine the path engine never runs a round to the end:
@@ -971,9 +989,6 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // ... and the end-of-pass (sparse) path kernel, whose rounds are long, never runs
         // above the hand-over
         if (ss->coop_max && !tune_has("sparse")) ss->path_sparse = std::min(ss->path_sparse, ss->coop_max);
-        // round budget once the chains are at most near_k/4 x coop_max (0: the usual budget)
-        ss->near_budget = ss->coop_max ? (uint32_t)std::max(0, tune_int("near_budget", 0)) : 0u;
-        ss->near_chains = (uint32_t)((uint64_t)ss->coop_max * (uint32_t)std::max(4, tune_int("near_k", 8)) / 4u);
         ss->round_batch = (uint32_t)std::max(1, tune_int("round_batch", (int)ss->round_batch));
         if (hipMalloc(&ss->ring, (size_t)ss->path_grid * PT_RING_F4 * sizeof(pt::F4)) != hipSuccess)
             return cleanup(fail(PT_E_OOM, "device allocation failed (path rings)"));
@@ -982,7 +997,7 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
             // code of their tile coordinates
             std::vector<std::pair<uint64_t, uint32_t>> key(ss->n_tiles_local);
             for (uint32_t t = 0; t < ss->n_tiles_local; ++t) {
-                const uint32_t gt = t * ss->tm.world + ss->tm.rank;
+                const uint32_t gt = ss->gtiles[t];
                 const uint32_t tx = gt % ss->tm.tiles_x, ty = gt / ss->tm.tiles_x;
                 uint64_t m = 0;
                 for (int b = 0; b < 16; ++b)
@@ -1097,13 +1112,12 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     uint32_t chains = ss->n_slots;
     for (uint32_t guard = 0;; ++guard) {
         if (chains <= ss->coop_max) {
-            // the cooperative engine runs every remaining chain to the end of the pass: teams
-            // of coop_team lanes first; once the queue is empty and at most coop_stop chains are
-            // left, those move on to a second launch with whole-wave teams (shorter chain cycle)
-            for (uint32_t stage = 0; chains; ++stage) {
-                const uint32_t team = stage == 0 ? ss->coop_team : 64u;
+            // the cooperative engine runs every remaining chain to the end of the pass, one launch
+            {
+                // (a scene beyond the engine's LDS tables runs the BIG instantiation: teams of 8 or 64)
+                const bool big = ss->depth > QC_FOLD || s->planes.size() > QC_NPL || s->emitters.size() > QC_NEM;
+                const uint32_t team = big && ss->coop_team != 64u ? 8u : ss->coop_team;
                 wp.parity = p;
-                wp.coop_stop = stage == 0 && team != 64u ? ss->coop_stop : 0u;
                 hipEvent_t i0, i1;
                 HIP_TRY(hipEventCreate(&i0));
                 HIP_TRY(hipEventCreate(&i1));
@@ -1116,11 +1130,11 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 const uint32_t grid = std::max(1u, std::min(ss->coop_grid, (chains + per_wg - 1u) / per_wg));
                 const bool cprof = tune_has("cprof");   // -DPT_CPROF builds: per-phase cycles on stderr
                 if (cprof) {
-                    if (!ss->wg_prof) HIP_TRY(hipMalloc(&ss->wg_prof, 256ull * ss->path_grid));
+                    if (!ss->wg_prof) HIP_TRY(hipMalloc(&ss->wg_prof, 512ull * ss->path_grid));
                     HIP_TRY(hipMemsetAsync(ss->wg_prof, 0, 64, ss->stream));
                     wp.wg_prof = ss->wg_prof;
                 }
-                HIP_TRY(pt_launch_coop(wp, grid, team, ss->stream, i0, i1));
+                HIP_TRY(pt_launch_coop(wp, grid, team, big, ss->stream, i0, i1));
                 if (cprof) {
                     unsigned long long cp[8];
                     HIP_TRY(hipMemcpyAsync(cp, wp.wg_prof, 64, hipMemcpyDeviceToHost, ss->stream));
@@ -1146,22 +1160,18 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                     HIP_TRY(e);
                 }
                 HIP_TRY(hipStreamSynchronize(ss->stream));
-                if (ss->ctl_host[pt::C_CARRY] != 0u || (stage > 0 && ss->ctl_host[pt::C_FRESH] != 0u))
+                if (ss->ctl_host[pt::C_CARRY] != 0u || ss->ctl_host[pt::C_FRESH] != 0u)
                     return fail(PT_E_HIP, "cooperative engine left chains behind");
-                chains = ss->ctl_host[pt::C_FRESH];
             }
             break;
         }
-        // near the cooperative hand-over, shorter rounds: the host sees the chain count
-        // fall below coop_max sooner after it does
-        wp.path_budget = ss->near_budget && chains <= ss->near_chains ? ss->near_budget : ss->path_budget;
         for (uint32_t r = 0; r < batch; ++r) {
             wp.parity = p;
             const std::string wgps = tune_str("wgprof");
             const char* wgp = wgps.c_str();
             if (*wgp) {
                 // diagnostics: per-round path workgroup timelines (32 u64 each) appended to the file
-                const size_t wgb = 256ull * ss->path_grid;
+                const size_t wgb = 512ull * ss->path_grid;
                 if (!ss->wg_prof) HIP_TRY(hipMalloc(&ss->wg_prof, wgb));
                 HIP_TRY(hipMemsetAsync(ss->wg_prof, 0, wgb, ss->stream));
                 wp.wg_prof = ss->wg_prof;
@@ -1180,7 +1190,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 fprintf(stderr, "round %u: in fresh %u carry %u -> out fresh %u carry %u exact %u\n", ss->rounds,
                         cnt[0][pt::C_FRESH], cnt[0][pt::C_CARRY], cnt[1][pt::C_FRESH], cnt[1][pt::C_CARRY],
                         cnt[1][pt::C_EXACT]);
-                std::vector<unsigned long long> h(32ull * ss->path_grid);
+                std::vector<unsigned long long> h(64ull * ss->path_grid);
                 HIP_TRY(hipMemcpyAsync(h.data(), wp.wg_prof, h.size() * 8, hipMemcpyDeviceToHost, ss->stream));
                 HIP_TRY(hipStreamSynchronize(ss->stream));
                 if (FILE* f = fopen(wgp, "ab")) {
@@ -1407,6 +1417,7 @@ void pt_session_free(pt_session* ss) {
     (void)hipFree(ss->st.rec); (void)hipFree(ss->st.fold); (void)hipFree(ss->counters);
     (void)hipFree(ss->out); (void)hipFree(ss->rad); (void)hipFree(ss->wg_prof);
     (void)hipFree(ss->tile_order);
+    (void)hipFree(ss->gtile_dev);
     (void)hipFree(ss->qbuf); (void)hipFree(ss->hid); (void)hipFree(ss->pidbuf);
     (void)hipFree(ss->carry); (void)hipFree(ss->ctl); (void)hipFree(ss->ring);
     if (ss->ctl_host) (void)hipHostFree(ss->ctl_host);
@@ -1423,7 +1434,8 @@ int pt_unpack_tiles(uint32_t W, uint32_t H, uint32_t rank, uint32_t world, const
     if (!packed || !rgb || world == 0) return fail(PT_E_INVALID, "bad argument");
     const uint32_t tiles_x = (W + 15u) / 16u, n_tiles = tiles_x * ((H + 15u) / 16u);
     uint32_t lt = 0;
-    for (uint32_t gt = rank; gt < n_tiles; gt += world, ++lt) {
+    for (uint32_t gt = 0; gt < n_tiles; ++gt) {
+        if (pt::tile_owner(gt, tiles_x, world) != rank) continue;
         const uint32_t tx = gt % tiles_x, ty = gt / tiles_x;
         for (uint32_t j = 0; j < 16u; ++j) {
             const uint32_t y = ty * 16u + j;
@@ -1431,6 +1443,7 @@ int pt_unpack_tiles(uint32_t W, uint32_t H, uint32_t rank, uint32_t world, const
             const uint32_t x0 = tx * 16u, w = std::min(16u, W - x0);
             memcpy(rgb + ((size_t)y * W + x0) * 3, packed + ((size_t)lt * 256u + j * 16u) * 3, (size_t)w * 3);
         }
+        ++lt;
     }
     return PT_OK;
 }
@@ -1439,7 +1452,8 @@ int pt_unpack_tiles_f32(uint32_t W, uint32_t H, uint32_t rank, uint32_t world, c
     if (!packed || !rad || world == 0) return fail(PT_E_INVALID, "bad argument");
     const uint32_t tiles_x = (W + 15u) / 16u, n_tiles = tiles_x * ((H + 15u) / 16u);
     uint32_t lt = 0;
-    for (uint32_t gt = rank; gt < n_tiles; gt += world, ++lt) {
+    for (uint32_t gt = 0; gt < n_tiles; ++gt) {
+        if (pt::tile_owner(gt, tiles_x, world) != rank) continue;
         const uint32_t tx = gt % tiles_x, ty = gt / tiles_x;
         for (uint32_t j = 0; j < 16u; ++j) {
             const uint32_t y = ty * 16u + j;
@@ -1447,30 +1461,47 @@ int pt_unpack_tiles_f32(uint32_t W, uint32_t H, uint32_t rank, uint32_t world, c
             const uint32_t x0 = tx * 16u, w = std::min(16u, W - x0);
             memcpy(rad + ((size_t)y * W + x0) * 3, packed + ((size_t)lt * 256u + j * 16u) * 3, (size_t)w * 12);
         }
+        ++lt;
     }
     return PT_OK;
 }
 
 // ------------------------------------------------------------- render -----
 namespace {
-// One process driving several GPUs: the packed u8 tiles of every session are
-// gathered to the first device with one grouped ncclGather over xGMI
-// (communicator cached per device set), then un-interleaved on the host.
-int gather_rccl(const std::vector<pt_session*>& sess, int dev0, uint32_t W, uint32_t H, uint8_t* rgb) {
-    static std::mutex mu;
-    static std::map<std::pair<int, int>, std::vector<ncclComm_t>> comms;
-    std::lock_guard<std::mutex> lk(mu);
-    const int n = (int)sess.size();
+// RCCL communicators over devices dev0 .. dev0+n-1, created once per process and
+// device set (pt_gather_init may create one ahead of the render)
+std::mutex g_comm_mu;
+std::map<std::pair<int, int>, std::vector<ncclComm_t>> g_comms;
+int comm_get(int dev0, int n, std::vector<ncclComm_t>** out) {
+    // (caller holds g_comm_mu)
     auto key = std::make_pair(dev0, n);
-    if (!comms.count(key)) {
+    auto it = g_comms.find(key);
+    if (it == g_comms.end()) {
         std::vector<int> devs(n);
         for (int g = 0; g < n; ++g) devs[g] = dev0 + g;
         std::vector<ncclComm_t> c(n);
         if (!rccl().ok) return fail(PT_E_RCCL, "librccl.so.1 not loadable");
         if (rccl().CommInitAll(c.data(), n, devs.data()) != ncclSuccess) return fail(PT_E_RCCL, "ncclCommInitAll failed");
-        comms[key] = c;
+        it = g_comms.emplace(key, c).first;
     }
-    auto& c = comms[key];
+    *out = &it->second;
+    return PT_OK;
+}
+
+// Test-only (PT_TUNE same_device=1): pt_render(ngpu = n) runs its n sessions and
+// host threads all on `device` -- the in-process multi-GPU path on one GPU.  RCCL
+// cannot place two ranks on one device, so the framebuffer goes through the host.
+bool same_device() { return tune_int("same_device", 0) != 0; }
+
+// One process driving several GPUs: the packed u8 tiles of every session are
+// gathered to the first device with one grouped ncclGather over xGMI
+// (communicator cached per device set), then un-interleaved on the host.
+int gather_rccl(const std::vector<pt_session*>& sess, int dev0, uint32_t W, uint32_t H, uint8_t* rgb) {
+    std::lock_guard<std::mutex> lk(g_comm_mu);
+    const int n = (int)sess.size();
+    std::vector<ncclComm_t>* cp = nullptr;
+    if (const int rc = comm_get(dev0, n, &cp)) return rc;
+    auto& c = *cp;
     size_t cap = 0;
     for (auto* x : sess) cap = std::max<size_t>(cap, 3ull * x->n_slots);
     cap = std::max<size_t>(cap, 16);
@@ -1513,6 +1544,14 @@ int gather_rccl(const std::vector<pt_session*>& sess, int dev0, uint32_t W, uint
 }
 }  // namespace
 
+int pt_gather_init(int device, int ngpu) {
+    if (ngpu < 1 || device < 0) return fail(PT_E_INVALID, "bad device range");
+    if (same_device()) return PT_OK;   // (test-only mode: host gather)
+    std::lock_guard<std::mutex> lk(g_comm_mu);
+    std::vector<ncclComm_t>* c = nullptr;
+    return comm_get(device, ngpu, &c);
+}
+
 void pt_render_opts_default(pt_render_opts* o) {
     if (!o) return;
     memset(o, 0, sizeof(*o));
@@ -1537,9 +1576,10 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
         for (auto* x : sess) pt_session_free(x);
         return code;
     };
+    const bool same = same_device();
     for (int g = 0; g < ngpu; ++g) {
         pt_session_opts so;
-        so.device = o.device + g;
+        so.device = same ? o.device : o.device + g;
         so.rank = (uint32_t)g;
         so.world = (uint32_t)ngpu;
         so.traversal = o.traversal;
@@ -1601,7 +1641,7 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
     if (rgb) {
         // PT_GATHER_AUTO: RCCL when ngpu > 1 (host fallback with a warning);
         // PT_GATHER_RCCL: RCCL at any ngpu, an error if it fails; PT_GATHER_HOST: never RCCL
-        const bool try_rccl = o.gather == PT_GATHER_RCCL || (o.gather == PT_GATHER_AUTO && ngpu > 1);
+        const bool try_rccl = !same && (o.gather == PT_GATHER_RCCL || (o.gather == PT_GATHER_AUTO && ngpu > 1));
         if (try_rccl && (rc = gather_rccl(sess, o.device, W, H, rgb)) == PT_OK) {
             agg.gather_rccl = 1;
         } else {
@@ -1729,7 +1769,7 @@ int pt_selftest_render_host(pt_scene* s, int32_t traversal, uint32_t x0, uint32_
     const uint32_t nt = std::max(1u, std::thread::hardware_concurrency());
     std::vector<std::thread> th;
     std::vector<uint32_t> errs(nt, 0);
-    // diagnostics: PT_QSTATS=<file> dumps per-query {aux visits, node tests, prim tests, exact} (u32 x4)
+    // diagnostics: PT_TUNE qstats=<file> dumps per-query {aux visits, node tests, prim tests, exact} (u32 x4)
     const std::string qpaths = tune_str("qstats");
     const char* qpath = qpaths.empty() ? nullptr : qpaths.c_str();
     std::vector<std::vector<std::array<uint32_t, 4>>> qlogs(nt);

@@ -26,7 +26,7 @@ TRAVERSAL_REPLAY = 0
 TRAVERSAL_EXACT = 1
 TRAVERSAL_REPLAY_DIV = 2
 GATHER_AUTO, GATHER_RCCL, GATHER_HOST = 0, 1, 2
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # One HIP runtime per process: PyTorch bundles its own libamdhip64 (soname
 # libamdhip64.so.7, but its users link the unversioned name), so loading
@@ -83,6 +83,7 @@ _sig = {
     "pt_scene_load_mem": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(_P)]),
     "pt_scene_prepare": (C.c_int, [_P]),
     "pt_device_init": (C.c_int, [C.c_int]),
+    "pt_gather_init": (C.c_int, [C.c_int, C.c_int]),
     "pt_scene_get_info": (C.c_int, [_P, C.POINTER(SceneInfo)]),
     "pt_scene_override": (C.c_int, [_P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "pt_scene_dump_bvh": (C.c_int, [_P, _P, C.c_size_t, _P, C.c_size_t]),
@@ -272,6 +273,17 @@ class Session:
             self._h = None
 
     __del__ = close
+
+
+def tile_owner(t, tiles_x, world):
+    """the rank that owns window tile t (include/pt.h sessions; pt_kernels.h tile_owner)"""
+    return (t % tiles_x + t // tiles_x) % world
+
+
+def rank_tiles(width, height, rank, world):
+    """the window tiles of `rank`, in its local (ascending) order"""
+    tiles_x, tiles_y = (width + 15) // 16, (height + 15) // 16
+    return [t for t in range(tiles_x * tiles_y) if tile_owner(t, tiles_x, world) == rank]
 
 
 def unpack_tiles(packed, width, height, rank, world, out=None):

@@ -46,8 +46,9 @@ def _fmt(x):
     return "%.6g" % x
 
 
-def generate(src_text, W, H, S, subdivide, variant):
-    """Return the generated scene text (SURVEY.md §8(d) recipe)."""
+def generate(src_text, W, H, S, subdivide, variant, depth=None):
+    """Return the generated scene text (SURVEY.md §8(d) recipe); `depth`
+    replaces the RAY_DEPTH line (test fixtures only, not a pinned config)."""
     lines = src_text.split("\n")
     out = []
     extra = {"diffuse": [], "metal": ["METALLIC"], "glass": ["DIELECTRIC", "IOR 1.5"]}[variant]
@@ -62,6 +63,10 @@ def generate(src_text, W, H, S, subdivide, variant):
             continue
         if tok == "SAMPLES":
             out.append("SAMPLES %d" % S)
+            i += 1
+            continue
+        if tok == "RAY_DEPTH" and depth is not None:
+            out.append("RAY_DEPTH %d" % depth)
             i += 1
             continue
         if tok == "TRIANGLE" and (subdivide or extra):
@@ -112,10 +117,10 @@ def make(config, out_path, check=True):
     return got
 
 
-def make_custom(src, W, H, S, subdivide, variant, out_path):
+def make_custom(src, W, H, S, subdivide, variant, out_path, depth=None):
     with open(src, "r", newline="") as f:
         text = f.read()
-    res = generate(text, W, H, S, subdivide, variant).encode()
+    res = generate(text, W, H, S, subdivide, variant, depth).encode()
     with open(out_path, "wb") as f:
         f.write(res)
     return hashlib.md5(res).hexdigest()

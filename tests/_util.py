@@ -159,11 +159,13 @@ def scene_path(src, gen=None):
     if gen is None:
         return os.path.join(SCENES, src)
     base = make_scene.CONFIGS[src][0] if src in make_scene.CONFIGS else src
-    W, H, S, sub, var = gen
-    out = os.path.join(GEN, "%s_%d_%d_%d_%d_%s.txt" % (os.path.splitext(base)[0], W, H, S, int(sub), var))
+    W, H, S, sub, var = gen[:5]
+    depth = gen[5] if len(gen) > 5 else None   # optional RAY_DEPTH override
+    out = os.path.join(GEN, "%s_%d_%d_%d_%d_%s%s.txt" % (os.path.splitext(base)[0], W, H, S, int(sub), var,
+                                                       "_d%d" % depth if depth is not None else ""))
     with _lock:
         if not os.path.exists(out):
-            make_scene.make_custom(os.path.join(SCENES, base), W, H, S, sub, var, out + ".tmp")
+            make_scene.make_custom(os.path.join(SCENES, base), W, H, S, sub, var, out + ".tmp", depth)
             os.replace(out + ".tmp", out)
     return out
 

@@ -59,11 +59,32 @@ IMAGES = {
     "c4metal_s4_win_1010_470_16x16": ("c4_metal", (1920, 1080, 4, True, "metal"), (1010, 470, 16, 16)),
     "c4glass_s4_win_830_610_16x16": ("c4_glass", (1920, 1080, 4, True, "glass"), (830, 610, 16, 16)),
     # config 5 (3840x2160, pixel-tiled over 8 GPUs): windows whose 16x16 tiles belong to
-    # ranks 0, 2+3, 6 and 7 of 8 (global tile ty*240+tx, rank = tile % 8); seeds y*3840+x
+    # ranks 3, 5+6, 1 and 5 of 8 (tile (tx, ty) -> rank (tx + ty) % 8; until round 3 the
+    # deal was t % 8 -> ranks 0, 2+3, 6, 7); seeds y*3840+x
     "c5s4_win_1920_1072_16x16": ("c5", (3840, 2160, 4, True, "diffuse"), (1920, 1072, 16, 16)),
     "c5s4_win_1952_1072_32x16": ("c5", (3840, 2160, 4, True, "diffuse"), (1952, 1072, 32, 16)),
     "c5s4_win_1760_1200_16x16": ("c5", (3840, 2160, 4, True, "diffuse"), (1760, 1200, 16, 16)),
     "c5s4_win_3824_2144_16x16": ("c5", (3840, 2160, 4, True, "diffuse"), (3824, 2144, 16, 16)),
+}
+
+# Deep stream positions: windows of the benchmark configurations at their OWN spp
+# (c3 256, c4 1024, c5 4096), RAY_DEPTH 10 paths, and a scene beyond the
+# cooperative engine's LDS limits (10 planes, 10 box/ellipsoid emitters, depth 8).
+# Each gets the reference's image + radiance (ref_harness) and a ray count from the
+# CPU restatement (oracle/pt_oracle.cpp), whose image must equal the reference's
+# byte-for-byte here; the ray count is then the restatement's count of
+# Scene::RayIntersection calls for those same pixels.
+DEEP = {
+    "c3_win_944_520_16x16": ("c3", None, (944, 520, 16, 16)),
+    "c4metal_win_900_560_16x16": ("c4_metal", None, (900, 560, 16, 16)),
+    "c4glass_win_900_560_16x16": ("c4_glass", None, (900, 560, 16, 16)),
+    # config 5 tiles of ranks 3 and 5 of 8 (tile (tx, ty) -> rank (tx + ty) % 8)
+    "c5_win_1920_1072_8x8": ("c5", None, (1920, 1072, 8, 8)),
+    "c5_win_3832_2152_8x8": ("c5", None, (3832, 2152, 8, 8)),
+    "dragon_d10_metal_48x48x16": ("practice5_dragon_10k.txt", (48, 48, 16, False, "metal", 10), None),
+    "dragon_d10_glass_48x48x16": ("practice5_dragon_10k.txt", (48, 48, 16, False, "glass", 10), None),
+    "c4glass_d10_s16_win_900_560_16x16": ("c3", (1920, 1080, 16, True, "glass", 10), (900, 560, 16, 16)),
+    "many_lights_48x48x8": ("many_lights.txt", (48, 48, 8, False, "diffuse"), None),
 }
 
 RNG_SEEDS = [0, 1, 2, 12345, 262143, 2073599, 2147483646, 4294967295]
@@ -95,15 +116,17 @@ def scene_file(tmp, src, gen):
         base = make_scene.CONFIGS[src][0]
     else:
         base = src
-    W, H, S, sub, var = gen
-    out = os.path.join(tmp, "%s_%d_%d_%d_%d_%s.txt" % (os.path.splitext(base)[0], W, H, S, sub, var))
+    W, H, S, sub, var = gen[:5]
+    depth = gen[5] if len(gen) > 5 else None   # optional RAY_DEPTH override
+    out = os.path.join(tmp, "%s_%d_%d_%d_%d_%s%s.txt" % (os.path.splitext(base)[0], W, H, S, sub, var,
+                                                      "_d%d" % depth if depth is not None else ""))
     if not os.path.exists(out):
-        make_scene.make_custom(os.path.join(SCENES, base), W, H, S, sub, var, out)
+        make_scene.make_custom(os.path.join(SCENES, base), W, H, S, sub, var, out, depth)
     return out
 
 
-def render_image(harness, tmp, name):
-    src, gen, win = IMAGES[name]
+def render_image(harness, tmp, name, table=None):
+    src, gen, win = (table or IMAGES)[name]
     sc = scene_file(tmp, src, gen)
     ppm = os.path.join(HERE, "img_%s.ppm" % name)
     rad = os.path.join(HERE, "rad_%s.f32" % name)
@@ -122,12 +145,43 @@ def render_image(harness, tmp, name):
     return entry
 
 
+def render_deep(harness, tmp, name):
+    """A DEEP fixture: the reference's window + the restatement's ray count."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import _util as U
+    entry = render_image(harness, tmp, name, DEEP)
+    src, gen, win = DEEP[name]
+    sc = scene_file(tmp, src, gen)
+    o = U.OracleScene(sc)
+    x0, y0, w, h = win if win else (0, 0, None, None)
+    rgb, rad, ctr = o.render(x0, y0, w, h)
+    ref_rad = np.fromfile(os.path.join(HERE, "rad_%s.f32" % name), np.float32).reshape(rad.shape)
+    ref_img = U.read_ppm(os.path.join(HERE, "img_%s.ppm" % name))
+    assert np.array_equal(rad.view(np.uint32), ref_rad.view(np.uint32)), name + ": restatement radiance differs"
+    assert np.array_equal(rgb, ref_img), name + ": restatement image differs"
+    entry["rays"] = int(ctr["rays"])
+    print("deep", name, entry["rays"], "rays")
+    return entry
+
+
 def main():
     if not os.path.isdir("/root/reference/hw5"):
         print("reference not present; cannot regenerate fixtures", file=sys.stderr)
         return 1
     subprocess.check_call(["sh", os.path.join(REPO, "oracle", "build_ref.sh")])
     harness = os.path.join(REF, "ref_harness")
+    if len(sys.argv) > 1 and sys.argv[1] == "--deep":
+        # (re)generate the deep fixtures (all, or the named ones) in the existing manifest
+        with open(os.path.join(HERE, "manifest.json")) as f:
+            manifest = json.load(f)
+        deep = manifest.setdefault("deep", {})
+        with tempfile.TemporaryDirectory() as tmp:
+            for name in (sys.argv[2:] or list(DEEP)):
+                deep[name] = render_deep(harness, tmp, name)
+                with open(os.path.join(HERE, "manifest.json"), "w") as f:
+                    json.dump(manifest, f, indent=1, sort_keys=True)
+        return 0
     if len(sys.argv) > 2 and sys.argv[1] == "--images":
         # add / refresh only the named image fixtures in the existing manifest
         with open(os.path.join(HERE, "manifest.json")) as f:

@@ -1,6 +1,6 @@
 """Multi-rank path on CPU: world-size-2 gloo runs of bench.py's tile deal and
 framebuffer gather (the N>1 data path; on the GPU box the same code runs
-over RCCL).  Tiles are 16x16, tile t belongs to rank t % world
+over RCCL).  Tiles are 16x16, tile (tx, ty) belongs to rank (tx + ty) % world
 (include/pt.h sessions, bench.py gather_tiles)."""
 import importlib.util
 import json
@@ -37,7 +37,9 @@ def _packed_for_rank(img, rank, world):
     H, W, _ = img.shape
     tx, ty = (W + 15) // 16, (H + 15) // 16
     out = []
-    for gt in range(rank, tx * ty, world):
+    for gt in range(tx * ty):
+        if (gt % tx + gt // tx) % world != rank:
+            continue
         t = np.zeros((16, 16, 3), np.uint8)
         x0, y0 = (gt % tx) * 16, (gt // tx) * 16
         blk = img[y0:y0 + 16, x0:x0 + 16]

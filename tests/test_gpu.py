@@ -153,7 +153,7 @@ def test_device_init(pt):
     assert pt._lib.pt_device_init(4096) == pt.PT_E_NO_GPU
 
 
-@pytest.mark.parametrize("engine", ["coop64", "coop32", "coop16", "coop8", "coop8h", "path"])
+@pytest.mark.parametrize("engine", ["coop64", "coop32", "coop16", "coop8", "path"])
 @pytest.mark.parametrize("name", sorted(M["images"]))
 def test_golden_images_each_engine(pt, name, engine, monkeypatch):
     """The replay traversal with one engine for the whole pass: the cooperative
@@ -161,12 +161,9 @@ def test_golden_images_each_engine(pt, name, engine, monkeypatch):
     all candidate leaves at once, root paths a block of nodes per round;
     pt_coop.h) or the path engine alone (coop=0).  All must reproduce the
     reference's bytes and ray count."""
-    # coop8h: teams of 8, and every chain handed over to whole-wave teams (a second launch)
-    # after its first cycle, mid-path (pixel state, fold records and next ray via HBM)
     coop = engine.startswith("coop")
-    team = engine[4:].rstrip("h") if coop else "64"
-    stop = "100000000" if engine.endswith("h") else "0"
-    monkeypatch.setenv("PT_TUNE", "coop=%s,coop_team=%s,coop_stop=%s" % ("100000000" if coop else "0", team, stop))
+    team = engine[4:] if coop else "64"
+    monkeypatch.setenv("PT_TUNE", "coop=%s,coop_team=%s" % ("100000000" if coop else "0", team))
     m, img, rad = U.golden_image(name)
     with pt.Scene.load(U.golden_scene_path(name)) as s:
         s.prepare()
@@ -176,23 +173,21 @@ def test_golden_images_each_engine(pt, name, engine, monkeypatch):
     assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
     assert np.array_equal(rgb, img)
     if coop:
-        assert st["rounds"] == (2 if engine.endswith("h") else 1)
+        assert st["rounds"] == 1
 
 
-@pytest.mark.parametrize("team", ["64", "16", "8", "8h"])
+@pytest.mark.parametrize("team", ["64", "16", "8"])
 @pytest.mark.parametrize("cfg", ["c1", "c2"])
 def test_coop_engine_full_config_md5(pt, cfg, team, monkeypatch):
-    """Configs 1 and 2 entirely on the cooperative engine: reference md5 and ray count
-    (8h: teams of 8 handing their last 4,096 chains over to whole-wave teams)."""
-    monkeypatch.setenv("PT_TUNE", "coop=100000000,coop_team=%s,coop_stop=%s" % (team.rstrip("h"),
-                                                                                "4096" if team.endswith("h") else "0"))
+    """Configs 1 and 2 entirely on the cooperative engine: reference md5 and ray count."""
+    monkeypatch.setenv("PT_TUNE", "coop=100000000,coop_team=%s" % team)
     full = M["full"][cfg]
     with pt.Scene.load(U.scene_path(cfg)) as s:
         rgb, _, st = s.render()
         w, h = s.info["width"], s.info["height"]
     ppm = b"P6\n%d %d\n255\n" % (w, h) + rgb.tobytes()
     assert U.md5(ppm) == full["md5"]
-    assert st["rays"] == full["rays"] and st["rounds"] == (2 if team.endswith("h") else 1)
+    assert st["rays"] == full["rays"] and st["rounds"] == 1
 
 
 @pytest.mark.parametrize("engine", ["path", "path_dense", "path_coop"])
@@ -254,8 +249,8 @@ def test_config5_rank_of_8_sessions_vs_reference_windows(pt):
         x0, y0, w, h = m["window"]
         for ty in range(y0 // 16, (y0 + h + 15) // 16):
             for tx in range(x0 // 16, (x0 + w + 15) // 16):
-                owners.setdefault((ty * tiles_x + tx) % world, set()).add(n)
-    assert len(owners) >= 4   # the windows span several ranks (0, 2, 3, 6, 7)
+                owners.setdefault((tx + ty) % world, set()).add(n)
+    assert len(owners) >= 4   # the windows span several ranks (1, 3, 5, 6)
     rgb = np.zeros((H, W, 3), np.uint8)
     rad = np.zeros((H, W, 3), np.float32)
     covered = np.zeros((H, W), bool)
@@ -272,7 +267,7 @@ def test_config5_rank_of_8_sessions_vs_reference_windows(pt):
             pt.unpack_tiles(ss.read_packed(), W, H, r, world, out=rgb)
             pt.unpack_tiles_f32(drad.cpu().numpy(), W, H, r, world, out=rad)
             mine = np.zeros(((H + 15) // 16, tiles_x), bool)
-            mine.reshape(-1)[r::world] = True
+            mine.reshape(-1)[pt.rank_tiles(W, H, r, world)] = True
             covered |= np.repeat(np.repeat(mine, 16, 0), 16, 1)[:H, :W]
             ss.close()
     assert m0["gen"][:3] == [W, H, 4]
@@ -297,6 +292,43 @@ def test_render_gather_paths(pt, ngpu_gather):
     assert st2["gather_rccl"] == st["gather_rccl"]
     assert np.array_equal(rgb, img) and np.array_equal(rgb2, img)
     assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
+
+
+@pytest.mark.parametrize("ngpu", [2, 3, 8])
+@pytest.mark.parametrize("cfg", ["c1", "c2"])
+def test_render_ngpu_sessions_on_one_device(pt, cfg, ngpu, monkeypatch):
+    """pt_render(ngpu = n): n host threads and n tile sessions (rank g of n) --
+    the drop-in's own multi-GPU path -- run here with every session on device 0
+    (PT_TUNE same_device=1, framebuffer through the host).  The gathered image and
+    the summed ray count must equal the reference's (= ngpu 1)."""
+    monkeypatch.setenv("PT_TUNE", "same_device=1")
+    full = M["full"][cfg]
+    with pt.Scene.load(U.scene_path(cfg)) as s:
+        rgb, _, st = s.render(ngpu=ngpu)
+        w, h = s.info["width"], s.info["height"]
+    ppm = b"P6\n%d %d\n255\n" % (w, h) + rgb.tobytes()
+    assert U.md5(ppm) == full["md5"]
+    assert st["rays"] == full["rays"] and st["errors"] == 0 and st["gather_rccl"] == 0
+
+
+def test_cli_ngpu_sessions_on_one_device(pt, tmp_path):
+    """The CLI with PT_NGPU=4 (4 sessions on device 0, PT_TUNE same_device=1): the
+    reference's config-1 bytes; the communicator set-up is done on the start-up
+    thread (phases_ms comm_init), not after the render."""
+    import subprocess
+    out = tmp_path / "c1.ppm"
+    exe = U.os.path.join(U.PKG, "build", "pt_render")
+    r = subprocess.run([exe, U.scene_path("c1"), str(out)], capture_output=True, text=True, timeout=300,
+                       env=dict(U.os.environ, PT_QUIET="1", PT_STATS="2", PT_NGPU="4", PT_TUNE="same_device=1"))
+    assert r.returncode == 0, r.stderr
+    assert "ngpu=4" in r.stderr and "comm_init=" in r.stderr, r.stderr
+    assert U.md5(out.read_bytes()) == M["full"]["c1"]["md5"]
+
+
+def test_gather_init_one_rank(pt):
+    """pt_gather_init creates (and caches) the RCCL communicator pt_render's gather uses."""
+    assert pt._lib.pt_gather_init(0, 1) == pt.PT_OK
+    assert pt._lib.pt_gather_init(0, 1) == pt.PT_OK
 
 
 def test_cli_rccl_gather_config1(pt, tmp_path):
@@ -337,3 +369,102 @@ def test_many_hitting_leaves_vs_oracle(pt, tmp_path, engine, monkeypatch):
     assert st["rays"] == octr["rays"]
     if not coop:
         assert st["fallbacks"] > 0
+
+
+# ---- deep stream positions (round 3): windows at each config's own spp, RAY_DEPTH 10,
+# and a scene beyond the cooperative engine's LDS tables (manifest "deep"; the ray
+# counts are the CPU restatement's, whose images equal the reference's)
+DEEP = M.get("deep", {})
+
+
+@pytest.mark.parametrize("name", sorted(DEEP))
+def test_deep_windows_bit_exact(pt, name):
+    """The window alone (its pixels' full sample streams: 256 / 1024 / 4096 spp for
+    configs 3 / 4 / 5), bit-exact with the reference, and the restatement's ray count."""
+    m = DEEP[name]
+    img = U.read_ppm(U.os.path.join(U.GOLDEN, "img_%s.ppm" % name))
+    rad = np.fromfile(U.os.path.join(U.GOLDEN, "rad_%s.f32" % name), np.float32).reshape(img.shape)
+    with pt.Scene.load(U.scene_path(m["scene"], tuple(m["gen"]) if m["gen"] else None)) as s:
+        s.prepare()
+        win = tuple(m["window"]) if m["window"] else None
+        rgb, r, st = s.render(radiance=True, window=win)
+    assert st["errors"] == 0
+    assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
+    assert np.array_equal(rgb, img)
+    assert st["rays"] == m["rays"]
+
+
+@pytest.mark.parametrize("cfg", ["c3", "c4_metal", "c4_glass"])
+def test_deep_full_frame_contains_reference_windows(pt, cfg):
+    """The whole 1920x1080 frame at the config's own spp (256 / 1024) -- the bench's
+    path: path-engine rounds, suspension, the cooperative hand-over at the pass end --
+    must hold the reference's deep windows bit-exactly."""
+    names = [n for n, m in DEEP.items() if m["scene"] == cfg and m["gen"] is None]
+    assert names
+    with pt.Scene.load(U.scene_path(cfg)) as s:
+        rgb, rad, st = s.render(radiance=True)
+    assert st["errors"] == 0
+    for n in names:
+        x0, y0, w, h = DEEP[n]["window"]
+        img = U.read_ppm(U.os.path.join(U.GOLDEN, "img_%s.ppm" % n))
+        wrad = np.fromfile(U.os.path.join(U.GOLDEN, "rad_%s.f32" % n), np.float32).reshape(img.shape)
+        assert rad[y0:y0 + h, x0:x0 + w].view(np.uint32).tolist() == wrad.view(np.uint32).tolist(), n
+        assert np.array_equal(rgb[y0:y0 + h, x0:x0 + w], img), n
+
+
+def test_deep_config5_rank_of_8_at_4096_spp(pt):
+    """Config 5 as the 8-GPU run renders it, to its full 4096 spp: the sessions of the
+    ranks owning the reference's deep 4K windows (rank = (tx + ty) % 8), each the whole
+    rank's share of the frame in one coalesced pass."""
+    import torch
+    world, W, H = 8, 3840, 2160
+    names = [n for n, m in DEEP.items() if m["scene"] == "c5"]
+    assert names
+    tiles_x = W // 16
+    owner = {}
+    for n in names:
+        x0, y0, w, h = DEEP[n]["window"]
+        assert x0 // 16 == (x0 + w - 1) // 16 and y0 // 16 == (y0 + h - 1) // 16   # one tile each
+        owner[n] = pt.tile_owner((y0 // 16) * tiles_x + x0 // 16, tiles_x, world)
+    with pt.Scene.load(U.scene_path("c5")) as s:
+        s.prepare()
+        assert (s.info["width"], s.info["height"], s.info["samples"]) == (W, H, 4096)
+        for r in sorted(set(owner.values())):
+            ss = pt.Session(s, rank=r, world=world)
+            for _ in range(4):
+                ss.trace(1024)   # coalesced into one 4096-spp pass
+            drad = torch.empty(ss.n_tiles * 256 * 3, dtype=torch.float32, device="cuda")
+            ss.resolve(dev_rad=drad.data_ptr())
+            ss.sync()
+            assert ss.stats()["errors"] == 0
+            rgb = pt.unpack_tiles(ss.read_packed(), W, H, r, world)
+            rad = pt.unpack_tiles_f32(drad.cpu().numpy(), W, H, r, world)
+            ss.close()
+            for n in [k for k, v in owner.items() if v == r]:
+                x0, y0, w, h = DEEP[n]["window"]
+                img = U.read_ppm(U.os.path.join(U.GOLDEN, "img_%s.ppm" % n))
+                wrad = np.fromfile(U.os.path.join(U.GOLDEN, "rad_%s.f32" % n), np.float32).reshape(img.shape)
+                assert rad[y0:y0 + h, x0:x0 + w].view(np.uint32).tolist() == wrad.view(np.uint32).tolist(), n
+                assert np.array_equal(rgb[y0:y0 + h, x0:x0 + w], img), n
+
+
+@pytest.mark.parametrize("engine", ["path", "coop8", "coop64"])
+@pytest.mark.parametrize("name", ["dragon_d10_metal_48x48x16", "dragon_d10_glass_48x48x16", "many_lights_48x48x8"])
+def test_deep_engines_beyond_coop_tables(pt, name, engine, monkeypatch):
+    """RAY_DEPTH 10 / 8, 10 planes and 10 emitters: each engine alone for the whole pass
+    (the path engine with coop=0; the cooperative engine forced) gives the reference's bytes."""
+    if name not in DEEP:
+        pytest.fail("deep fixture %s missing" % name)
+    coop = engine.startswith("coop")
+    monkeypatch.setenv("PT_TUNE", "coop=%s,coop_team=%s" % ("100000000" if coop else "0", engine[4:] if coop else "8"))
+    m = DEEP[name]
+    img = U.read_ppm(U.os.path.join(U.GOLDEN, "img_%s.ppm" % name))
+    rad = np.fromfile(U.os.path.join(U.GOLDEN, "rad_%s.f32" % name), np.float32).reshape(img.shape)
+    with pt.Scene.load(U.scene_path(m["scene"], tuple(m["gen"]))) as s:
+        rgb, r, st = s.render(radiance=True)
+    assert st["errors"] == 0
+    assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
+    assert np.array_equal(rgb, img)
+    assert st["rays"] == m["rays"]
+    if coop:
+        assert st["coop_launches"] >= 1

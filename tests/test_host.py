@@ -35,7 +35,7 @@ def test_abi_exports_every_declared_symbol():
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
     assert set(names) == set(pt.EXPORTED)
-    assert pt.abi_version() == pt.ABI_VERSION == 3
+    assert pt.abi_version() == pt.ABI_VERSION == 4
 
 
 @pytest.mark.parametrize("name", sorted(M["bvh"]))
@@ -238,6 +238,7 @@ def test_device_init_without_gpu_fails_loudly():
     if U.gpu_available():
         pytest.skip("GPU present")
     assert pt._lib.pt_device_init(0) in (pt.PT_E_NO_GPU, pt.PT_E_HIP)
+    assert pt._lib.pt_gather_init(0, 0) == pt.PT_E_INVALID
 
 
 def _stack_scene(n=60, seed=7):

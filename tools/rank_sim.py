@@ -22,7 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
     ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
-    ap.add_argument("--ranks", default="first", choices=["first", "last", "both"])
+    ap.add_argument("--ranks", default="first", choices=["first", "last", "both", "all"])
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--spp-per-step", type=int, default=16)
     a = ap.parse_args()
@@ -32,7 +32,7 @@ def main():
     with pt.Scene.load(path) as s:
         s.prepare()
         for w in a.worlds:
-            ranks = {"first": [0], "last": [w - 1], "both": sorted({0, w - 1})}[a.ranks]
+            ranks = {"first": [0], "last": [w - 1], "both": sorted({0, w - 1}), "all": list(range(w))}[a.ranks]
             for r in ranks:
                 ss = pt.Session(s, device=0, rank=r, world=w)
                 spp = a.spp_per_step * w
@@ -56,6 +56,11 @@ def main():
                 out.append(rec)
                 print(json.dumps(rec), flush=True)
                 ss.close()
+            per = [r["mray_s"] for r in out if r["world"] == w]
+            if len(per) > 1:
+                # an N-GPU job ends with its slowest rank
+                print(json.dumps({"world": w, "ranks": len(per), "min_mray_s": min(per), "max_mray_s": max(per),
+                                  "spread": (max(per) - min(per)) / max(per)}), flush=True)
     return out
 
 

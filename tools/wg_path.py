@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise a PT_WGPROF dump of the path engine (-DPT_WPROF build): 16 u64 per
+"""Summarise a PT_TUNE wgprof dump of the path engine (-DPT_WPROF build): 64 u64 per
 workgroup per round: start, end (100 MHz), QW trips, QW active lane-trips, QW
 sleep trips, ring takes, rays, SW batches, SW items, SW spins, SW busy cycles."""
 import sys
@@ -7,7 +7,7 @@ import numpy as np
 
 G = int(sys.argv[2])
 NQ = int(sys.argv[3]) if len(sys.argv) > 3 else 2   # query waves per workgroup (PT_NQ)
-a = np.fromfile(sys.argv[1], np.uint64).reshape(-1, G, 32).astype(np.int64)
+a = np.fromfile(sys.argv[1], np.uint64).reshape(-1, G, 64).astype(np.int64)
 tot = a.sum(axis=(0, 1))
 span = []
 for r in a:
@@ -32,3 +32,8 @@ print("QW cycles per trip: refill %.0f, step %.0f, done %.0f; trips with aux lan
          tot[24] / max(tot[2], 1), tot[25] / max(tot[2], 1)))
 print("SW cycles per batch: shade_item %.0f, next-ray push + publish %.0f, the rest (ring reads, fences) %.0f"
       % (tot[27] / max(tot[7], 1), tot[28] / max(tot[7], 1), (tot[10] - tot[27] - tot[28]) / max(tot[7], 1)))
+print("QW step: load wait %.0f + exec %.0f cycles per stepping trip; refill data wait %.0f cycles per refilling trip (%.3f of trips)"
+      % (tot[32] / max(tot[2] - tot[4], 1), tot[33] / max(tot[2] - tot[4], 1), tot[34] / max(tot[35], 1), tot[35] / max(tot[2], 1)))
+print("SW per batch: ring read wait %.0f; shade_item phases: pixel+prim %.0f, vertex %.0f, fold+sum %.0f, next ray+store %.0f"
+      % (tot[36] / max(tot[7], 1), tot[40] / max(tot[7], 1), tot[41] / max(tot[7], 1), tot[42] / max(tot[7], 1),
+         tot[43] / max(tot[7], 1)))

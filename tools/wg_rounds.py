@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
-"""Per-round spans of a path-engine PT_WGPROF dump, next to the round log (n in)."""
+"""Per-round spans of a path-engine PT_TUNE wgprof dump, next to the round log (n in)."""
 import re
 import sys
 import numpy as np
 
-a = np.fromfile(sys.argv[1], np.uint64).reshape(-1, int(sys.argv[2]), 32).astype(np.int64)
+a = np.fromfile(sys.argv[1], np.uint64).reshape(-1, int(sys.argv[2]), 64).astype(np.int64)
 L = [l for l in open(sys.argv[3]) if l.startswith("round")]
 tot = 0.0
 for i, r in enumerate(a):

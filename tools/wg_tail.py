@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
-"""Per-round breakdown of a path-engine PT_WGPROF dump (32 u64 per WG per round)."""
+"""Per-round breakdown of a path-engine PT_TUNE wgprof dump (64 u64 per WG per round)."""
 import sys
 import numpy as np
 
 G = int(sys.argv[2])
-a = np.fromfile(sys.argv[1], np.uint64).reshape(-1, G, 32).astype(np.float64)
+a = np.fromfile(sys.argv[1], np.uint64).reshape(-1, G, 64).astype(np.float64)
 sel = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else range(len(a))
 for i in sel:
     r = a[i]
