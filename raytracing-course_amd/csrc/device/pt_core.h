@@ -267,8 +267,8 @@ PT_HD bool isect_box(const Ray& r, f3 s, Hit& h) {
     return true;
 }
 
-// src/primitives.cpp:120-152 (roots in f64: ::sqrt(double) at :130-131)
-PT_HD bool isect_ellipsoid(const Ray& r, f3 rad, Hit& h) {
+// src/primitives.cpp:120-146: the ellipsoid's t and side (roots in f64: ::sqrt(double) at :130-131)
+PT_HD bool ellipsoid_root(const Ray& r, f3 rad, float& t, uint32_t& in) {
     const float a = dot(r.d / rad, r.d / rad);
     const float b = 2.f * dot(r.o / rad, r.d / rad);
     const float c = dot(r.o / rad, r.o / rad) - 1.f;
@@ -279,8 +279,15 @@ PT_HD bool isect_ellipsoid(const Ray& r, f3 rad, Hit& h) {
     float x2 = (float)(((double)-b + sd) / (double)(2.f * a));
     if (x1 > x2) { const float tt = x1; x1 = x2; x2 = tt; }
     if (x2 < 0.f) return false;
-    const uint32_t in = (x1 < 0.f) ? 1u : 0u;
-    const float t = in ? x2 : x1;
+    in = (x1 < 0.f) ? 1u : 0u;
+    t = in ? x2 : x1;
+    return true;
+}
+// src/primitives.cpp:120-152
+PT_HD bool isect_ellipsoid(const Ray& r, f3 rad, Hit& h) {
+    float t;
+    uint32_t in;
+    if (!ellipsoid_root(r, rad, t, in)) return false;
     const f3 p = r.o + t * r.d;
     f3 n = normalize(p / (rad * rad));
     if (in) n = -1.f * n;

@@ -10,6 +10,7 @@ namespace pt {
 template <uint32_t STRIDE>
 struct LdsMemN {
     uint32_t* base;
+    uint32_t cap = 0xffffffffu;   // words available (a query needing more takes the exact DFS)
     __device__ __forceinline__ void set(uint32_t i, uint32_t v) { base[i * STRIDE] = v; }
     __device__ __forceinline__ uint32_t get(uint32_t i) const { return base[i * STRIDE]; }
 };

@@ -115,14 +115,16 @@ struct WaveParams {
     uint32_t path_runend;         // a round with at most this many chains runs them to the end of the pass
     unsigned long long* progress; // optional host-mapped count of finished samples (progress bar), or null
     uint32_t path_cap;            // chains a workgroup may hold (<= PT_CMAX)
+    uint32_t lstack;              // aux stack words a query lane may use (<= PT_LSTACK; deeper: exact DFS)
     const uint32_t* tile_order;   // k_wcamera: block b seeds local tile tile_order[b] (null: tile b)
     uint32_t sparse_steps;        // steps per loop trip of the end-of-pass (sparse) kernel
-    F4* ring;                     // per-workgroup ray/done rings, PT_RING_F4 F4 per workgroup
     uint32_t coop_reserve;        // k_wcoop: aux stack words kept free for a depth-first descent (3 (aux depth + 2))
+    uint32_t shade_min;           // k_wpath shade wave: batches of fewer items wait (s_sleep) up to ...
+    uint32_t shade_wait;          // ... this many shader clocks for more (0: never)
 };
 
 // path engine geometry: PT_NQ query waves + 1 shade wave per workgroup; at most
-// PT_CMAX chains resident per workgroup (= the capacity of its two rings).
+// PT_CMAX chains resident per workgroup (= the capacity of its ray ring).
 // Two query waves per shade wave since the hit-region query made the queries
 // cheaper than their shading (3 -> 2 at 4 workgroups per CU: +13 % at rank-of-1,
 // +20 % at rank-of-8; 1 query wave: -8 %)
@@ -136,8 +138,15 @@ struct WaveParams {
 #ifndef PT_CMAX
 #define PT_CMAX 512u
 #endif
-// per workgroup: ray ring ro, rd; PT_NQ done rings ro, rd; ray-ring plane ids
-#define PT_RING_F4 ((3u + 2u * PT_NQ) * PT_CMAX + PT_CMAX / 4u)
+// The rings and the query lanes' aux stacks live in LDS (4 workgroups per CU:
+// 38.9 KB each of the CU's 160 KB):
+//   ray ring   PT_CMAX entries (52 B: ray, slot, plane t and prim, q_prep record)
+//   done rings PT_DQN entries per query wave (32 B: ray, slot, closest prim),
+//              flow-controlled (a finished query waits in its lane while its ring is full)
+//   aux stack  PT_LSTACK words per query lane; a query that would need more takes the
+//              exact DFS (none of 10^6 measured queries needed more than 11)
+#define PT_DQN 64u
+#define PT_LSTACK 16u
 
 // cooperative engine (k_wcoop, the end of a pass): one wave per chain, QC_WAVES
 // independent waves per workgroup, per-wave LDS for the query (pt_wave.hip QcLds)

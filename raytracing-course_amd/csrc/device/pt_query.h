@@ -159,16 +159,24 @@ struct Query {
     uint32_t node;              // Q_AUX: aux node, or PT_LEAFQ | ordinal of the leaf being probed
     uint32_t lb;                // every hitting leaf below lb has been decided
     uint32_t cand;              // probe: its leaf; Q_REPLAY: the hitting leaf being decided (hidx[ne])
-    float bound;
     float dl;                   // certification margin (t units, see q_leaf_certain)
-    uint32_t lref, lcnt;        // probe: the leaf's primitive range
-    uint32_t li;                // probe: primitives tested (bit 31: next fetch = full record)
-    float lt;                   // probe: leaf first-min t so far
-    int lid;                    // probe: its primitive (-1 none)
-    uint32_t off;               // walk: ancestor list offset
-    uint32_t e[4];              // walk: the entries under test (0xffffffff = none)
-    uint32_t astar;             // walk: deepest ancestor at or above that LCA seen so far
-    float t1c, mc;              // leaf check: approximate entry and certification margin
+    // the probe's state (Q_AUX) and the decision's (Q_REPLAY) share registers: li is 0
+    // whenever an aux pass starts (q_init_pre, q_pass_done)
+    union {
+        struct {
+            uint32_t lref, lcnt;        // probe: the leaf's primitive range
+            uint32_t li;                // probe: primitives tested (bit 31: this step = full record)
+            float lt;                   // probe: leaf first-min t so far
+            int lid;                    // probe: its primitive (-1 none)
+        };
+        struct {
+            uint32_t off;               // walk: ancestor list offset
+            uint32_t e[4];              // walk: the entries under test (0xffffffff = none)
+            uint32_t astar;             // walk: deepest ancestor at or above that LCA seen so far
+            float bound;                // walk: the segment's bound
+            float t1c, mc;              // leaf check: approximate entry and certification margin
+        };
+    };
     uint32_t hidx[PT_QHK];      // hitting leaves (reference index, sorted; 0xffffffff = empty)
     float ht[PT_QHK];           // ... their first-min t
     int hid[PT_QHK];            // ... and its primitive
@@ -482,9 +490,21 @@ PT_HD void q_aux_next(Query& q, Mem& stk, uint32_t next) {
     q_next_decision(q);
 }
 
+// Diagnostics builds (PT_QPROF, device only): each step kind's branch stamps the
+// shader clock on entry into qp[kind] (this lane's copy; the caller takes the
+// wave's and attributes the time to the kinds in program order).
+#if defined(PT_QPROF) && defined(__HIP_DEVICE_COMPILE__)
+#define PT_QPROF_DEV 1
+#define QP_STAMP(i) do { uint64_t t_; asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); qp[i] = (uint32_t)t_; } while (0)
+#define QP_ARG , uint32_t* qp
+#else
+#define QP_STAMP(i) (void)0
+#define QP_ARG
+#endif
 template <class Mem>
-PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r[8]) {
+PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r[8] QP_ARG) {
     if (q.phase == Q_AUX && !(q.node & PT_LEAFQ)) {
+        QP_STAMP(0);
         // one wide node: PT_AUXW child entries
         C.aux++;
         const f3 oinv = mk3(q.ray.o.x * q.inv.x, q.ray.o.y * q.inv.y, q.ray.o.z * q.inv.z);
@@ -538,19 +558,29 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
             const uint32_t item = isleaf ? (PT_LEAFQ | rng) : code;
             const bool push = take && next != 0xffffffffu;
             if (take && next == 0xffffffffu) next = item;
-            if (push) stk.set(q.sp++, item);
+            if (push) {
+                if (q.sp < stk.cap) stk.set(q.sp, item);
+                q.sp++;   // (past the stack's capacity: the exact DFS below)
+            }
+        }
+        if (q.sp > stk.cap) {
+            q.phase = Q_EXACT;   // the pending items do not fit the stack: exact DFS (same result)
+            return;
         }
 #ifdef PT_QDIAG
         if (next == 0xffffffffu && q.sp == 0u) C.passes++;
+        if (q.sp > C.steps) C.steps = q.sp;   // (diagnostics: the deepest aux stack of the query)
 #endif
         q_aux_next(q, stk, next);
         return;
     }
     if (q.phase == Q_AUX) {
+        QP_STAMP(1);
         // probe a candidate leaf: the first strict minimum over its primitives
-        // (src/bvh.cpp:205-213), independent of any bound
-        Hit h;
-        bool ok = false;
+        // (src/bvh.cpp:205-213), independent of any bound.  Every record form goes
+        // through ONE test of each primitive kind (a wave runs each kind's code once
+        // whatever mix of forms its lanes hold), and only t is computed: the
+        // consumer recomputes the closest hit's normal and side.
         if (q.li == 0u) {
             // its bundle: its first primitive and the primitive range
             q.cand = f2u(r[3].x);
@@ -565,36 +595,48 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
                 q_aux_next(q, stk, 0xffffffffu);
                 return;
             }
-            if (f2u(r[0].w) & PT_QP_FULL) {
-                q.li = 0x80000000u;               // not representable compactly: full record next step
-                return;
-            }
-            ok = f2u(r[0].w) == T_TRIANGLE
-                     ? isect_triangle(q.ray, mk3(r[0].x, r[0].y, r[0].z), mk3(r[1].x, r[1].y, r[1].z),
-                                      mk3(r[1].w, r[2].x, r[2].y), h)
-                     : bvh_prim_intersect(qprim_expand(r[0], r[1], r[2]), q.ray, h);
-        } else if (q.li & 0x80000000u) {
-            Prim pr;
-            pr.p0 = r[0]; pr.p1 = r[1]; pr.p2 = r[2]; pr.p3 = r[3]; pr.p4 = r[4];
-            q.li &= 0x7fffffffu;
-            ok = bvh_prim_intersect(pr, q.ray, h);
-        } else if (f2u(r[0].w) & PT_QP_FULL) {
-            q.li |= 0x80000000u;
-            return;
-        } else if (f2u(r[0].w) == T_TRIANGLE) {
-            // plain triangle (pos = +0, identity rotation): the world->local rotation
-            // changes at most the sign of zero components, which changes neither the
-            // accept decision nor t (a signed zero only matters in a sum that is
-            // exactly zero, where every compare here is false either way); the
-            // consumer recomputes n with the full transform
-            ok = isect_triangle(q.ray, mk3(r[0].x, r[0].y, r[0].z), mk3(r[1].x, r[1].y, r[1].z),
-                                mk3(r[1].w, r[2].x, r[2].y), h);
-        } else {
-            ok = bvh_prim_intersect(qprim_expand(r[0], r[1], r[2]), q.ray, h);
         }
+        const bool full = (q.li & 0x80000000u) != 0u;   // this step holds the full 80-B record
+        const uint32_t cty = f2u(r[0].w);
+        if (!full && (cty & PT_QP_FULL)) {
+            q.li |= 0x80000000u;                        // not representable compactly: full record next step
+            return;
+        }
+        // the primitive (a compact record expands to the same bits)
+        Prim pr = qprim_expand(r[0], r[1], r[2]);
+        if (full) { pr.p0 = r[0]; pr.p1 = r[1]; pr.p2 = r[2]; pr.p3 = r[3]; pr.p4 = r[4]; }
+        const uint32_t ty = f2u(pr.p0.w);
+        // A plain triangle (compact: pos = +0, identity rotation) is tested on the world
+        // ray: the world->local rotation changes at most the sign of zero components,
+        // which changes neither the accept decision nor t (a signed zero only matters in
+        // a sum that is exactly zero, where every compare here is false either way).
+        // Every other record goes to local space exactly as Primitive::Intersect does.
+        Ray lr = q.ray;
+        if (full || cty != T_TRIANGLE) {
+            const f3 pos = mk3(pr.p0.x, pr.p0.y, pr.p0.z);
+            q4 qq;
+            qq.x = pr.p1.x; qq.y = pr.p1.y; qq.z = pr.p1.z; qq.w = pr.p1.w;
+            const q4 cq = conj(qq);
+            lr.o = qrot(cq, q.ray.o + -1.f * pos);
+            lr.d = qrot(cq, q.ray.d);
+        }
+        const f3 pa = mk3(pr.p2.x, pr.p2.y, pr.p2.z);
+        bool ok;
+        float t = 0.f;
+        uint32_t in;
+        if (ty == T_TRIANGLE) {
+            Hit h;
+            ok = isect_triangle(lr, pa, mk3(pr.p3.x, pr.p3.y, pr.p3.z), mk3(pr.p3.w, pr.p4.x, pr.p4.y), h);
+            t = h.t;
+        } else if (ty == T_BOX) {
+            ok = slab(lr.o, lr.d, pa, t, in);
+        } else {
+            ok = ellipsoid_root(lr, pa, t, in);
+        }
+        const uint32_t li = q.li & 0x7fffffffu;
         C.ptests++;
-        if (ok && h.t < q.lt) { q.lt = h.t; q.lid = (int)(q.lref + q.li); }
-        q.li = q.li + 1u;
+        if (ok && t < q.lt) { q.lt = t; q.lid = (int)(q.lref + li); }
+        q.li = li + 1u;
         if (q.li < q.lcnt) return;
         q.li = 0u;
         if (q.lid >= 0 && !q_add_hit(q, q.cand, q.lt, q.lid)) {
@@ -606,6 +648,7 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
     }
     // Q_REPLAY: is hitting leaf hidx[ne] (= cand) entered?
     if (q.walk == R_CAND) {
+        QP_STAMP(2);
         // its own leaf record (+ where its ancestor list is)
         Node nd;
         nd.a = r[0];
@@ -639,6 +682,7 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
         return;
     }
     if (q.walk == R_WALK_E) {
+        QP_STAMP(3);
         // next 4 list entries (ancestors, then the leaf; 0xffffffff = padding)
         const uint32_t hlast = q_sel(q.hidx, q.ne - 1u, 0u);   // last recorded hit (none: 0)
         bool any = false, accept = false;
@@ -669,6 +713,7 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
         return;
     }
     // R_WALK_N: the records of the pending entries, tested with B
+    QP_STAMP(4);
     bool reject = false;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -704,7 +749,12 @@ PT_HD void q_step(const SceneView& S, Query& q, QCounts& C, Mem& stk) {
     F4 r[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) r[k] = blob_piece(S, off[k]);
+#ifdef PT_QPROF_DEV
+    uint32_t qp[5];
+    q_exec(S, q, C, stk, r, qp);
+#else
     q_exec(S, q, C, stk, r);
+#endif
 }
 
 // exact stack DFS for the rays the replay leaves (planes again + bvh_exact:

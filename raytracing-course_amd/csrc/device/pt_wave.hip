@@ -229,33 +229,43 @@ __global__ void __launch_bounds__(256) k_wcamera_merge(WaveParams P) {
 // shade wave, last out, hands the remaining chains' next rays to the fresh queue
 // of the next round.  Rounds then only rebalance chains between workgroups.
 //
-// Rings: entries in global memory (per workgroup), positions in LDS, ordered by
-// workgroup-scope release/acquire fences (the waves of a workgroup share one CU
-// and its L1).  Every ring has ONE producer, which publishes its entries in order,
-// so a consumer takes a contiguous range: the ray ring is written by the shade
-// wave, and each query wave has its own done ring.  At most PT_CMAX chains are
-// resident per workgroup and a chain has at most one ring entry, so no ring
-// overflows and no entry is overwritten before it has been read.
+// Rings: entries and positions in LDS, ordered by workgroup-scope release/acquire
+// fences.  Every ring has ONE producer, which publishes its entries in order, so a
+// consumer takes a contiguous range: the ray ring is written by the shade wave, and
+// each query wave has its own done ring.  At most PT_CMAX chains are resident per
+// workgroup and a chain has at most one ring entry, so the ray ring (PT_CMAX
+// entries) never overflows; a done ring (PT_DQN entries) is flow-controlled by its
+// consumer's head.  No entry is overwritten before it has been read.
 struct PathLds {
     uint32_t rq_head;             // next ray-ring entry to take (query waves, CAS)
     uint32_t rq_tail;             // ray-ring entries published (shade wave)
     uint32_t resident;            // chains held by this workgroup
     uint32_t qw_done;             // query waves that have left
     uint32_t dq_tail[PT_NQ];      // done-ring entries published, per query wave
-    uint32_t dq_head[PT_NQ];      // done-ring entries consumed (diagnostics)
+    uint32_t dq_head[PT_NQ];      // done-ring entries read by the shade wave (free space for the producer)
+    F4 rq_ro[PT_CMAX];            // ray ring: {o.xyz, slot}
+    F4 rq_rd[PT_CMAX];            //           {d.xyz, P}
+    F4 rq_ri[PT_CMAX];            //           q_prep record
+    int rq_pid[PT_CMAX];          //           closest plane
+    F4 dq_ro[PT_NQ][PT_DQN];      // done rings: {o.xyz, slot}
+    F4 dq_rd[PT_NQ][PT_DQN];      //             {d.xyz, u32 closest prim | 0xffffffff}
+    uint32_t stk[PT_LSTACK * 64u * PT_NQ];   // query lanes' aux stacks, [word][lane]
 };
 
-__device__ __forceinline__ uint32_t lds_read(const uint32_t& v) { return *(const volatile uint32_t*)&v; }
-__device__ __forceinline__ void lds_write(uint32_t& v, uint32_t x) { *(volatile uint32_t*)&v = x; }
+// LDS accessors with the address space spelled out (a reference to a __shared__ member is a
+// generic pointer, which the compiler may otherwise lower to flat instructions)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PT_LDS __attribute__((address_space(3)))
+#else
+#define PT_LDS
+#endif
+__device__ __forceinline__ uint32_t lds_read(const uint32_t& v) { return *(const volatile PT_LDS uint32_t*)&v; }
+__device__ __forceinline__ void lds_write(uint32_t& v, uint32_t x) { *(volatile PT_LDS uint32_t*)&v = x; }
+template <class T>
+__device__ __forceinline__ T lds_get(const T* a, uint32_t i) { return ((const PT_LDS T*)a)[i]; }
+template <class T>
+__device__ __forceinline__ void lds_put(T* a, uint32_t i, const T& v) { ((PT_LDS T*)a)[i] = v; }
 
-struct PathRing {
-    F4* rq_ro;                    // ray ring: {o.xyz, slot}
-    F4* rq_rd;                    //           {d.xyz, P}
-    int* rq_pid;                  //           closest plane
-    F4* rq_ri;                    //           q_prep record
-    F4* dq_ro;                    // done rings (PT_NQ x PT_CMAX): {o.xyz, slot}
-    F4* dq_rd;                    //                               {d.xyz, u32 closest prim | 0xffffffff}
-};
 
 #define PT_PATH_REFILL_MIN 8u      // idle lanes before a query wave refills (any, once the round's work is out)
 #define PT_NOWORK 0xffffffffu
@@ -266,9 +276,8 @@ struct PathRing {
 // up to P.sparse_steps steps.  A separate instantiation, so its registers do not
 // weigh on the main kernel.
 template <bool SPARSE>
-__device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L, const PathRing& G,
-                                                uint32_t* lds_stack, uint32_t qw) {
-    LdsMemN<64u * PT_NQ> stk{lds_stack + 64u * qw + lane_id()};
+__device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L, uint32_t qw) {
+    LdsMemN<64u * PT_NQ> stk{L.stk + 64u * qw + lane_id(), P.lstack};
     const uint32_t p = P.parity;
     const uint32_t* in = P.ctl + PT_CTL_SET * p;
     uint32_t* out = P.ctl + PT_CTL_SET * (1u - p);
@@ -291,19 +300,21 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     uint32_t trip = 0u;
     const uint32_t wq = qw;                 // this query wave's done ring
     uint32_t rr = 0u;                       // replay step kind served last
-    const uint32_t dq_base = wq * PT_CMAX;
-    uint32_t dq_res = 0u;                   // done-ring entries reserved (and written)
-    uint32_t dq_pend = 0u, dq_pub = 0u;     // ... written before this trip / published
+    uint32_t dq_res = 0u;                   // done-ring entries written and published
     bool active = false;
     uint32_t slot = 0u;
     Query q;
     QCounts C{0u, 0u, 0u, 0u};
-    uint32_t rays = 0u, fallbacks = 0u, init_exact = 0u;
+    // wave-level counters (scalar registers; per-lane ones would cost VGPRs)
+    uint64_t rays = 0u, fallbacks = 0u, init_exact = 0u, planes = 0u;
 #ifdef PT_WPROF
     uint64_t pf_trips = 0, pf_act = 0, pf_sleep = 0, pf_ring = 0, pf_pulled = 0, pf_exit_budget = 0, pf_res = 0,
              pf_dq = 0, pf_rq = 0, pf_tripcyc = 0, pf_qlat = 0, pf_qn = 0, pf_qsteps = 0, pf_refillcyc = 0;
     uint64_t pf_stepcyc = 0, pf_auxtrips = 0, pf_picktrips = 0, pf_stepped = 0, pf_donecyc = 0;
     uint64_t pf_ldcyc = 0, pf_excyc = 0, pf_rfdata = 0, pf_rftrips = 0;
+#ifdef PT_QPROF
+    uint64_t pf_kind[6] = {0, 0, 0, 0, 0, 0}, pf_kindn[5] = {0, 0, 0, 0, 0};
+#endif
     uint64_t pf_t0 = __builtin_amdgcn_s_memtime(), pf_qstart = 0;
     uint32_t pf_qs = 0;
 #endif
@@ -422,6 +433,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 given += take;
             }
             if (src == 2u) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            bool took = false;   // a fresh ray (not a resumed query) started in this lane
 #ifdef PT_WPROF
             const uint64_t pf_r0 = __ballot(src != 0u) ? pf_now() : 0;
 #endif
@@ -444,10 +456,10 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                     pid = FQ.pid[fi];
                     pre = FQ.ri[fi];
                 } else {
-                    o = G.rq_ro[gi];
-                    d = G.rq_rd[gi];
-                    pid = G.rq_pid[gi];
-                    pre = G.rq_ri[gi];
+                    o = lds_get(L.rq_ro, gi);
+                    d = lds_get(L.rq_rd, gi);
+                    pid = lds_get(L.rq_pid, gi);
+                    pre = lds_get(L.rq_ri, gi);
                 }
 #ifdef PT_WPROF
                 PF_WAIT4(o); PF_WAIT4(d); PF_WAIT4(pre);
@@ -456,16 +468,18 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 ray.o = mk3(o.x, o.y, o.z);
                 ray.d = mk3(d.x, d.y, d.z);
                 slot = f2u(o.w);
-                rays++;
-                C.planes += P.S.n_planes;
+                took = true;
 #ifdef PT_WPROF
                 pf_qstart = __builtin_amdgcn_s_memtime();
                 pf_qs = 0;
 #endif
                 q_init_pre(ray, d.w, pid, pre, q);
-                if (q.phase == Q_EXACT) init_exact++;
                 active = true;
             }
+            const uint32_t ntook = (uint32_t)__popcll(__ballot(took));
+            rays += ntook;
+            planes += (uint64_t)ntook * P.S.n_planes;
+            init_exact += (uint32_t)__popcll(__ballot(took && q.phase == Q_EXACT));
 #ifdef PT_WPROF
             if (pf_r0) {
                 pf_rfdata += pf_now() - pf_r0;
@@ -524,10 +538,43 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
 #pragma unroll
                 for (int k = 0; k < 8; ++k) PF_WAIT4(r[k]);
                 const uint64_t tb = pf_now();
+#ifdef PT_QPROF_DEV
+                uint32_t qp[5] = {0u, 0u, 0u, 0u, 0u};
+                q_exec(P.S, q, C, stk, r, qp);
+#else
                 q_exec(P.S, q, C, stk, r);
+#endif
                 const uint64_t tc = pf_now();
                 pf_ldcyc += tb - ta;
                 pf_excyc += tc - tb;
+#ifdef PT_QPROF_DEV
+                {
+                    // each kind's stamp (wave max), then durations in program order
+                    uint32_t ts[6];
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) {
+                        uint32_t v = qp[i];
+                        for (int off = 32; off >= 1; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off, 64));
+                        ts[i] = __builtin_amdgcn_readfirstlane(v);
+                    }
+                    // (the compiler lays the kinds' blocks out in its own order: each executed
+                    // kind runs until the next later stamp, or the end of the step)
+                    const uint32_t t0 = (uint32_t)tb, t1 = (uint32_t)tc;
+                    uint32_t first = t1;
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) {
+                        if (ts[i] == 0u) continue;
+                        uint32_t nx = t1;
+#pragma unroll
+                        for (int j = 0; j < 5; ++j)
+                            if (ts[j] != 0u && ts[j] - t0 > ts[i] - t0 && ts[j] - t0 < nx - t0) nx = ts[j];
+                        pf_kind[i] += nx - ts[i];
+                        pf_kindn[i]++;
+                        if (ts[i] - t0 < first - t0) first = ts[i];
+                    }
+                    pf_kind[5] += first - t0;   // before the first kind's stamp
+                }
+#endif
             }
 #else
             if (kind == 0u || kind == pick) q_step(P.S, q, C, stk);
@@ -537,25 +584,23 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
         const uint64_t pf_s1 = __builtin_amdgcn_s_memtime();
         pf_stepcyc += pf_s1 - pf_s0;
 #endif
-        // Publish the done-ring entries written before this trip: their stores were issued
-        // before this trip's loads, which have completed (in-order vmcnt), so the release
-        // fence here does not wait on fresh stores.
-        if (dq_pend != dq_pub) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane_id() == 0u) lds_write(L.dq_tail[wq], dq_pend);
-            dq_pub = dq_pend;
-        }
-        // finished queries -> this wave's done ring, in lane order (the shade wave
-        // recomputes t, n and side from the prim)
-        const bool fin = active && q.phase == Q_DONE;
-        const unsigned long long mfin = __ballot(fin);
+        // finished queries -> this wave's done ring, in lane order, as far as it has room
+        // (the shade wave recomputes t, n and side from the prim); the others wait in
+        // their lanes (phase Q_DONE) for the next trip
+        const uint32_t room = PT_DQN - (dq_res - __builtin_amdgcn_readfirstlane(lds_read(L.dq_head[wq])));
+        const unsigned long long mfin = __ballot(active && q.phase == Q_DONE);
+        const uint32_t rank = lanes_below(mfin);
+        const bool fin = active && q.phase == Q_DONE && rank < room;
+        const uint32_t nfin = (uint32_t)__popcll(mfin) < room ? (uint32_t)__popcll(mfin) : room;
         const uint32_t dq_at = dq_res;
-        dq_res += (uint32_t)__popcll(mfin);
+        dq_res += nfin;
+        fallbacks += (uint32_t)__popcll(__ballot(active && q.phase == Q_EXACT));
         if (active) {
             if (fin) {
-                const uint32_t j = dq_base + (dq_at + lanes_below(mfin)) % PT_CMAX;
-                G.dq_ro[j] = F4{q.ray.o.x, q.ray.o.y, q.ray.o.z, u2f(slot)};
-                G.dq_rd[j] = F4{q.ray.d.x, q.ray.d.y, q.ray.d.z, u2f(q.res_id < 0 ? 0xffffffffu : (uint32_t)q.res_id)};
+                const uint32_t j = wq * PT_DQN + (dq_at + rank) % PT_DQN;
+                lds_put(&L.dq_ro[0][0], j, F4{q.ray.o.x, q.ray.o.y, q.ray.o.z, u2f(slot)});
+                lds_put(&L.dq_rd[0][0], j,
+                        F4{q.ray.d.x, q.ray.d.y, q.ray.d.z, u2f(q.res_id < 0 ? 0xffffffffu : (uint32_t)q.res_id)});
                 active = false;
 #ifdef PT_WPROF
                 if (pf_qstart) {
@@ -570,25 +615,27 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 P.ex.ro[k] = F4{q.ray.o.x, q.ray.o.y, q.ray.o.z, u2f(slot)};
                 P.ex.rd[k] = F4{q.ray.d.x, q.ray.d.y, q.ray.d.z, u2f(k)};
                 atomicSub(&L.resident, 1u);
-                fallbacks++;
                 active = false;
             }
         }
-        dq_pend = dq_res;   // written this trip: published next trip
+        if (nfin) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane_id() == 0u) lds_write(L.dq_tail[wq], dq_res);
+        }
 #ifdef PT_WPROF
         pf_donecyc += __builtin_amdgcn_s_memtime() - pf_s1;
 #endif
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane_id() == 0u) lds_write(L.dq_tail[wq], dq_res);
     unsigned long long* ctr = ctr_copy(P.counters);
-    wave_add_u64(ctr + 0, rays);
     wave_add_u64(ctr + 1, C.nodes);
     wave_add_u64(ctr + 2, C.ptests);
-    wave_add_u64(ctr + 3, C.planes);
     wave_add_u64(ctr + 5, C.aux);
-    wave_add_u64(ctr + 6, fallbacks);
-    wave_add_u64(ctr + 7, init_exact);
+    if (lane_id() == 0u) {
+        if (rays) atomicAdd(ctr + 0, (unsigned long long)rays);
+        if (planes) atomicAdd(ctr + 3, (unsigned long long)planes);
+        if (fallbacks) atomicAdd(ctr + 6, (unsigned long long)fallbacks);
+        if (init_exact) atomicAdd(ctr + 7, (unsigned long long)init_exact);
+    }
 #ifdef PT_WPROF
     if (P.wg_prof && lane_id() == 0u) {
         unsigned long long* w = P.wg_prof + 64ull * blockIdx.x;
@@ -613,6 +660,10 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
         atomicAdd(w + 33, pf_excyc);
         atomicAdd(w + 34, pf_rfdata);
         atomicAdd(w + 35, pf_rftrips);
+#ifdef PT_QPROF
+        for (int i = 0; i < 6; ++i) atomicAdd(w + 48 + i, pf_kind[i]);
+        for (int i = 0; i < 5; ++i) atomicAdd(w + 54 + i, pf_kindn[i]);
+#endif
     }
     if (P.wg_prof) {
         unsigned long long* w = P.wg_prof + 64ull * blockIdx.x;
@@ -625,10 +676,9 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     if (lane_id() == 0u) atomicAdd(&L.qw_done, 1u);
 }
 
-__device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L, const PathRing& G) {
+__device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L) {
     uint32_t* out = P.ctl + PT_CTL_SET * (1u - P.parity);
     const RayQ N = P.fq[1u - P.parity];
-    const RayQ RQ{G.rq_ro, G.rq_rd, G.rq_pid, G.rq_ri};
     const uint32_t lane = lane_id();
     uint32_t head[PT_NQ];             // done rings consumed (this wave only)
 #pragma unroll
@@ -639,6 +689,8 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
     uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // shade_item phases
 #endif
     uint32_t prog = 0u;               // finished samples not yet added to P.progress
+    bool waiting = false;             // holding back a small batch (since wait_t0)
+    uint64_t wait_t0 = 0;
     for (;;) {
         // published entries of the done rings (ring indices are compile-time: no scratch)
         uint32_t av[PT_NQ], total = 0u;
@@ -662,13 +714,35 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
-        // up to 64 of them, rings in order (a ring is never starved for long: its
-        // producer's chains are the ones the other rings are not holding)
+        // A batch costs about the same instructions for 1 or 64 items, and the shade wave
+        // shares its SIMD's issue with query waves: with many chains in flight, a small
+        // batch may wait (sleeping) for more items (P.shade_min / P.shade_wait)
+        if (total < P.shade_min && lds_read(L.qw_done) != PT_NQ &&
+            total * 4u < (uint32_t)__builtin_amdgcn_readfirstlane(lds_read(L.resident))) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            if (!waiting) {
+                waiting = true;
+                wait_t0 = now;
+            }
+            if (now - wait_t0 < P.shade_wait) {
+                __builtin_amdgcn_s_sleep(2);
+                continue;
+            }
+        }
+        waiting = false;
+        // up to 64 of them: a fair share of each ring first (a full ring holds back its
+        // producer's finished queries), then the rest in ring order
         uint32_t take[PT_NQ], n = 0u;
 #pragma unroll
         for (uint32_t w = 0; w < PT_NQ; ++w) {
-            take[w] = av[w] < 64u - n ? av[w] : 64u - n;
+            take[w] = av[w] < 64u / PT_NQ ? av[w] : 64u / PT_NQ;
             n += take[w];
+        }
+#pragma unroll
+        for (uint32_t w = 0; w < PT_NQ; ++w) {
+            const uint32_t x = av[w] - take[w] < 64u - n ? av[w] - take[w] : 64u - n;
+            take[w] += x;
+            n += x;
         }
 #ifdef PT_WPROF
         const uint64_t c0 = __builtin_amdgcn_s_memtime();
@@ -679,13 +753,23 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
         uint32_t j = 0u, before = 0u;
 #pragma unroll
         for (uint32_t w = 0; w < PT_NQ; ++w) {
-            if (lane >= before && lane < before + take[w]) j = w * PT_CMAX + (head[w] + lane - before) % PT_CMAX;
+            if (lane >= before && lane < before + take[w]) j = w * PT_DQN + (head[w] + lane - before) % PT_DQN;
             before += take[w];
         }
 #pragma unroll
         for (uint32_t w = 0; w < PT_NQ; ++w) head[w] += take[w];
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const bool have = lane < n;
+        F4 o = F4{0.f, 0.f, 0.f, 0.f}, d = o;
+        if (have) {
+            o = lds_get(&L.dq_ro[0][0], j);
+            d = lds_get(&L.dq_rd[0][0], j);
+        }
+        // the entries are in registers: their slots go back to the producers
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#pragma unroll
+        for (uint32_t w = 0; w < PT_NQ; ++w)
+            if (lane == w) lds_write(L.dq_head[w], head[w]);
         Ray ray;
         uint32_t slot = 0u;
         bool emit = false, sdone = false;
@@ -693,7 +777,6 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
         const uint64_t c1 = __builtin_amdgcn_s_memtime();
 #endif
         if (have) {
-            const F4 o = G.dq_ro[j], d = G.dq_rd[j];
 #ifdef PT_WPROF
             PF_WAIT4(o); PF_WAIT4(d);
             pf_rdc += pf_now() - c1;
@@ -713,9 +796,6 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
             if (lane == 0u) __hip_atomic_fetch_add(P.progress, (unsigned long long)prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             prog = 0u;
         }
-#ifdef PT_WPROF
-        if (lane < PT_NQ) lds_write(L.dq_head[lane], head[lane]);
-#endif
         const bool flush = __builtin_amdgcn_readfirstlane(lds_read(L.qw_done)) == PT_NQ;
         const unsigned long long me = __ballot(emit);
         uint32_t gone = (uint32_t)__popcll(__ballot(have && !emit));   // pixels done with this pass
@@ -725,7 +805,17 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
             if (emit) push_ray(P, N, k, ray, slot);
             gone += (uint32_t)__popcll(me);
         } else {
-            if (emit) push_ray(P, RQ, (tail + lanes_below(me)) % PT_CMAX, ray, slot);
+            if (emit) {
+                // the next ray into the LDS ray ring (RayQ form: push_ray's plane test and set-up)
+                const uint32_t e = (tail + lanes_below(me)) % PT_CMAX;
+                float pt;
+                int pid;
+                q_planes(P.S, ray, pt, pid);
+                lds_put(L.rq_ro, e, F4{ray.o.x, ray.o.y, ray.o.z, u2f(slot)});
+                lds_put(L.rq_rd, e, F4{ray.d.x, ray.d.y, ray.d.z, pt});
+                lds_put(L.rq_pid, e, pid);
+                lds_put(L.rq_ri, e, q_prep(P.S, ray));
+            }
             tail += (uint32_t)__popcll(me);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0u) lds_write(L.rq_tail, tail);
@@ -763,21 +853,17 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L,
         const uint32_t k = wave_append(out + C_FRESH, has);
         if (has) {
             const uint32_t e = i % PT_CMAX;
-            N.ro[k] = G.rq_ro[e];
-            N.rd[k] = G.rq_rd[e];
-            N.pid[k] = G.rq_pid[e];
-            N.ri[k] = G.rq_ri[e];
+            N.ro[k] = lds_get(L.rq_ro, e);
+            N.rd[k] = lds_get(L.rq_rd, e);
+            N.pid[k] = lds_get(L.rq_pid, e);
+            N.ri[k] = lds_get(L.rq_ri, e);
         }
     }
 }
 
 template <bool SPARSE>
 __global__ void __launch_bounds__(PT_PATH_WG) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAVES_PER_EU, PT_PATH_WAVES_PER_EU))) k_wpath(WaveParams P) {
-    extern __shared__ uint32_t lds_stack[];
     __shared__ PathLds L;
-    F4* r = P.ring + (size_t)blockIdx.x * PT_RING_F4;
-    const PathRing G{r, r + PT_CMAX, reinterpret_cast<int*>(r + (2u + 2u * PT_NQ) * PT_CMAX),
-                     r + (2u + 2u * PT_NQ) * PT_CMAX + PT_CMAX / 4u, r + 2u * PT_CMAX, r + (2u + PT_NQ) * PT_CMAX};
     if (threadIdx.x == 0u) {
         L.rq_head = L.rq_tail = L.resident = L.qw_done = 0u;
     }
@@ -788,8 +874,8 @@ __global__ void __launch_bounds__(PT_PATH_WG) __attribute__((amdgpu_waves_per_eu
     __syncthreads();
     // waves 0 .. PT_NQ-1 query, wave PT_NQ shades
     const uint32_t wave = threadIdx.x >> 6;
-    if (wave == PT_NQ) path_shade_wave(P, L, G);
-    else path_query_wave<SPARSE>(P, L, G, lds_stack, wave);
+    if (wave == PT_NQ) path_shade_wave(P, L);
+    else path_query_wave<SPARSE>(P, L, wave);
 }
 
 // ---- cooperative engine (end of a pass) ---------------------------------------
@@ -1450,9 +1536,9 @@ hipError_t pt_launch_path_round(pt::WaveParams p, uint32_t path_grid, uint32_t s
     p.path = 1u;
     if (e0 && (e = hipEventRecord(e0, s)) != hipSuccess) return e;
     if (sparse)
-        hipLaunchKernelGGL(pt::k_wpath<true>, dim3(path_grid), dim3(PT_PATH_WG), 4u * 64u * PT_NQ * p.aux_stack, s, p);
+        hipLaunchKernelGGL(pt::k_wpath<true>, dim3(path_grid), dim3(PT_PATH_WG), 0, s, p);
     else
-        hipLaunchKernelGGL(pt::k_wpath<false>, dim3(path_grid), dim3(PT_PATH_WG), 4u * 64u * PT_NQ * p.aux_stack, s, p);
+        hipLaunchKernelGGL(pt::k_wpath<false>, dim3(path_grid), dim3(PT_PATH_WG), 0, s, p);
     if (e1 && (e = hipEventRecord(e1, s)) != hipSuccess) return e;
     const uint32_t exact_lds = 64u * 4u * (p.max_stack ? p.max_stack : 1u);
     hipLaunchKernelGGL(pt::k_wexact, dim3(64), dim3(64), exact_lds, s, p);

@@ -81,7 +81,11 @@ const Rccl& rccl() {
 //   round_batch=N     path rounds launched per chain count while the chains are far above
 //                     the hand-over (default 1)
 //   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
+//   shade_min=N, shade_wait=C  path engine: a shade batch of fewer than N items waits up to C
+//                     shader clocks for more while many chains are in flight (default 0: off)
 //   cap=N             chains a workgroup may hold
+//   lstack=N          aux stack words a path-engine query may use (default and maximum PT_LSTACK;
+//                     a query needing more takes the exact DFS)
 //   rowmajor=1        seed a pass in row-major tile order instead of Z-order
 //   variant=V         megakernel variant bits (1 filtered tests, 2 XCD-banded tiles)
 //   roundlog=1|2      per-round kernel times / pixels' remaining samples on stderr
@@ -194,7 +198,6 @@ struct pt_session {
     unsigned long long* wg_prof = nullptr;
     // wavefront engine buffers (replay traversal)
     bool wave = false;
-    pt::F4* ring = nullptr;       // path engine: path_grid * PT_RING_F4
     uint32_t path_grid = 0, path_budget = 1024, path_runend = 0, path_sparse = 0, sparse_steps = 8;
     uint32_t coop_max = 0, coop_grid = 0, coop_reserve = 0;   // cooperative engine (k_wcoop) at the end of a pass
     uint32_t round_batch = 1;     // rounds launched per count while the chains are far above the hand-over
@@ -990,8 +993,6 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // above the hand-over
         if (ss->coop_max && !tune_has("sparse")) ss->path_sparse = std::min(ss->path_sparse, ss->coop_max);
         ss->round_batch = (uint32_t)std::max(1, tune_int("round_batch", (int)ss->round_batch));
-        if (hipMalloc(&ss->ring, (size_t)ss->path_grid * PT_RING_F4 * sizeof(pt::F4)) != hipSuccess)
-            return cleanup(fail(PT_E_OOM, "device allocation failed (path rings)"));
         if (ss->n_tiles_local) {
             // seeding order of the pass: the local tiles sorted by the Z-order (Morton)
             // code of their tile coordinates
@@ -1088,7 +1089,11 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.tile_order = tune_int("rowmajor", 0) ? nullptr : ss->tile_order;
     wp.sparse_steps = ss->sparse_steps;
     wp.coop_reserve = ss->coop_reserve;
-    wp.ring = ss->ring;
+    wp.shade_min = (uint32_t)std::max(0, tune_int("shade_min", 0));
+    wp.shade_wait = (uint32_t)std::max(0, tune_int("shade_wait", 0));
+    // aux stack words per query lane (PT_TUNE lstack=N < PT_LSTACK: tests of the exact-DFS
+    // hand-over of queries that outgrow it)
+    wp.lstack = std::min<uint32_t>(PT_LSTACK, (uint32_t)std::max(1, tune_int("lstack", (int)PT_LSTACK)));
     if (ss->on_progress && !ss->prog_host) {
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ss->prog_host), 8, hipHostMallocMapped | hipHostMallocCoherent));
         *ss->prog_host = 0ull;
@@ -1419,7 +1424,7 @@ void pt_session_free(pt_session* ss) {
     (void)hipFree(ss->tile_order);
     (void)hipFree(ss->gtile_dev);
     (void)hipFree(ss->qbuf); (void)hipFree(ss->hid); (void)hipFree(ss->pidbuf);
-    (void)hipFree(ss->carry); (void)hipFree(ss->ctl); (void)hipFree(ss->ring);
+    (void)hipFree(ss->carry); (void)hipFree(ss->ctl);
     if (ss->ctl_host) (void)hipHostFree(ss->ctl_host);
     if (ss->prog_host) (void)hipHostFree(ss->prog_host);
     if (ss->stream) {
@@ -1703,6 +1708,7 @@ int pt_write_ppm(const char* path, uint32_t W, uint32_t H, const uint8_t* rgb) {
 namespace {
 struct HostStack {
     std::vector<uint32_t> v;
+    uint32_t cap = 0xffffffffu;
     void set(uint32_t i, uint32_t x) { if (v.size() <= i) v.resize(i + 1); v[i] = x; }
     uint32_t get(uint32_t i) const { return v[i]; }
 };

@@ -218,6 +218,22 @@ def test_suspended_queries_resume_bit_exact(pt, name, budget, engine, monkeypatc
     assert np.array_equal(rgb, img)
 
 
+@pytest.mark.parametrize("name", ["dragon_64x64x16", "c3s4_win_944_520_16x16", "rabbid_48x48x4"])
+def test_aux_stack_overflow_takes_exact_dfs(pt, name, monkeypatch):
+    """A path-engine query whose pending aux items outgrow its LDS stack (PT_TUNE
+    lstack=1 here; PT_LSTACK words by default) hands its ray to the exact DFS:
+    same bytes and ray count, and the hand-over is counted."""
+    monkeypatch.setenv("PT_TUNE", "lstack=1,coop=0")
+    m, img, rad = U.golden_image(name)
+    with pt.Scene.load(U.golden_scene_path(name)) as s:
+        s.prepare()
+        win = tuple(m["window"]) if m["window"] else None
+        rgb, r, st = s.render(radiance=True, window=win)
+    assert st["errors"] == 0 and st["fallbacks"] > 0
+    assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
+    assert np.array_equal(rgb, img)
+
+
 def test_megakernel_engine_bit_exact(pt, monkeypatch):
     """PT_TUNE engine=mega: the megakernel (one lane per pixel, whole paths) on the
     replay traversal gives the same bytes as the path engine"""

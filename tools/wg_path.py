@@ -37,3 +37,8 @@ print("QW step: load wait %.0f + exec %.0f cycles per stepping trip; refill data
 print("SW per batch: ring read wait %.0f; shade_item phases: pixel+prim %.0f, vertex %.0f, fold+sum %.0f, next ray+store %.0f"
       % (tot[36] / max(tot[7], 1), tot[40] / max(tot[7], 1), tot[41] / max(tot[7], 1), tot[42] / max(tot[7], 1),
          tot[43] / max(tot[7], 1)))
+if tot[54:59].sum():
+    names = ["aux node", "probe", "leaf check", "walk entries", "walk nodes"]
+    print("QW exec by step kind (cycles per trip with that kind, share of trips): " + "; ".join(
+        "%s %.0f (%.2f)" % (n, tot[48 + i] / max(tot[54 + i], 1), tot[54 + i] / max(tot[2] - tot[4], 1)) for i, n in enumerate(names))
+        + "; before the first kind %.0f per stepping trip" % (tot[53] / max(tot[2] - tot[4], 1)))
