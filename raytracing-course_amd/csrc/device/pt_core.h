@@ -295,9 +295,10 @@ PT_HD bool isect_ellipsoid(const Ray& r, f3 rad, Hit& h) {
     return true;
 }
 
-// src/primitives.cpp:155-174 -- plane through the LOCAL ORIGIN
-PT_HD bool isect_triangle(const Ray& r, f3 a, f3 b, f3 c, Hit& h) {
-    const f3 n = normalize(cross(b - a, c - a));
+// src/primitives.cpp:155-174 -- plane through the LOCAL ORIGIN;
+// n = normalize(cross(b - a, c - a)) given (the query's records store it, computed
+// by the host with these same operations: bit-identical)
+PT_HD bool isect_triangle_n(const Ray& r, f3 a, f3 b, f3 c, f3 n, Hit& h) {
     Hit ph;
     if (!isect_plane(r, n, ph)) return false;
     const f3 p = r.o + ph.t * r.d;
@@ -306,6 +307,9 @@ PT_HD bool isect_triangle(const Ray& r, f3 a, f3 b, f3 c, Hit& h) {
     if (!(dot(cross(c - b, p - b), n) > 0.f)) return false;
     h = ph;
     return true;
+}
+PT_HD bool isect_triangle(const Ray& r, f3 a, f3 b, f3 c, Hit& h) {
+    return isect_triangle_n(r, a, b, c, normalize(cross(b - a, c - a)), h);
 }
 
 // src/primitives.cpp:14-52: world -> local by conj(q), test, normal back + renormalise

@@ -11,8 +11,14 @@ template <uint32_t STRIDE>
 struct LdsMemN {
     uint32_t* base;
     uint32_t cap = 0xffffffffu;   // words available (a query needing more takes the exact DFS)
+    uint32_t trash = 0u;          // a word setc may write when its condition is false (0: none)
     __device__ __forceinline__ void set(uint32_t i, uint32_t v) { base[i * STRIDE] = v; }
     __device__ __forceinline__ uint32_t get(uint32_t i) const { return base[i * STRIDE]; }
+    // set(i, v) if c; with a trash word the store is unconditional (no exec-mask branch)
+    __device__ __forceinline__ void setc(uint32_t i, uint32_t v, bool c) {
+        if (trash) base[(c ? i : trash) * STRIDE] = v;
+        else if (c) base[i * STRIDE] = v;
+    }
 };
 using LdsMem = LdsMemN<256u>;
 

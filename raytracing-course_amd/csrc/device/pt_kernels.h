@@ -119,8 +119,6 @@ struct WaveParams {
     const uint32_t* tile_order;   // k_wcamera: block b seeds local tile tile_order[b] (null: tile b)
     uint32_t sparse_steps;        // steps per loop trip of the end-of-pass (sparse) kernel
     uint32_t coop_reserve;        // k_wcoop: aux stack words kept free for a depth-first descent (3 (aux depth + 2))
-    uint32_t shade_min;           // k_wpath shade wave: batches of fewer items wait (s_sleep) up to ...
-    uint32_t shade_wait;          // ... this many shader clocks for more (0: never)
 };
 
 // path engine geometry: PT_NQ query waves + 1 shade wave per workgroup; at most
@@ -146,7 +144,7 @@ struct WaveParams {
 //   aux stack  PT_LSTACK words per query lane; a query that would need more takes the
 //              exact DFS (none of 10^6 measured queries needed more than 11)
 #define PT_DQN 64u
-#define PT_LSTACK 16u
+#define PT_LSTACK 16u                  // (+1 word per lane: the stack's trash word)
 
 // cooperative engine (k_wcoop, the end of a pass): one wave per chain, QC_WAVES
 // independent waves per workgroup, per-wave LDS for the query (pt_wave.hip QcLds)

@@ -99,11 +99,13 @@ enum : uint32_t { Q_AUX = 0u, Q_REPLAY = 1u, Q_DONE = 2u, Q_EXACT = 3u };
 enum : uint32_t { R_CAND = 0u, R_WALK_E = 1u, R_WALK_N = 2u };
 #define PT_RKINDS 3u
 
-// compact primitive records of the query (48 B, blob section o_qprim, same index
+// compact primitive records of the query (64 B, blob section o_qprim, same index
 // as the full 80-B records):
-//   plain triangle (pos = +0, rotation = (0,0,0,1) exactly): {a.xyz, T_TRIANGLE}, {b.xyz, c.x}, {c.y, c.z, -, -}
-//   box / ellipsoid:                                        {size.xyz, type}, {pos.xyz, rot.x}, {rot.yzw, -}
-//   anything else:                                           {-, -, -, type | PT_QP_FULL} -> full record
+//   plain triangle (pos = +0, rotation = (0,0,0,1) exactly): {a.xyz, T_TRIANGLE}, {b.xyz, n.x}, {c.xyz, n.y},
+//                           {n.z, -, -, -} with n = normalize(cross(b - a, c - a)) (host, same operations)
+//   box / ellipsoid:        {size.xyz, type}, {pos.xyz, rot.x}, {rot.yzw, -}, {-}
+//   anything else:          {-, -, -, type | PT_QP_FULL} -> full record
+#define PT_QPRIM_BYTES 64u
 #define PT_QP_FULL 0x100u
 
 // the full Prim a compact record stands for (bit-identical fields, so
@@ -115,8 +117,8 @@ PT_HD Prim qprim_expand(const F4& r0, const F4& r1, const F4& r2) {
         P.p0 = F4{0.f, 0.f, 0.f, r0.w};
         P.p1 = F4{0.f, 0.f, 0.f, 1.f};
         P.p2 = F4{r0.x, r0.y, r0.z, 0.f};
-        P.p3 = r1;
-        P.p4 = F4{r2.x, r2.y, 0.f, 0.f};
+        P.p3 = F4{r1.x, r1.y, r1.z, r2.x};
+        P.p4 = F4{r2.y, r2.z, 0.f, 0.f};
     } else {
         P.p0 = F4{r1.x, r1.y, r1.z, r0.w};
         P.p1 = F4{r1.w, r2.x, r2.y, r2.z};
@@ -129,8 +131,9 @@ PT_HD Prim qprim_expand(const F4& r0, const F4& r1, const F4& r2) {
 
 // leaf bundle (64 B, blob section o_bundle, one per reference leaf, numbered in
 // the order the wide aux nodes hold the leaves; the number -- the leaf's
-// "ordinal" -- is carried in its wide aux entry's b.z): the compact record of
-// the leaf's first primitive, then {leaf node index, first prim, prim count, 0}
+// "ordinal" -- is carried in its wide aux entry's b.z): the first three pieces of
+// the compact record of the leaf's first primitive, then {leaf node index, first
+// prim, prim count, the record's n.z}
 #define PT_BUNDLE_BYTES 64u
 #define PT_LEAFQ 0x80000000u    // Q_AUX item: a candidate leaf to probe (| its ordinal)
 
@@ -190,7 +193,7 @@ static_assert(PT_QHK < 16, "nh and ne are 4-bit fields");
 struct QCounts {
     uint32_t nodes, aux, ptests, planes;
 #ifdef PT_QDIAG
-    uint32_t cands, passes, steps;
+    uint32_t cands, passes, steps, rc_acc, rc_rej, rc_walk;
 #endif
 };
 
@@ -452,9 +455,11 @@ PT_HD void q_addr(const SceneView& S, const Query& q, uint32_t off[8]) {
             for (int k = 0; k < 8; ++k) off[k] = b0 + 16u * (uint32_t)(k < 5 ? k : 4);
             return;
         }
-        b0 = S.o_qprim + 48u * (q.lref + q.li);   // the leaf's next compact primitive
-        b1 = b0 + 16u;
-        b2 = b0 + 32u;
+        // the leaf's next compact primitive: 4 pieces
+        b0 = S.o_qprim + PT_QPRIM_BYTES * (q.lref + q.li);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) off[k] = b0 + 16u * (uint32_t)(k < 4 ? k : 3);
+        return;
     } else if (q.walk == R_CAND) {
         b0 = S.o_nodes + 32u * q.cand;
         b1 = b0 + 16u;
@@ -536,6 +541,10 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
         // the largest listed hitting leaf when the list is full (else none): a leaf
         // above it could only join the list to drop out again
         const uint32_t hmax = q.hidx[PT_QHK - 1];
+        // (bookkeeping in locals and selects: the packed fields are written once, and a
+        // stack push is one store whatever the entry -- no per-entry exec-mask branches)
+        uint32_t sp = q.sp;
+        bool ovf = false;
 #pragma unroll
         for (int k = 0; k < PT_AUXW; ++k) {
             // every entry's box is conservative: a reference leaf passing it is a
@@ -553,20 +562,21 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
             const bool above = isleaf ? lidx > hmax
                                       : (hmax != 0xffffffffu && ((rng & 0xffffu) << S.aux_rshift) > hmax);
             const bool fresh = isleaf ? lidx >= q.lb : ((rng >> 16) << S.aux_rshift) >= q.lb;
-            if (h && fresh && above) q.overflow = 1u;
+            ovf = ovf || (h && fresh && above);
             const bool take = h && fresh && !above;
             const uint32_t item = isleaf ? (PT_LEAFQ | rng) : code;
-            const bool push = take && next != 0xffffffffu;
-            if (take && next == 0xffffffffu) next = item;
-            if (push) {
-                if (q.sp < stk.cap) stk.set(q.sp, item);
-                q.sp++;   // (past the stack's capacity: the exact DFS below)
-            }
+            const bool first = take && next == 0xffffffffu;
+            const bool push = take && !first;
+            next = first ? item : next;
+            stk.setc(sp, item, push && sp < stk.cap);
+            sp += push ? 1u : 0u;   // (past the stack's capacity: the exact DFS below)
         }
-        if (q.sp > stk.cap) {
+        if (ovf) q.overflow = 1u;
+        if (sp > stk.cap) {
             q.phase = Q_EXACT;   // the pending items do not fit the stack: exact DFS (same result)
             return;
         }
+        q.sp = sp;
 #ifdef PT_QDIAG
         if (next == 0xffffffffu && q.sp == 0u) C.passes++;
         if (q.sp > C.steps) C.steps = q.sp;   // (diagnostics: the deepest aux stack of the query)
@@ -609,24 +619,36 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
         // A plain triangle (compact: pos = +0, identity rotation) is tested on the world
         // ray: the world->local rotation changes at most the sign of zero components,
         // which changes neither the accept decision nor t (a signed zero only matters in
-        // a sum that is exactly zero, where every compare here is false either way).
-        // Every other record goes to local space exactly as Primitive::Intersect does.
+        // a sum that is exactly zero, where every compare here is false either way).  The
+        // same holds for the rotation of any record whose rotation is exactly (0,0,0,1)
+        // (only t is wanted here, not the normal): its local ray is (o - pos, d).  Other
+        // records go to local space exactly as Primitive::Intersect does.
         Ray lr = q.ray;
         if (full || cty != T_TRIANGLE) {
             const f3 pos = mk3(pr.p0.x, pr.p0.y, pr.p0.z);
-            q4 qq;
-            qq.x = pr.p1.x; qq.y = pr.p1.y; qq.z = pr.p1.z; qq.w = pr.p1.w;
-            const q4 cq = conj(qq);
-            lr.o = qrot(cq, q.ray.o + -1.f * pos);
-            lr.d = qrot(cq, q.ray.d);
+            lr.o = q.ray.o + -1.f * pos;
+            const bool ident = f2u(pr.p1.x) == 0u && f2u(pr.p1.y) == 0u && f2u(pr.p1.z) == 0u &&
+                               f2u(pr.p1.w) == 0x3f800000u;
+            if (!ident) {
+                q4 qq;
+                qq.x = pr.p1.x; qq.y = pr.p1.y; qq.z = pr.p1.z; qq.w = pr.p1.w;
+                const q4 cq = conj(qq);
+                lr.o = qrot(cq, lr.o);
+                lr.d = qrot(cq, q.ray.d);
+            }
         }
         const f3 pa = mk3(pr.p2.x, pr.p2.y, pr.p2.z);
         bool ok;
         float t = 0.f;
         uint32_t in;
         if (ty == T_TRIANGLE) {
+            const f3 pb = mk3(pr.p3.x, pr.p3.y, pr.p3.z), pc = mk3(pr.p3.w, pr.p4.x, pr.p4.y);
+            // a compact record carries the triangle's normal (n.z: in the bundle's header
+            // piece, or the record's fourth piece)
+            f3 n = mk3(r[1].w, r[2].w, q.li == 0u ? r[3].w : r[3].x);
+            if (full) n = normalize(cross(pb - pa, pc - pa));
             Hit h;
-            ok = isect_triangle(lr, pa, mk3(pr.p3.x, pr.p3.y, pr.p3.z), mk3(pr.p3.w, pr.p4.x, pr.p4.y), h);
+            ok = isect_triangle_n(lr, pa, pb, pc, n, h);
             t = h.t;
         } else if (ty == T_BOX) {
             ok = slab(lr.o, lr.d, pa, t, in);
@@ -657,6 +679,9 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
         const uint32_t info = f2u(k4 == 0u ? r[2].x : k4 == 1u ? r[2].y : k4 == 2u ? r[2].z : r[2].w);
         C.nodes++;
         const uint32_t v = q_leaf_certain(q, nd);
+#ifdef PT_QDIAG
+        if (v == 1u) C.rc_acc++; else if (v == 0u) C.rc_rej++; else C.rc_walk++;
+#endif
         if (v == 1u) {
             q_entered(q);
             return;

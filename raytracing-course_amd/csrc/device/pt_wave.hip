@@ -72,7 +72,8 @@ __device__ __forceinline__ Ray camera_sample(const CamView& cam, Rng& R, uint32_
 // to the chain's next ray (the child, or the next sample's camera ray); false
 // when the pixel has reached this pass's target.  `ray` enters as the query ray.
 // `sdone` returns whether a sample of the pixel ended here.
-__device__ __forceinline__ bool shade_item(const WaveParams& P, uint32_t slot, Ray& ray, uint32_t hid,
+template <class EM>
+__device__ __forceinline__ bool shade_item(const WaveParams& P, const EM& em, uint32_t slot, Ray& ray, uint32_t hid,
                                            bool& sdone PF_ARGS) {
     bool emit = false;
 #ifdef PT_WPROF
@@ -95,7 +96,7 @@ __device__ __forceinline__ bool shade_item(const WaveParams& P, uint32_t slot, R
         PF_MARK(0);   // pixel record + prim loads, the hit recomputed
         uint32_t idm;
         float s1, s2;
-        const bool cont = shade_vertex(P.S, R, ray, h, (int)hid, idm, s1, s2);
+        const bool cont = shade_vertex_e(P.S, em, P.S.shade[hid], R, ray, h, (int)hid, idm, s1, s2);
         PF_MARK(1);   // the vertex: material, sampling, pdfs
         HbmVStore vs = fold_store(P.st, slot);
         vs.put(nv, idm, s1, s2);
@@ -229,6 +230,20 @@ __global__ void __launch_bounds__(256) k_wcamera_merge(WaveParams P) {
 // shade wave, last out, hands the remaining chains' next rays to the fresh queue
 // of the next round.  Rounds then only rebalance chains between workgroups.
 //
+// LDS accessors with the address space spelled out (a reference to a __shared__ member is a
+// generic pointer, which the compiler may otherwise lower to flat instructions)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PT_LDS __attribute__((address_space(3)))
+#else
+#define PT_LDS
+#endif
+__device__ __forceinline__ uint32_t lds_read(const uint32_t& v) { return *(const volatile PT_LDS uint32_t*)&v; }
+__device__ __forceinline__ void lds_write(uint32_t& v, uint32_t x) { *(volatile PT_LDS uint32_t*)&v = x; }
+template <class T>
+__device__ __forceinline__ T lds_get(const T* a, uint32_t i) { return ((const PT_LDS T*)a)[i]; }
+template <class T>
+__device__ __forceinline__ void lds_put(T* a, uint32_t i, const T& v) { ((PT_LDS T*)a)[i] = v; }
+
 // Rings: entries and positions in LDS, ordered by workgroup-scope release/acquire
 // fences.  Every ring has ONE producer, which publishes its entries in order, so a
 // consumer takes a contiguous range: the ray ring is written by the shade wave, and
@@ -249,22 +264,42 @@ struct PathLds {
     int rq_pid[PT_CMAX];          //           closest plane
     F4 dq_ro[PT_NQ][PT_DQN];      // done rings: {o.xyz, slot}
     F4 dq_rd[PT_NQ][PT_DQN];      //             {d.xyz, u32 closest prim | 0xffffffff}
-    uint32_t stk[PT_LSTACK * 64u * PT_NQ];   // query lanes' aux stacks, [word][lane]
+    uint32_t stk[(PT_LSTACK + 1u) * 64u * PT_NQ];   // query lanes' aux stacks, [word][lane] (+ a trash word)
+    // the shade wave's copies of the first planes and emitters (any further ones: HBM)
+    F4 pl[QC_NPL * 5u];
+    F4 em[QC_NEM * 5u];
+    uint32_t pl_id[QC_NPL];
+};
+// the first QC_NPL planes / QC_NEM emitters from the workgroup's LDS copy, any further ones from HBM
+struct PlanesPath {
+    const PathLds& L;
+    const SceneView& S;
+    __device__ Prim operator()(uint32_t k, uint32_t& pi) const {
+        if (k < QC_NPL) {
+            pi = lds_get(L.pl_id, k);
+            Prim p;
+            p.p0 = lds_get(L.pl, 5u * k); p.p1 = lds_get(L.pl, 5u * k + 1u); p.p2 = lds_get(L.pl, 5u * k + 2u);
+            p.p3 = lds_get(L.pl, 5u * k + 3u); p.p4 = lds_get(L.pl, 5u * k + 4u);
+            return p;
+        }
+        pi = S.planes[k];
+        return S.prims[pi];
+    }
+};
+struct EmitPath {
+    const PathLds& L;
+    const SceneView& S;
+    __device__ Prim operator()(uint32_t k) const {
+        if (k < QC_NEM) {
+            Prim p;
+            p.p0 = lds_get(L.em, 5u * k); p.p1 = lds_get(L.em, 5u * k + 1u); p.p2 = lds_get(L.em, 5u * k + 2u);
+            p.p3 = lds_get(L.em, 5u * k + 3u); p.p4 = lds_get(L.em, 5u * k + 4u);
+            return p;
+        }
+        return S.prims[S.emitters[k]];
+    }
 };
 
-// LDS accessors with the address space spelled out (a reference to a __shared__ member is a
-// generic pointer, which the compiler may otherwise lower to flat instructions)
-#if defined(__HIP_DEVICE_COMPILE__)
-#define PT_LDS __attribute__((address_space(3)))
-#else
-#define PT_LDS
-#endif
-__device__ __forceinline__ uint32_t lds_read(const uint32_t& v) { return *(const volatile PT_LDS uint32_t*)&v; }
-__device__ __forceinline__ void lds_write(uint32_t& v, uint32_t x) { *(volatile PT_LDS uint32_t*)&v = x; }
-template <class T>
-__device__ __forceinline__ T lds_get(const T* a, uint32_t i) { return ((const PT_LDS T*)a)[i]; }
-template <class T>
-__device__ __forceinline__ void lds_put(T* a, uint32_t i, const T& v) { ((PT_LDS T*)a)[i] = v; }
 
 
 #define PT_PATH_REFILL_MIN 8u      // idle lanes before a query wave refills (any, once the round's work is out)
@@ -277,7 +312,7 @@ __device__ __forceinline__ void lds_put(T* a, uint32_t i, const T& v) { ((PT_LDS
 // weigh on the main kernel.
 template <bool SPARSE>
 __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L, uint32_t qw) {
-    LdsMemN<64u * PT_NQ> stk{L.stk + 64u * qw + lane_id(), P.lstack};
+    LdsMemN<64u * PT_NQ> stk{L.stk + 64u * qw + lane_id(), P.lstack, PT_LSTACK};
     const uint32_t p = P.parity;
     const uint32_t* in = P.ctl + PT_CTL_SET * p;
     uint32_t* out = P.ctl + PT_CTL_SET * (1u - p);
@@ -689,8 +724,6 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
     uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // shade_item phases
 #endif
     uint32_t prog = 0u;               // finished samples not yet added to P.progress
-    bool waiting = false;             // holding back a small batch (since wait_t0)
-    uint64_t wait_t0 = 0;
     for (;;) {
         // published entries of the done rings (ring indices are compile-time: no scratch)
         uint32_t av[PT_NQ], total = 0u;
@@ -714,22 +747,6 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
-        // A batch costs about the same instructions for 1 or 64 items, and the shade wave
-        // shares its SIMD's issue with query waves: with many chains in flight, a small
-        // batch may wait (sleeping) for more items (P.shade_min / P.shade_wait)
-        if (total < P.shade_min && lds_read(L.qw_done) != PT_NQ &&
-            total * 4u < (uint32_t)__builtin_amdgcn_readfirstlane(lds_read(L.resident))) {
-            const uint64_t now = __builtin_amdgcn_s_memtime();
-            if (!waiting) {
-                waiting = true;
-                wait_t0 = now;
-            }
-            if (now - wait_t0 < P.shade_wait) {
-                __builtin_amdgcn_s_sleep(2);
-                continue;
-            }
-        }
-        waiting = false;
         // up to 64 of them: a fair share of each ring first (a full ring holds back its
         // producer's finished queries), then the rest in ring order
         uint32_t take[PT_NQ], n = 0u;
@@ -784,7 +801,7 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
             slot = f2u(o.w);
             ray.o = mk3(o.x, o.y, o.z);
             ray.d = mk3(d.x, d.y, d.z);
-            emit = shade_item(P, slot, ray, f2u(d.w), sdone PF_PASS);
+            emit = shade_item(P, EmitPath{L, P.S}, slot, ray, f2u(d.w), sdone PF_PASS);
         }
 #ifdef PT_WPROF
         const uint64_t c2 = __builtin_amdgcn_s_memtime();
@@ -810,7 +827,7 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
                 const uint32_t e = (tail + lanes_below(me)) % PT_CMAX;
                 float pt;
                 int pid;
-                q_planes(P.S, ray, pt, pid);
+                q_planes_e(P.S, PlanesPath{L, P.S}, ray, pt, pid);
                 lds_put(L.rq_ro, e, F4{ray.o.x, ray.o.y, ray.o.z, u2f(slot)});
                 lds_put(L.rq_rd, e, F4{ray.d.x, ray.d.y, ray.d.z, pt});
                 lds_put(L.rq_pid, e, pid);
@@ -864,6 +881,16 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
 template <bool SPARSE>
 __global__ void __launch_bounds__(PT_PATH_WG) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAVES_PER_EU, PT_PATH_WAVES_PER_EU))) k_wpath(WaveParams P) {
     __shared__ PathLds L;
+    {
+        // the first planes and emitters (the shade wave's plane tests and light sampling)
+        const uint32_t npl = (P.S.n_planes < QC_NPL ? P.S.n_planes : QC_NPL) * 5u;
+        const uint32_t nem = (P.S.n_emitters < QC_NEM ? P.S.n_emitters : QC_NEM) * 5u;
+        for (uint32_t i = threadIdx.x; i < npl; i += blockDim.x)
+            lds_put(L.pl, i, reinterpret_cast<const F4*>(P.S.prims + P.S.planes[i / 5u])[i % 5u]);
+        for (uint32_t i = threadIdx.x; i < nem; i += blockDim.x)
+            lds_put(L.em, i, reinterpret_cast<const F4*>(P.S.prims + P.S.emitters[i / 5u])[i % 5u]);
+        if (threadIdx.x < npl / 5u) lds_put(L.pl_id, threadIdx.x, P.S.planes[threadIdx.x]);
+    }
     if (threadIdx.x == 0u) {
         L.rq_head = L.rq_tail = L.resident = L.qw_done = 0u;
     }
@@ -942,11 +969,14 @@ struct EmitLds {
 // normal goes through the same last step, normalize(qrot(rotation, n)), so the Hit
 // has the full test's bits; other records expand to the full form.
 __device__ __forceinline__ bool qc_prim_hit(const SceneView& S, uint32_t i, const Ray& ray, Hit& h) {
-    const uint32_t o = S.o_qprim + 48u * i;
-    const F4 r0 = blob_piece(S, o), r1 = blob_piece(S, o + 16u), r2 = blob_piece(S, o + 32u);
+    const uint32_t o = S.o_qprim + PT_QPRIM_BYTES * i;
+    const F4 r0 = blob_piece(S, o), r1 = blob_piece(S, o + 16u), r2 = blob_piece(S, o + 32u),
+             r3 = blob_piece(S, o + 48u);
     const uint32_t ty = f2u(r0.w);
     if (ty == T_TRIANGLE) {
-        if (!isect_triangle(ray, mk3(r0.x, r0.y, r0.z), mk3(r1.x, r1.y, r1.z), mk3(r1.w, r2.x, r2.y), h)) return false;
+        if (!isect_triangle_n(ray, mk3(r0.x, r0.y, r0.z), mk3(r1.x, r1.y, r1.z), mk3(r2.x, r2.y, r2.z),
+                              mk3(r1.w, r2.w, r3.x), h))
+            return false;
         q4 q;
         q.x = 0.f; q.y = 0.f; q.z = 0.f; q.w = 1.f;
         h.n = normalize(qrot(q, h.n));
@@ -1481,7 +1511,7 @@ __global__ void __launch_bounds__(256) k_wshade(WaveParams P) {
             slot = f2u(o.w);
             ray.o = mk3(o.x, o.y, o.z);
             ray.d = mk3(d.x, d.y, d.z);
-            emit = shade_item(P, slot, ray, hid, sdone PF_PASS);
+            emit = shade_item(P, EmitGlobal{P.S}, slot, ray, hid, sdone PF_PASS);
         }
         if (P.progress) {
             const uint32_t nd = (uint32_t)__popcll(__ballot(sdone));

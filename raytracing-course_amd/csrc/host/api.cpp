@@ -81,8 +81,6 @@ const Rccl& rccl() {
 //   round_batch=N     path rounds launched per chain count while the chains are far above
 //                     the hand-over (default 1)
 //   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
-//   shade_min=N, shade_wait=C  path engine: a shade batch of fewer than N items waits up to C
-//                     shader clocks for more while many chains are in flight (default 0: off)
 //   cap=N             chains a workgroup may hold
 //   lstack=N          aux stack words a path-engine query may use (default and maximum PT_LSTACK;
 //                     a query needing more takes the exact DFS)
@@ -446,7 +444,7 @@ void build_query_blob(pt_scene* s) {
     b.clear();
     // every section's 16-B pieces, reserved at once (the blob is tens of MB)
     b.reserve(s->dnodes.size() * 2 + s->auxsl.size() * 2 + (s->anc_info.size() + s->anc.size()) / 4 +
-              s->dprims.size() * (3 + 5 + 4) + 64);
+              s->dprims.size() * (4 + 5 + 4) + 64);
     auto append = [&b](const void* p, size_t bytes) {
         const uint32_t o = (uint32_t)(b.size() * 16);
         const size_t n = (bytes + 15) / 16;
@@ -475,30 +473,35 @@ void build_query_blob(pt_scene* s) {
     s->o_aux = append(aux.data(), aux.size() * sizeof(pt::AuxSL));
     s->o_ainfo = append(s->anc_info.data(), s->anc_info.size() * 4);
     s->o_anc = append(s->anc.data(), s->anc.size() * 4);
-    std::vector<pt::F4> qp(3 * s->dprims.size());
+    std::vector<pt::F4> qp(4 * s->dprims.size());
     for (size_t i = 0; i < s->dprims.size(); ++i) {
         const pt::Prim& P = s->dprims[i];
         const uint32_t type = pt::f2u(P.p0.w);
         const bool pos0 = pt::f2u(P.p0.x) == 0u && pt::f2u(P.p0.y) == 0u && pt::f2u(P.p0.z) == 0u;
         const bool rot1 = pt::f2u(P.p1.x) == 0u && pt::f2u(P.p1.y) == 0u && pt::f2u(P.p1.z) == 0u &&
                           pt::f2u(P.p1.w) == 0x3f800000u;
-        pt::F4* r = &qp[3 * i];
+        pt::F4* r = &qp[4 * i];
         if (type == pt::T_TRIANGLE && pos0 && rot1) {
-            r[0] = pt::F4{P.p2.x, P.p2.y, P.p2.z, P.p0.w};
-            r[1] = P.p3;
-            r[2] = pt::F4{P.p4.x, P.p4.y, 0.f, 0.f};
+            // with the triangle's normal exactly as IntersectTriangle computes it
+            const pt::f3 a = pt::mk3(P.p2.x, P.p2.y, P.p2.z), b = pt::mk3(P.p3.x, P.p3.y, P.p3.z),
+                         c = pt::mk3(P.p3.w, P.p4.x, P.p4.y);
+            const pt::f3 n = pt::normalize(pt::cross(b - a, c - a));
+            r[0] = pt::F4{a.x, a.y, a.z, P.p0.w};
+            r[1] = pt::F4{b.x, b.y, b.z, n.x};
+            r[2] = pt::F4{c.x, c.y, c.z, n.y};
+            r[3] = pt::F4{n.z, 0.f, 0.f, 0.f};
         } else if (type == pt::T_BOX || type == pt::T_ELLIPSOID) {
             r[0] = pt::F4{P.p2.x, P.p2.y, P.p2.z, P.p0.w};
             r[1] = pt::F4{P.p0.x, P.p0.y, P.p0.z, P.p1.x};
             r[2] = pt::F4{P.p1.y, P.p1.z, P.p1.w, 0.f};
         } else {
             r[0] = pt::F4{0.f, 0.f, 0.f, pt::u2f(type | PT_QP_FULL)};
-            r[1] = r[2] = pt::F4{0.f, 0.f, 0.f, 0.f};
+            r[1] = r[2] = r[3] = pt::F4{0.f, 0.f, 0.f, 0.f};
         }
     }
     s->o_qprim = append(qp.data(), qp.size() * sizeof(pt::F4));
-    // leaf bundles (pt_query.h): the compact record of the leaf's first primitive,
-    // then {leaf node index, first primitive, primitive count, 0}
+    // leaf bundles (pt_query.h): the compact record of the leaf's first primitive
+    // (pieces 0-2), then {leaf node index, first primitive, primitive count, its n.z}
     std::vector<pt::F4> bu(4 * leaves.size());
     for (size_t k = 0; k < leaves.size(); ++k) {
         const pt::Node& n = s->dnodes[leaves[k]];
@@ -506,9 +509,9 @@ void build_query_blob(pt_scene* s) {
         const uint32_t first = pt::f2u(n.b.z), cnt = pt::f2u(n.b.w);
         if (cnt) {
             if (first >= s->dprims.size()) throw std::runtime_error("leaf primitive out of range");
-            r[0] = qp[3 * first]; r[1] = qp[3 * first + 1]; r[2] = qp[3 * first + 2];
+            r[0] = qp[4 * first]; r[1] = qp[4 * first + 1]; r[2] = qp[4 * first + 2];
         }
-        r[3] = pt::F4{pt::u2f(leaves[k]), pt::u2f(first), pt::u2f(cnt), 0.f};
+        r[3] = pt::F4{pt::u2f(leaves[k]), pt::u2f(first), pt::u2f(cnt), cnt ? qp[4 * first + 3].x : 0.f};
     }
     s->o_bundle = append(bu.data(), bu.size() * sizeof(pt::F4));
     s->o_prim = append(s->dprims.data(), s->dprims.size() * sizeof(pt::Prim));
@@ -1089,8 +1092,6 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.tile_order = tune_int("rowmajor", 0) ? nullptr : ss->tile_order;
     wp.sparse_steps = ss->sparse_steps;
     wp.coop_reserve = ss->coop_reserve;
-    wp.shade_min = (uint32_t)std::max(0, tune_int("shade_min", 0));
-    wp.shade_wait = (uint32_t)std::max(0, tune_int("shade_wait", 0));
     // aux stack words per query lane (PT_TUNE lstack=N < PT_LSTACK: tests of the exact-DFS
     // hand-over of queries that outgrow it)
     wp.lstack = std::min<uint32_t>(PT_LSTACK, (uint32_t)std::max(1, tune_int("lstack", (int)PT_LSTACK)));
@@ -1709,6 +1710,7 @@ namespace {
 struct HostStack {
     std::vector<uint32_t> v;
     uint32_t cap = 0xffffffffu;
+    void setc(uint32_t i, uint32_t x, bool c) { if (c) set(i, x); }
     void set(uint32_t i, uint32_t x) { if (v.size() <= i) v.resize(i + 1); v[i] = x; }
     uint32_t get(uint32_t i) const { return v[i]; }
 };
@@ -1803,7 +1805,7 @@ int pt_selftest_render_host(pt_scene* s, int32_t traversal, uint32_t x0, uint32_
                             cc.fallbacks += ex;
                             if (Q.planes & 0x80000000u) cc.errs |= 4u;   // recomputed hit differs (checked below)
 #ifdef PT_QDIAG
-                            if (qlog) qlog->push_back({Q.aux, Q.steps, Q.ptests | (ex << 31), Q.cands | (Q.passes << 16)});
+                            if (qlog) qlog->push_back({Q.aux, Q.rc_acc | (Q.rc_rej << 16), Q.rc_walk, Q.cands | (Q.passes << 16)});
 #else
                             if (qlog) qlog->push_back({Q.aux, Q.nodes, Q.ptests | (ex << 31), 0u});
 #endif
