@@ -314,7 +314,7 @@ def roofline(st0, st1, traffic_json, key):
     alg_bytes = (nodes * st1["node_bytes"] + ptests * st1["prim_bytes"] + auxv * st1["aux_bytes"]) / launches
     launch_s = (isect_ms / 1e3) / launches
     achieved = alg_bytes / launch_s / 1e9 if launch_s > 0 else 0.0
-    rec = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+    rec = {"bound": "hbm", "priced_against": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_wpath",
            "alg_bytes_per_launch": alg_bytes, "launch_ms": launch_s * 1e3, "launches": launches,
            "rays_share": (d["rays"] - d["coop_rays"]) / max(d["rays"], 1),
@@ -348,8 +348,12 @@ def roofline(st0, st1, traffic_json, key):
                 "wave_wait_any_frac": prof["wait_any_frac"],
                 "source": "profiles/%s SQ_ACTIVE_INST_VALU / SQ_INSTS_VALU / SQ_WAIT_ANY per wave-cycle"
                           % prof.get("profile", "?")}
-    rec["note"] = ("algorithmic = 4-wide aux BVH nodes (128 B) + reference node records (32 B) + compact primitive "
-                   "records (48 B; a probe's 64-B leaf bundle counts its primitive) per visit; the ~30 MB working set "
+            # `bound` names what the counters say limits the kernel; `peak`/`frac` stay priced
+            # against HBM (the kernel has no MFMA work)
+            rec["bound"] = rec["limiter"]["verdict"]
+    rec["note"] = ("algorithmic = 4-wide aux BVH nodes (128 B) + reference node records (32 B) + primitive geometry "
+                   "(48 B; the 64-B compact record adds a precomputed normal, a probe's 96-B leaf bundle carries its "
+                   "first primitive and the leaf box) per visit; the ~30 MB working set "
                    "is L2/Infinity-Cache resident; the query's work per ray fell from ~1.5 KB (round 1) to ~0.7 KB, so "
                    "frac falls as Mray/s rises; what limits the kernel is in `limiter` (rocprofv3 SQ counters, "
                    "DESIGN.md §4)")

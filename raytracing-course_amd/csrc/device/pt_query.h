@@ -94,7 +94,7 @@ PT_HD bool aux_entry_hit(const F4& ea, const F4& eb, const Ray& ray, f3 inv, f3 
 struct AuxSL { F4 a, b; };
 #define PT_AUX_INTERNAL 0xffffffffu
 
-enum : uint32_t { Q_AUX = 0u, Q_REPLAY = 1u, Q_DONE = 2u, Q_EXACT = 3u };
+enum : uint32_t { Q_AUX = 0u, Q_REPLAY = 1u, Q_DONE = 2u, Q_EXACT = 3u, Q_DECIDE = 4u };
 // replay step kinds: each issues one round of independent loads
 enum : uint32_t { R_CAND = 0u, R_WALK_E = 1u, R_WALK_N = 2u };
 #define PT_RKINDS 3u
@@ -129,12 +129,13 @@ PT_HD Prim qprim_expand(const F4& r0, const F4& r1, const F4& r2) {
     return P;
 }
 
-// leaf bundle (64 B, blob section o_bundle, one per reference leaf, numbered in
+// leaf bundle (96 B, blob section o_bundle, one per reference leaf, numbered in
 // the order the wide aux nodes hold the leaves; the number -- the leaf's
 // "ordinal" -- is carried in its wide aux entry's b.z): the first three pieces of
 // the compact record of the leaf's first primitive, then {leaf node index, first
-// prim, prim count, the record's n.z}
-#define PT_BUNDLE_BYTES 64u
+// prim, prim count, the record's n.z}, then the leaf's node record box {c.xyz,
+// s.x}, {s.y, s.z, -, -} (the probe prices its certain accept, q_leaf_accept_t)
+#define PT_BUNDLE_BYTES 96u
 #define PT_LEAFQ 0x80000000u    // Q_AUX item: a candidate leaf to probe (| its ordinal)
 
 #ifndef PT_QHK
@@ -146,7 +147,7 @@ struct Query {
     f3 inv;                     // 1/d (IEEE, once per ray)
     float P;                    // closest plane t (the BVH bound at the root)
     // small state packed into two registers
-    uint32_t phase : 2;         // Q_*
+    uint32_t phase : 3;         // Q_* (Q_DECIDE only inside q_exec)
     uint32_t walk : 2;          // Q_REPLAY step kind: R_CAND, R_WALK_E, R_WALK_N
     uint32_t par : 1;           // near-zero direction component: exact node tests, robust aux boxes
     uint32_t robust : 1;        // leaf check: the ray crosses the leaf box robustly (t1c, mc valid)
@@ -157,7 +158,7 @@ struct Query {
     uint32_t len : 7;           // walk: ancestor list length
     uint32_t nh : 4;            // hitting leaves in the list (<= PT_QHK)
     uint32_t ne : 4;            // ... of which the first ne are decided and entered (the recorded hits)
-    uint32_t spare : 24;        // (fills the word: a narrower unit is accessed bytewise, which keeps
+    uint32_t spare : 23;        // (fills the word: a narrower unit is accessed bytewise, which keeps
                                 //  the whole Query out of registers)
     uint32_t node;              // Q_AUX: aux node, or PT_LEAFQ | ordinal of the leaf being probed
     uint32_t lb;                // every hitting leaf below lb has been decided
@@ -171,6 +172,7 @@ struct Query {
             uint32_t li;                // probe: primitives tested (bit 31: this step = full record)
             float lt;                   // probe: leaf first-min t so far
             int lid;                    // probe: its primitive (-1 none)
+            float lacc;                 // probe: the leaf's certain-accept threshold
         };
         struct {
             uint32_t off;               // walk: ancestor list offset
@@ -183,6 +185,7 @@ struct Query {
     uint32_t hidx[PT_QHK];      // hitting leaves (reference index, sorted; 0xffffffff = empty)
     float ht[PT_QHK];           // ... their first-min t
     int hid[PT_QHK];            // ... and its primitive
+    float hacc[PT_QHK];         // ... and its certain-accept threshold (q_leaf_accept_t)
     float bt;                   // best BVH leaf hit so far (first strict minimum)
     float res_t;                // result so far (plane, then BVH hits that beat it): t and prim;
     int res_id;                 // the normal is recomputed from the prim by the consumer
@@ -293,7 +296,7 @@ PT_HD T q_sel(const T (&a)[PT_QHK], uint32_t k, T dflt) {
 // the list full the largest entry (undecided: it is above c >= lb) or c itself
 // drops out and another pass follows.  Returns false when every slot holds an
 // entered hit (the exact DFS takes the ray).
-PT_HD bool q_add_hit(Query& q, uint32_t c, float t, int id) {
+PT_HD bool q_add_hit(Query& q, uint32_t c, float t, int id, float acc) {
     if (q.ne == PT_QHK) return false;
 #pragma unroll
     for (int k = 0; k < PT_QHK; ++k) {
@@ -301,9 +304,10 @@ PT_HD bool q_add_hit(Query& q, uint32_t c, float t, int id) {
         const uint32_t xi = q.hidx[k];
         const float xt = q.ht[k];
         const int xd = q.hid[k];
+        const float xa = q.hacc[k];
         if (sw) {
-            q.hidx[k] = c; q.ht[k] = t; q.hid[k] = id;
-            c = xi; t = xt; id = xd;
+            q.hidx[k] = c; q.ht[k] = t; q.hid[k] = id; q.hacc[k] = acc;
+            c = xi; t = xt; id = xd; acc = xa;
         }
     }
     if (c != 0xffffffffu) q.overflow = 1u;   // a hitting leaf above the kept ones dropped out
@@ -328,22 +332,11 @@ PT_HD void q_pass_done(Query& q) {
     q.phase = Q_DONE;
 }
 
-// decide the next undecided hitting leaf, if any
-PT_HD void q_next_decision(Query& q) {
-    if (q.ne < q.nh) {
-        q.cand = q_sel(q.hidx, q.ne, 0xffffffffu);
-        q.walk = R_CAND;
-        q.phase = Q_REPLAY;
-        return;
-    }
-    q_pass_done(q);
-}
-
-// hitting leaf hidx[ne] is entered: it becomes a recorded hit
+// hitting leaf hidx[ne] (= cand) is entered: it becomes a recorded hit
 // (src/bvh.cpp:205-213 + the recursion's fold: the BVH result is the first
 // strict minimum over entered hits in preorder; it replaces the plane hit iff
 // strictly closer, src/scene.cpp:68-74)
-PT_HD void q_entered(Query& q) {
+PT_HD void q_record_entered(Query& q) {
     const float t = q_sel(q.ht, q.ne, PT_INF);
     const int id = q_sel(q.hid, q.ne, -1);
     if (t < q.bt) {
@@ -352,7 +345,33 @@ PT_HD void q_entered(Query& q) {
     }
     q.ne = q.ne + 1u;
     q.lb = q.cand + 1u;
+}
+
+// the next undecided hitting leaf is decided at the end of the step (q_decide)
+PT_HD void q_next_decision(Query& q) { q.phase = Q_DECIDE; }
+
+PT_HD void q_entered(Query& q) {
+    q_record_entered(q);
     q_next_decision(q);
+}
+
+// End of a step that left the lane at a decision (phase Q_DECIDE; one place in
+// the code): hitting leaves whose precomputed certain accept holds (q_leaf_certain's
+// first case: lo = min(P, recorded hits) = min(P, bt) >= the threshold the probe
+// computed, q_leaf_accept_t) are entered here; the first other one gets the leaf
+// check (R_CAND), or the pass is done.
+PT_HD void q_decide(Query& q) {
+#pragma unroll 1
+    while (q.ne < q.nh) {
+        q.cand = q_sel(q.hidx, q.ne, 0xffffffffu);
+        if (!(fminf(q.P, q.bt) >= q_sel(q.hacc, q.ne, PT_INF))) {
+            q.walk = R_CAND;
+            q.phase = Q_REPLAY;
+            return;
+        }
+        q_record_entered(q);
+    }
+    q_pass_done(q);
 }
 
 // hitting leaf hidx[ne] is not entered: it leaves the list (an unentered leaf
@@ -364,6 +383,7 @@ PT_HD void q_rejected(Query& q) {
             q.hidx[k] = q.hidx[k + 1];
             q.ht[k] = q.ht[k + 1];
             q.hid[k] = q.hid[k + 1];
+            q.hacc[k] = q.hacc[k + 1];
         }
     }
     q.hidx[PT_QHK - 1] = 0xffffffffu;
@@ -385,6 +405,25 @@ PT_HD float q_bound_between(const Query& q, uint32_t a, uint32_t r) {
         }
     }
     return m;
+}
+
+// The certain-accept threshold of a leaf (q_leaf_certain's first case, computed by
+// the probe from the bundle's copy of the leaf's node record, the same floats and
+// operations): the leaf is entered whenever lo = min(P, recorded hits) >= it;
+// +inf if the ray does not cross the leaf box robustly.
+PT_HD float q_leaf_accept_t(const Query& q, const F4& na, const F4& nb) {
+    const f3 c = mk3(na.x, na.y, na.z);
+    const f3 s = mk3(na.w, nb.x, nb.y);
+    const f3 o = q.ray.o + -1.f * c;
+    const f3 nlo = -1.f * s - o, nhi = s - o;
+    const float ax = nlo.x * q.inv.x, bx = nhi.x * q.inv.x;
+    const float ay = nlo.y * q.inv.y, by = nhi.y * q.inv.y;
+    const float az = nlo.z * q.inv.z, bz = nhi.z * q.inv.z;
+    const float t1 = smax(smax(smin(ax, bx), smin(ay, by)), smin(az, bz));
+    const float t2 = smin(smin(smax(ax, bx), smax(ay, by)), smax(az, bz));
+    const float m = q.dl + (fabsf(t1) + fabsf(t2)) * 0x1p-18f;
+    const bool robust = !q.par && t1 + m <= t2 - m && t2 - m >= 0.f;
+    return robust ? t1 + m : INFINITY;
 }
 
 // Hitting-leaf check before any root-path replay.  Every bound the replay
@@ -442,10 +481,10 @@ PT_HD void q_addr(const SceneView& S, const Query& q, uint32_t off[8]) {
             return;
         }
         if (q.li == 0u) {
-            // the leaf's bundle (first primitive + primitive range): 4 pieces
+            // the leaf's bundle (first primitive + primitive range + leaf box): 6 pieces
             b0 = S.o_bundle + PT_BUNDLE_BYTES * (q.node & 0x7fffffffu);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) off[k] = b0 + 16u * (uint32_t)(k < 4 ? k : 3);
+            for (int k = 0; k < 8; ++k) off[k] = b0 + 16u * (uint32_t)(k < 6 ? k : 5);
             return;
         }
         if (q.li & 0x80000000u) {
@@ -507,7 +546,7 @@ PT_HD void q_aux_next(Query& q, Mem& stk, uint32_t next) {
 #define QP_ARG
 #endif
 template <class Mem>
-PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r[8] QP_ARG) {
+PT_HD void q_exec_kind(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r[8] QP_ARG) {
     if (q.phase == Q_AUX && !(q.node & PT_LEAFQ)) {
         QP_STAMP(0);
         // one wide node: PT_AUXW child entries
@@ -598,6 +637,7 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
             q.lcnt = f2u(r[3].z);
             q.lt = PT_INF;
             q.lid = -1;
+            q.lacc = q_leaf_accept_t(q, r[4], r[5]);
 #ifdef PT_QDIAG
             C.cands++;
 #endif
@@ -661,7 +701,7 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
         q.li = li + 1u;
         if (q.li < q.lcnt) return;
         q.li = 0u;
-        if (q.lid >= 0 && !q_add_hit(q, q.cand, q.lt, q.lid)) {
+        if (q.lid >= 0 && !q_add_hit(q, q.cand, q.lt, q.lid, q.lacc)) {
             q.phase = Q_EXACT;
             return;
         }
@@ -756,6 +796,17 @@ PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r
     q.pos += 4u;
     if (q.pos >= q.len) q_entered(q);   // the leaf (last entry) was entered too
     else q.walk = R_WALK_E;
+}
+
+// one step's compute: the step kind's transition, then the precomputed accepts
+template <class Mem>
+PT_HD void q_exec(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r[8] QP_ARG) {
+#ifdef PT_QPROF_DEV
+    q_exec_kind(S, q, C, stk, r, qp);
+#else
+    q_exec_kind(S, q, C, stk, r);
+#endif
+    if (q.phase == Q_DECIDE) q_decide(q);
 }
 
 PT_HD F4 blob_piece(const SceneView& S, uint32_t off) {

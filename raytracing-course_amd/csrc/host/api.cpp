@@ -179,6 +179,7 @@ struct pt_scene {
     uint32_t auxw_stack = 0;    // per-lane stack words of the wide aux traversal
     uint32_t aux_rshift = 0;    // leaf-range packing of the wide aux entries (annotate_aux_ranges)
     std::vector<float> regions;   // per reference node: its leaf's hit region {lo, hi} (lo > hi: unbounded)
+    uint32_t aux_coarse_leaves = 0;   // leaf entries whose binary16 own box is > 4x wider than the f32 one
     float thr[256];
     std::map<int, DevScene> dev;
     std::mutex mu;
@@ -418,6 +419,10 @@ void encode_aux_entries(pt_scene* s, std::vector<pt::AuxSL>& aux) {
         }
         nodeB[n] = u;
     }
+    // binary16 keeps parity (outward rounding) but not culling: past |x| = 65504 a bound
+    // becomes infinite, and its step is 2 or more above 2048 -- leaf boxes much smaller
+    // than that step are then visited by far more rays (counted, warned about once)
+    size_t coarse = 0, leaves = 0;
     for (size_t i = 0; i < aux.size(); ++i) {
         pt::AuxSL& e = aux[i];
         if (pt::f2u(e.b.w) == 0xFFFFFFFFu) continue;
@@ -428,12 +433,27 @@ void encode_aux_entries(pt_scene* s, std::vector<pt::AuxSL>& aux) {
             h[j] = f16_out(A[j], j >= 3);
             h[6 + j] = f16_out(B[j], j >= 3);
         }
+        if (pt::f2u(e.b.w) & 0x80000000u) {
+            ++leaves;
+            bool c = false;
+            for (int j = 0; j < 3; ++j) {
+                const float w32 = A[3 + j] - A[j];
+                const float w16 = (float)__builtin_bit_cast(_Float16, (uint16_t)h[3 + j]) -
+                                  (float)__builtin_bit_cast(_Float16, (uint16_t)h[j]);
+                c = c || !(w16 <= 4.f * w32 + 1e-3f);
+            }
+            coarse += c ? 1u : 0u;
+        }
         const uint32_t range = pt::f2u(e.b.z), code = pt::f2u(e.b.w);
         // {lo.x, lo.y}, {lo.z, hi.x}, {hi.y, hi.z} per box
         e.a = pt::F4{pt::u2f(h[0] | h[1] << 16), pt::u2f(h[2] | h[3] << 16), pt::u2f(h[4] | h[5] << 16),
                      pt::u2f(h[6] | h[7] << 16)};
         e.b = pt::F4{pt::u2f(h[8] | h[9] << 16), pt::u2f(h[10] | h[11] << 16), pt::u2f(range), pt::u2f(code)};
     }
+    s->aux_coarse_leaves = (uint32_t)coarse;
+    if (leaves && coarse * 100 > leaves)
+        fprintf(stderr, "pt: %zu of %zu leaf boxes are more than 4x wider in the binary16 aux BVH (coordinates "
+                        "beyond ~2048 or +-65504): results stay exact, traversal visits more nodes\n", coarse, leaves);
 }
 
 // one 16-B-aligned blob holding every array the wavefront query reads
@@ -502,16 +522,19 @@ void build_query_blob(pt_scene* s) {
     s->o_qprim = append(qp.data(), qp.size() * sizeof(pt::F4));
     // leaf bundles (pt_query.h): the compact record of the leaf's first primitive
     // (pieces 0-2), then {leaf node index, first primitive, primitive count, its n.z}
-    std::vector<pt::F4> bu(4 * leaves.size());
+    std::vector<pt::F4> bu(6 * leaves.size());
     for (size_t k = 0; k < leaves.size(); ++k) {
         const pt::Node& n = s->dnodes[leaves[k]];
-        pt::F4* r = &bu[4 * k];
+        pt::F4* r = &bu[6 * k];
         const uint32_t first = pt::f2u(n.b.z), cnt = pt::f2u(n.b.w);
         if (cnt) {
             if (first >= s->dprims.size()) throw std::runtime_error("leaf primitive out of range");
             r[0] = qp[4 * first]; r[1] = qp[4 * first + 1]; r[2] = qp[4 * first + 2];
         }
         r[3] = pt::F4{pt::u2f(leaves[k]), pt::u2f(first), pt::u2f(cnt), cnt ? qp[4 * first + 3].x : 0.f};
+        // the leaf's box exactly as its node record holds it (c, s)
+        r[4] = n.a;
+        r[5] = pt::F4{n.b.x, n.b.y, 0.f, 0.f};
     }
     s->o_bundle = append(bu.data(), bu.size() * sizeof(pt::F4));
     s->o_prim = append(s->dprims.data(), s->dprims.size() * sizeof(pt::Prim));
@@ -1394,7 +1417,8 @@ int pt_session_stats(pt_session* ss, pt_stats* st) {
     st->node_bytes = sizeof(pt::Node);
     st->prim_bytes = sizeof(pt::Prim);
     // algorithmic bytes per counted unit: wavefront query = 4-wide aux node (128 B),
-    // reference node record (32 B), compact primitive record (48 B)
+    // reference node record (32 B), primitive geometry (48 B: the 64-B compact record
+    // adds the precomputed triangle normal, a layout choice, not counted)
     st->aux_bytes = ss->wave ? PT_AUXW * sizeof(pt::AuxSL) : sizeof(pt::AuxNode);
     if (ss->wave) st->prim_bytes = 48;
     st->isect_ms = ss->isect_ms;

@@ -288,3 +288,38 @@ def test_many_hitting_leaves_match_oracle(tmp_path, engine, monkeypatch):
     assert np.array_equal(hits[hit].view(np.uint32), ohits[hit].view(np.uint32))
     if engine == "replay":
         assert ctr["fallbacks"] > 0          # some rays exceed the list: the exact DFS took them
+
+
+def _moved_scene(src, dst, k, d):
+    """`src` with every length (positions, vertices, box sizes, camera position)
+    multiplied by k, then every position moved by d along x: far from the origin the
+    binary16 step (2^(e-10)) dwarfs small leaf boxes, and past 65504 they are infinite."""
+    out = []
+    for line in open(src):
+        w = line.split()
+        if w and w[0] in ("POSITION", "TRIANGLE", "BOX", "ELLIPSOID", "CAMERA_POSITION"):
+            v = [float(x) * k for x in w[1:]]
+            if w[0] in ("POSITION", "CAMERA_POSITION"):
+                v[0] += d
+            line = " ".join([w[0]] + [repr(x) for x in v]) + "\n"
+        out.append(line)
+    with open(dst, "w") as f:
+        f.writelines(out)
+
+
+@pytest.mark.parametrize("k,d", [(1.0, 3.0e4), (1.0e5, 0.0)])
+def test_coarse_binary16_aux_boxes_warn_and_stay_exact(tmp_path, capfd, k, d):
+    """far-out coordinates make the binary16 aux boxes coarse (a step of 16
+    at 3e4, infinite past 65504).  pt_scene_prepare says so on stderr, and the replay
+    still returns the exact traversal's result bit for bit (only the culling degrades)."""
+    path = str(tmp_path / "dragon_moved.txt")
+    _moved_scene(U.scene_path("practice5_dragon_10k.txt"), path, k, d)
+    with pt.Scene.load(U.scene_path("practice5_dragon_10k.txt")) as s:
+        s.prepare()
+    assert "binary16" not in capfd.readouterr().err
+    with pt.Scene.load(path) as s:
+        s.prepare()
+        assert "binary16" in capfd.readouterr().err
+        got = {t: s.selftest_render_host(232, 200, 16, 16, spp=2, traversal=v) for t, v in TRAVERSALS.items()}
+    assert got["replay"].view(np.uint32).tolist() == got["exact"].view(np.uint32).tolist()
+    assert got["replay_div"].view(np.uint32).tolist() == got["exact"].view(np.uint32).tolist()
