@@ -1408,6 +1408,13 @@ k_wcoop(WaveParams P) {
         emit = __shfl(emit ? 1 : 0, (int)tbase, 64) != 0;
         QC_TICK(3);
         if (have && !emit) {
+#ifdef PT_CPROF
+            // when the chains end: a histogram over 2^20-cycle buckets of the wave's lifetime
+            if (tl == 0u && P.wg_prof) {
+                const uint64_t bk = (__builtin_amdgcn_s_memtime() - cp_start) >> 20;
+                atomicAdd(P.wg_prof + 16 + (bk < 47u ? bk : 47u), 1ull);
+            }
+#endif
             // the pixel has reached the pass target: its state back to HBM
             if (tl == 0u) {
                 PixelHot hot;

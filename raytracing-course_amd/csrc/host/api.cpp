@@ -1160,13 +1160,13 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 const bool cprof = tune_has("cprof");   // -DPT_CPROF builds: per-phase cycles on stderr
                 if (cprof) {
                     if (!ss->wg_prof) HIP_TRY(hipMalloc(&ss->wg_prof, 512ull * ss->path_grid));
-                    HIP_TRY(hipMemsetAsync(ss->wg_prof, 0, 64, ss->stream));
+                    HIP_TRY(hipMemsetAsync(ss->wg_prof, 0, 512, ss->stream));
                     wp.wg_prof = ss->wg_prof;
                 }
                 HIP_TRY(pt_launch_coop(wp, grid, team, big, ss->stream, i0, i1));
                 if (cprof) {
-                    unsigned long long cp[8];
-                    HIP_TRY(hipMemcpyAsync(cp, wp.wg_prof, 64, hipMemcpyDeviceToHost, ss->stream));
+                    unsigned long long cp[64];
+                    HIP_TRY(hipMemcpyAsync(cp, wp.wg_prof, 512, hipMemcpyDeviceToHost, ss->stream));
                     HIP_TRY(hipStreamSynchronize(ss->stream));
                     float ms = 0.f;
                     HIP_TRY(hipEventElapsedTime(&ms, i0, i1));
@@ -1175,6 +1175,10 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                             "cycle: expand %.0f cand %.0f decide %.0f shade %.0f nextray %.0f; wave lifetime %.0f\n",
                             team, chains, grid, ms, cp[5], cp[6], cp[0] / cyc, cp[1] / cyc, cp[2] / cyc, cp[3] / cyc,
                             cp[4] / cyc, (double)cp[7] / (grid * (double)QC_WAVES));
+                    // chains ending per 2^20-cycle bucket of their wave's lifetime
+                    fprintf(stderr, "coop chain ends per 2^20 cycles:");
+                    for (int i = 16; i < 64; ++i) fprintf(stderr, " %llu", cp[i]);
+                    fprintf(stderr, "\n");
                     wp.wg_prof = nullptr;
                 }
                 ss->rounds++;
