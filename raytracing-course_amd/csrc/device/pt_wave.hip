@@ -1471,12 +1471,19 @@ k_wcoop(WaveParams P) {
 #endif
 }
 
-// exact stack DFS for the handed-back rays; 64-lane workgroups, stack in LDS
+// The rays the path engine hands back (Q_EXACT: an aux stack deeper than the
+// engine's LDS stack, a hitting-leaf list full of entered hits, non-finite
+// components); 64-lane workgroups, one ray per lane, stack in LDS.  The replay
+// first, with a stack as deep as the wide aux tree needs (a ray that only
+// overflowed the engine's 16 words -- the common case -- costs its ~100 aux
+// steps, not a whole reference DFS of ~10^4 node visits, tens of ms on one lane),
+// then the exact stack DFS for what the replay cannot take (q_run).
 __global__ void __launch_bounds__(64) k_wexact(WaveParams P) {
     extern __shared__ uint32_t lds_stack[];
     uint32_t* out = P.ctl + PT_CTL_SET * (1u - P.parity);
     const uint32_t n = out[C_EXACT];
-    LdsMemN<64u> stk{lds_stack + threadIdx.x};
+    const uint32_t words = P.max_stack > P.aux_stack ? P.max_stack : P.aux_stack;
+    LdsMemN<64u> stk{lds_stack + threadIdx.x, words, words};   // (+ a trash word)
     QCounts C{0u, 0u, 0u, 0u};
     for (uint32_t k = blockIdx.x * 64u + threadIdx.x; k < n; k += gridDim.x * 64u) {
         const F4 o = P.ex.ro[k], d = P.ex.rd[k];
@@ -1484,7 +1491,8 @@ __global__ void __launch_bounds__(64) k_wexact(WaveParams P) {
         ray.o = mk3(o.x, o.y, o.z);
         ray.d = mk3(d.x, d.y, d.z);
         Hit h;
-        const int id = q_exact(P.S, ray, stk, h, C);
+        uint32_t used = 0u;
+        const int id = q_run(P.S, ray, stk, h, C, used);
         const uint32_t j = f2u(d.w);   // the ray's work index
         P.done.ro[j] = o;
         P.done.rd[j] = F4{d.x, d.y, d.z, 0.f};
@@ -1577,7 +1585,8 @@ hipError_t pt_launch_path_round(pt::WaveParams p, uint32_t path_grid, uint32_t s
     else
         hipLaunchKernelGGL(pt::k_wpath<false>, dim3(path_grid), dim3(PT_PATH_WG), 0, s, p);
     if (e1 && (e = hipEventRecord(e1, s)) != hipSuccess) return e;
-    const uint32_t exact_lds = 64u * 4u * (p.max_stack ? p.max_stack : 1u);
+    const uint32_t xw = p.max_stack > p.aux_stack ? p.max_stack : p.aux_stack;
+    const uint32_t exact_lds = 64u * 4u * ((xw ? xw : 1u) + 1u);
     hipLaunchKernelGGL(pt::k_wexact, dim3(64), dim3(64), exact_lds, s, p);
     hipLaunchKernelGGL(pt::k_wshade, dim3(shade_grid), dim3(256), 0, s, p);
     return hipGetLastError();

@@ -221,8 +221,9 @@ def test_suspended_queries_resume_bit_exact(pt, name, budget, engine, monkeypatc
 @pytest.mark.parametrize("name", ["dragon_64x64x16", "c3s4_win_944_520_16x16", "rabbid_48x48x4"])
 def test_aux_stack_overflow_takes_exact_dfs(pt, name, monkeypatch):
     """A path-engine query whose pending aux items outgrow its LDS stack (PT_TUNE
-    lstack=1 here; PT_LSTACK words by default) hands its ray to the exact DFS:
-    same bytes and ray count, and the hand-over is counted."""
+    lstack=1 here; PT_LSTACK words by default) hands its ray to k_wexact (the replay
+    again with a stack as deep as the aux tree needs, then the exact DFS if the
+    replay cannot take it): same bytes and ray count, and the hand-over is counted."""
     monkeypatch.setenv("PT_TUNE", "lstack=1,coop=0")
     m, img, rad = U.golden_image(name)
     with pt.Scene.load(U.golden_scene_path(name)) as s:

@@ -22,7 +22,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3")
     ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
-    ap.add_argument("--ranks", default="first", choices=["first", "last", "both", "all"])
+    ap.add_argument("--ranks", default="first",
+                    help="first | last | both | all | a comma list of ranks (in that order, repeats allowed)")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--spp-per-step", type=int, default=16)
     a = ap.parse_args()
@@ -32,7 +33,8 @@ def main():
     with pt.Scene.load(path) as s:
         s.prepare()
         for w in a.worlds:
-            ranks = {"first": [0], "last": [w - 1], "both": sorted({0, w - 1}), "all": list(range(w))}[a.ranks]
+            named = {"first": [0], "last": [w - 1], "both": sorted({0, w - 1}), "all": list(range(w))}
+            ranks = named[a.ranks] if a.ranks in named else [int(x) % w for x in a.ranks.split(",")]
             for r in ranks:
                 ss = pt.Session(s, device=0, rank=r, world=w)
                 spp = a.spp_per_step * w
@@ -47,12 +49,14 @@ def main():
                 st1 = ss.stats()
                 rays = st1["rays"] - st0["rays"]
                 rounds = st1["rounds"] - st0["rounds"]
-                rec = {"world": w, "rank": r, "tiles": ss.n_tiles, "spp_per_step": spp, "mray_s": rays / dt / 1e6,
+                rec = {"world": w, "rank": r, "session": len(out), "tiles": ss.n_tiles, "spp_per_step": spp, "mray_s": rays / dt / 1e6,
                        "ms_per_step": dt * 1e3 / a.steps, "rounds_per_step": rounds / a.steps,
                        "rays_per_round": rays / max(rounds, 1),
                        "isect_ms_per_round": (st1["isect_ms"] - st0["isect_ms"]) / max(rounds, 1),
                        "coop_ms_per_step": (st1["coop_ms"] - st0["coop_ms"]) / a.steps,
-                       "coop_ray_share": (st1["coop_rays"] - st0["coop_rays"]) / max(rays, 1)}
+                       "coop_ray_share": (st1["coop_rays"] - st0["coop_rays"]) / max(rays, 1),
+                       "fallbacks": st1["fallbacks"] - st0["fallbacks"],
+                       "kernel_ms_per_step": (st1["kernel_ms"] - st0["kernel_ms"]) / a.steps}
                 out.append(rec)
                 print(json.dumps(rec), flush=True)
                 ss.close()
