@@ -133,6 +133,13 @@ struct WaveParams {
 #ifndef PT_PATH_WAVES_PER_EU
 #define PT_PATH_WAVES_PER_EU 3u        // k_wpath occupancy (waves per SIMD) the compiler is held to
 #endif
+#ifndef PT_PROBE_EVERY
+#define PT_PROBE_EVERY 3u              // k_wpath: candidate probes every n-th trip (1: every trip; 2 / 4 / 8 measured
+                                       // within 1 % of 3, all +8-10 % over 1)
+#endif
+#ifndef PT_PROBE_MIN
+#define PT_PROBE_MIN 16u               // ... or whenever this many lanes wait for one
+#endif
 #ifndef PT_CMAX
 #define PT_CMAX 512u
 #endif

@@ -333,6 +333,9 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     bool exhausted = false;
     uint32_t wpost = 0u;              // trips since the round's work ran out
     uint32_t trip = 0u;
+#if PT_PROBE_EVERY > 1
+    uint32_t ptrip = 0u;              // trips (for the probe turn)
+#endif
     const uint32_t wq = qw;                 // this query wave's done ring
     uint32_t rr = 0u;                       // replay step kind served last
     uint32_t dq_res = 0u;                   // done-ring entries written and published
@@ -545,7 +548,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
         } else {
             // One replay step kind per trip besides the aux steps (the kinds' code paths
             // would otherwise all be issued every trip): round-robin over the kinds present.
-            const uint32_t kind = active && q.phase == Q_REPLAY ? 1u + q.walk : active && q.phase == Q_AUX ? 0u : 7u;
+            uint32_t kind = active && q.phase == Q_REPLAY ? 1u + q.walk : active && q.phase == Q_AUX ? 0u : 7u;
             uint32_t present = 0u;
 #pragma unroll
             for (uint32_t k = 1; k <= PT_RKINDS; ++k)
@@ -557,6 +560,15 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 if (pick == 0u && ((present >> c) & 1u)) pick = c;
             }
             if (pick) rr = pick;
+#if PT_PROBE_EVERY > 1
+            // candidate probes (the aux pass's leaf steps) run on every PT_PROBE_EVERY-th trip,
+            // or whenever PT_PROBE_MIN lanes wait for one: the probe code is issued for the
+            // whole wave, so a trip that carries it for a few lanes costs every lane
+            const bool want_probe = kind == 0u && (q.node & PT_LEAFQ) != 0u;
+            const bool probe_go = (++ptrip % PT_PROBE_EVERY) == 0u ||
+                                  (uint32_t)__popcll(__ballot(want_probe)) >= PT_PROBE_MIN;
+            if (want_probe && !probe_go) kind = 7u;
+#endif
 #ifdef PT_WPROF
             if (__ballot(kind == 0u) != 0ull) pf_auxtrips++;
             if (pick) pf_picktrips++;
