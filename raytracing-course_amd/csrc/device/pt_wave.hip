@@ -302,7 +302,8 @@ struct EmitPath {
 
 
 
-#define PT_PATH_REFILL_MIN 8u      // idle lanes before a query wave refills (any, once the round's work is out)
+#define PT_PATH_REFILL_MIN 8u      // idle lanes before a query wave refills (any, once the round's work is out;
+                                   // 4 / 16 measured -1 % / -1.5 % in round 3)
 #define PT_NOWORK 0xffffffffu
 #define PT_CAPPED 0xfffffffeu
 
