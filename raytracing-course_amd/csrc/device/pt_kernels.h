@@ -137,6 +137,10 @@ struct WaveParams {
 #define PT_PROBE_EVERY 3u              // k_wpath: candidate probes every n-th trip (1: every trip; 2 / 4 / 8 measured
                                        // within 1 % of 3, all +8-10 % over 1)
 #endif
+#ifndef PT_AUX2
+#define PT_AUX2 1u                     // k_wpath: extra aux-node steps per trip for the lanes whose next
+                                       // step is one (+4.5 % at rank-of-1; 167 VGPRs)
+#endif
 #ifndef PT_PROBE_MIN
 #define PT_PROBE_MIN 16u               // ... or whenever this many lanes wait for one
 #endif

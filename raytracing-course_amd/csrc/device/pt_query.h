@@ -545,82 +545,88 @@ PT_HD void q_aux_next(Query& q, Mem& stk, uint32_t next) {
 #define QP_STAMP(i) (void)0
 #define QP_ARG
 #endif
+// The aux-node step kind (one wide node: PT_AUXW child entries); ends in the next
+// aux item, the end of the pass (Q_DECIDE) or the exact DFS.
+template <class Mem>
+PT_HD void q_exec_aux(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r[8]) {
+    C.aux++;
+    const f3 oinv = mk3(q.ray.o.x * q.inv.x, q.ray.o.y * q.inv.y, q.ray.o.z * q.inv.z);
+    // all PT_AUXW slab tests first, branch-free (the robust form only when a lane
+    // of the wave needs it); then the bookkeeping per entry
+    // both boxes of each entry (own box, hit region: see PT_LEAF_MARGIN),
+    // branch-free; the robust own-box form only when a lane of the wave needs it
+    const float mt = PT_LEAF_MARGIN * q.dl;
+    const bool mwide = !(mt < INFINITY);
+    bool hit[PT_AUXW];
+#pragma unroll
+    for (int k = 0; k < PT_AUXW; ++k) {
+        const F4 ea = r[2 * k], eb = r[2 * k + 1];
+        float tn, tf, un, uf;
+        aux_slab16(f2u(ea.x), f2u(ea.y), f2u(ea.z), q.inv, oinv, tn, tf);
+        aux_slab16(f2u(ea.w), f2u(eb.x), f2u(eb.y), q.inv, oinv, un, uf);
+        hit[k] = tn <= tf && tf >= 0.f && (mwide || (un - mt <= uf + mt && uf + mt >= 0.f));
+    }
+    if (pt_any(q.par != 0u)) {
+#pragma unroll
+        for (int k = 0; k < PT_AUXW; ++k) {
+            const F4 ea = r[2 * k];
+            if (q.par)
+                hit[k] = aux_box_par(h16(f2u(ea.x)), h16(f2u(ea.x) >> 16), h16(f2u(ea.y)), h16(f2u(ea.y) >> 16),
+                                     h16(f2u(ea.z)), h16(f2u(ea.z) >> 16), q.ray, q.inv, oinv);
+        }
+    }
+    uint32_t next = 0xffffffffu;
+    // the largest listed hitting leaf when the list is full (else none): a leaf
+    // above it could only join the list to drop out again
+    const uint32_t hmax = q.hidx[PT_QHK - 1];
+    // (bookkeeping in locals and selects: the packed fields are written once, and a
+    // stack push is one store whatever the entry -- no per-entry exec-mask branches)
+    uint32_t sp = q.sp;
+    bool ovf = false;
+#pragma unroll
+    for (int k = 0; k < PT_AUXW; ++k) {
+        // every entry's box is conservative: a reference leaf passing it is a
+        // candidate, probed next (its own slab test is decided only if one of
+        // its primitives is hit: a leaf failing it is never entered,
+        // src/bvh.cpp:188-198)
+        const uint32_t code = f2u(r[2 * k + 1].w);
+        const uint32_t rng = f2u(r[2 * k + 1].z);   // leaf: its ordinal; internal: its leaf range
+        const bool h = hit[k] && code != 0xffffffffu;
+        const bool isleaf = (code & 0x80000000u) != 0u;
+        const uint32_t lidx = code & 0x7fffffffu;
+        // a subtree is skipped when all its leaves lie below lb (decided in an
+        // earlier pass), or above the largest listed hitting leaf of a full
+        // list: it could only add hits the list would drop, so another pass follows
+        const bool above = isleaf ? lidx > hmax
+                                  : (hmax != 0xffffffffu && ((rng & 0xffffu) << S.aux_rshift) > hmax);
+        const bool fresh = isleaf ? lidx >= q.lb : ((rng >> 16) << S.aux_rshift) >= q.lb;
+        ovf = ovf || (h && fresh && above);
+        const bool take = h && fresh && !above;
+        const uint32_t item = isleaf ? (PT_LEAFQ | rng) : code;
+        const bool first = take && next == 0xffffffffu;
+        const bool push = take && !first;
+        next = first ? item : next;
+        stk.setc(sp, item, push && sp < stk.cap);
+        sp += push ? 1u : 0u;   // (past the stack's capacity: the exact DFS below)
+    }
+    if (ovf) q.overflow = 1u;
+    if (sp > stk.cap) {
+        q.phase = Q_EXACT;   // the pending items do not fit the stack: exact DFS (same result)
+        return;
+    }
+    q.sp = sp;
+#ifdef PT_QDIAG
+    if (next == 0xffffffffu && q.sp == 0u) C.passes++;
+    if (q.sp > C.steps) C.steps = q.sp;   // (diagnostics: the deepest aux stack of the query)
+#endif
+    q_aux_next(q, stk, next);
+}
+
 template <class Mem>
 PT_HD void q_exec_kind(const SceneView& S, Query& q, QCounts& C, Mem& stk, const F4 r[8] QP_ARG) {
     if (q.phase == Q_AUX && !(q.node & PT_LEAFQ)) {
         QP_STAMP(0);
-        // one wide node: PT_AUXW child entries
-        C.aux++;
-        const f3 oinv = mk3(q.ray.o.x * q.inv.x, q.ray.o.y * q.inv.y, q.ray.o.z * q.inv.z);
-        // all PT_AUXW slab tests first, branch-free (the robust form only when a lane
-        // of the wave needs it); then the bookkeeping per entry
-        // both boxes of each entry (own box, hit region: see PT_LEAF_MARGIN),
-        // branch-free; the robust own-box form only when a lane of the wave needs it
-        const float mt = PT_LEAF_MARGIN * q.dl;
-        const bool mwide = !(mt < INFINITY);
-        bool hit[PT_AUXW];
-#pragma unroll
-        for (int k = 0; k < PT_AUXW; ++k) {
-            const F4 ea = r[2 * k], eb = r[2 * k + 1];
-            float tn, tf, un, uf;
-            aux_slab16(f2u(ea.x), f2u(ea.y), f2u(ea.z), q.inv, oinv, tn, tf);
-            aux_slab16(f2u(ea.w), f2u(eb.x), f2u(eb.y), q.inv, oinv, un, uf);
-            hit[k] = tn <= tf && tf >= 0.f && (mwide || (un - mt <= uf + mt && uf + mt >= 0.f));
-        }
-        if (pt_any(q.par != 0u)) {
-#pragma unroll
-            for (int k = 0; k < PT_AUXW; ++k) {
-                const F4 ea = r[2 * k];
-                if (q.par)
-                    hit[k] = aux_box_par(h16(f2u(ea.x)), h16(f2u(ea.x) >> 16), h16(f2u(ea.y)), h16(f2u(ea.y) >> 16),
-                                         h16(f2u(ea.z)), h16(f2u(ea.z) >> 16), q.ray, q.inv, oinv);
-            }
-        }
-        uint32_t next = 0xffffffffu;
-        // the largest listed hitting leaf when the list is full (else none): a leaf
-        // above it could only join the list to drop out again
-        const uint32_t hmax = q.hidx[PT_QHK - 1];
-        // (bookkeeping in locals and selects: the packed fields are written once, and a
-        // stack push is one store whatever the entry -- no per-entry exec-mask branches)
-        uint32_t sp = q.sp;
-        bool ovf = false;
-#pragma unroll
-        for (int k = 0; k < PT_AUXW; ++k) {
-            // every entry's box is conservative: a reference leaf passing it is a
-            // candidate, probed next (its own slab test is decided only if one of
-            // its primitives is hit: a leaf failing it is never entered,
-            // src/bvh.cpp:188-198)
-            const uint32_t code = f2u(r[2 * k + 1].w);
-            const uint32_t rng = f2u(r[2 * k + 1].z);   // leaf: its ordinal; internal: its leaf range
-            const bool h = hit[k] && code != 0xffffffffu;
-            const bool isleaf = (code & 0x80000000u) != 0u;
-            const uint32_t lidx = code & 0x7fffffffu;
-            // a subtree is skipped when all its leaves lie below lb (decided in an
-            // earlier pass), or above the largest listed hitting leaf of a full
-            // list: it could only add hits the list would drop, so another pass follows
-            const bool above = isleaf ? lidx > hmax
-                                      : (hmax != 0xffffffffu && ((rng & 0xffffu) << S.aux_rshift) > hmax);
-            const bool fresh = isleaf ? lidx >= q.lb : ((rng >> 16) << S.aux_rshift) >= q.lb;
-            ovf = ovf || (h && fresh && above);
-            const bool take = h && fresh && !above;
-            const uint32_t item = isleaf ? (PT_LEAFQ | rng) : code;
-            const bool first = take && next == 0xffffffffu;
-            const bool push = take && !first;
-            next = first ? item : next;
-            stk.setc(sp, item, push && sp < stk.cap);
-            sp += push ? 1u : 0u;   // (past the stack's capacity: the exact DFS below)
-        }
-        if (ovf) q.overflow = 1u;
-        if (sp > stk.cap) {
-            q.phase = Q_EXACT;   // the pending items do not fit the stack: exact DFS (same result)
-            return;
-        }
-        q.sp = sp;
-#ifdef PT_QDIAG
-        if (next == 0xffffffffu && q.sp == 0u) C.passes++;
-        if (q.sp > C.steps) C.steps = q.sp;   // (diagnostics: the deepest aux stack of the query)
-#endif
-        q_aux_next(q, stk, next);
+        q_exec_aux(S, q, C, stk, r);
         return;
     }
     if (q.phase == Q_AUX) {
@@ -831,6 +837,18 @@ PT_HD void q_step(const SceneView& S, Query& q, QCounts& C, Mem& stk) {
 #else
     q_exec(S, q, C, stk, r);
 #endif
+}
+
+// One aux-node step only (a lane whose next step is an aux node: phase Q_AUX, node
+// not a leaf); the decisions a pass end leaves are resolved as in q_exec.
+template <class Mem>
+PT_HD void q_aux_step(const SceneView& S, Query& q, QCounts& C, Mem& stk) {
+    const uint32_t b = S.o_aux + q.node * (uint32_t)(PT_AUXW * sizeof(AuxSL));
+    F4 r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r[k] = blob_piece(S, b + 16u * (uint32_t)k);
+    q_exec_aux(S, q, C, stk, r);
+    if (q.phase == Q_DECIDE) q_decide(q);
 }
 
 // exact stack DFS for the rays the replay leaves (planes again + bvh_exact:

@@ -627,6 +627,15 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
 #else
             if (kind == 0u || kind == pick) q_step(P.S, q, C, stk);
 #endif
+#if PT_AUX2
+            // PT_AUX2 more aux-node steps in the same trip for the lanes whose next step is one
+#pragma unroll 1
+            for (uint32_t x = 0; x < PT_AUX2; ++x) {
+                const bool a2 = active && q.phase == Q_AUX && !(q.node & PT_LEAFQ);
+                if (__ballot(a2) == 0ull) break;
+                if (a2) q_aux_step(P.S, q, C, stk);
+            }
+#endif
         }
 #ifdef PT_WPROF
         const uint64_t pf_s1 = __builtin_amdgcn_s_memtime();
