@@ -137,6 +137,67 @@ __device__ __forceinline__ bool shade_item(const WaveParams& P, const EM& em, ui
 }
 #undef PF_MARK
 
+#if PT_DEFER_ENDS
+// shade_item in two halves (the shade wave's deferred path ends): the vertex half
+// returns true with `ray` = the child ray, or false when the path ended (the miss,
+// or the vertex ends it) with the pixel record updated (RNG, vertex count) and
+// `miss` telling how; the end half -- the backward fold into the sum, the next
+// sample's camera ray -- runs later in a batch of ended paths (end_item).  The
+// pixel's operations and their order are shade_item's: a pixel has one chain, and
+// its next sample starts only from end_item.
+template <class EM>
+__device__ __forceinline__ bool vertex_item(const WaveParams& P, const EM& em, uint32_t slot, Ray& ray, uint32_t hid,
+                                            bool& miss) {
+    PixelHot hot = load_hot(P.st, slot);
+    uint32_t nv = hot.nv;
+    Rng R = hot.R;
+    bool live = false;
+    miss = hid == 0xffffffffu;
+    if (!miss) {
+        Hit h;
+        (void)prim_intersect(P.S.prims[hid], ray, h);
+        uint32_t idm;
+        float s1, s2;
+        const bool cont = shade_vertex_e(P.S, em, P.S.shade[hid], R, ray, h, (int)hid, idm, s1, s2);
+        HbmVStore vs = fold_store(P.st, slot);
+        vs.put(nv, idm, s1, s2);
+        ++nv;
+        live = cont && nv < P.depth;   // RayTrace(.., 0) = 0
+    }
+    hot.nv = nv;
+    hot.R = R;
+    store_hot(P.st, slot, hot);
+    return live;
+}
+// src/scene.cpp:198 sum += RayTrace(...), then the next sample's camera ray
+// (returns true with `ray` set) unless the pixel has reached the pass target
+__device__ __forceinline__ bool end_item(const WaveParams& P, uint32_t slot, bool miss, Ray& ray) {
+    PixelHot hot = load_hot(P.st, slot);
+    Rng R = hot.R;
+    f3 L = miss ? P.S.bg : mk3(0.f, 0.f, 0.f);
+    HbmVStore vs = fold_store(P.st, slot);
+    for (uint32_t k = hot.nv; k > 0u; --k) {
+        uint32_t idm;
+        float s1, s2;
+        vs.get(k - 1u, idm, s1, s2);
+        L = fold_vertex(P.S, L, idm, s1, s2);
+    }
+    uint32_t pix;
+    const f3 sum = load_sum_pix(P.st, slot, pix);
+    store_sum(P.st, slot, sum + L, pix);
+    hot.done += 1u;
+    hot.nv = 0u;
+    bool emit = false;
+    if (hot.done < P.target) {
+        ray = camera_sample(P.cam, R, pix % P.tm.W, pix / P.tm.W);
+        emit = true;
+    }
+    hot.R = R;
+    store_hot(P.st, slot, hot);
+    return emit;
+}
+#endif
+
 __global__ void __launch_bounds__(256) k_wcamera(WaveParams P) {
     // blocks append in about block order: the queue follows tile_order (Z-order of
     // the tiles, so the pixels resident together form compact image regions)
@@ -746,6 +807,11 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
     uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // shade_item phases
 #endif
     uint32_t prog = 0u;               // finished samples not yet added to P.progress
+#if PT_DEFER_ENDS
+    // ended paths waiting for their fold (this wave's own queue: slot | miss << 31)
+    uint32_t* endq = P.endq + (size_t)blockIdx.x * PT_CMAX;
+    uint32_t e_head = 0u, e_tail = 0u;
+#endif
     for (;;) {
         // published entries of the done rings (ring indices are compile-time: no scratch)
         uint32_t av[PT_NQ], total = 0u;
@@ -754,13 +820,34 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
             av[w] = __builtin_amdgcn_readfirstlane(lds_read(L.dq_tail[w])) - head[w];
             total += av[w];
         }
+        Ray ray;
+        uint32_t slot = 0u;
+        bool emit = false, sdone = false, have = false;
+#ifdef PT_WPROF
+        uint64_t c0 = __builtin_amdgcn_s_memtime(), c2 = c0;
+#endif
+#if PT_DEFER_ENDS
+        const uint32_t pend = e_tail - e_head;
+        if (pend >= PT_END_MIN || (total == 0u && pend > 0u)) {
+            // a batch of ended paths: folds, sums, the next samples' camera rays
+            const uint32_t n = pend < 64u ? pend : 64u;
+            have = lane < n;
+            if (have) {
+                const uint32_t v = endq[(e_head + lane) % PT_CMAX];
+                slot = v & 0x7fffffffu;
+                emit = end_item(P, slot, (v >> 31) != 0u, ray);
+                sdone = true;
+            }
+            e_head += n;
+        } else
+#endif
         if (total == 0u) {
             if (lds_read(L.qw_done) == PT_NQ) {
                 // every query wave has left (and published): one more look, then done
                 uint32_t left = 0u;
 #pragma unroll
                 for (uint32_t w = 0; w < PT_NQ; ++w) left += lds_read(L.dq_tail[w]) - head[w];
-                if (__builtin_amdgcn_readfirstlane(left) == 0u) break;
+                if (__builtin_amdgcn_readfirstlane(left) == 0u) break;   // (no ended path waits: see above)
                 continue;
             }
 #ifdef PT_WPROF
@@ -768,7 +855,7 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
 #endif
             __builtin_amdgcn_s_sleep(1);
             continue;
-        }
+        } else {
         // up to 64 of them: a fair share of each ring first (a full ring holds back its
         // producer's finished queries), then the rest in ring order
         uint32_t take[PT_NQ], n = 0u;
@@ -784,7 +871,7 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
             n += x;
         }
 #ifdef PT_WPROF
-        const uint64_t c0 = __builtin_amdgcn_s_memtime();
+        c0 = __builtin_amdgcn_s_memtime();
         pf_batches++;
         pf_items += n;
 #endif
@@ -798,7 +885,7 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
 #pragma unroll
         for (uint32_t w = 0; w < PT_NQ; ++w) head[w] += take[w];
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        const bool have = lane < n;
+        have = lane < n;
         F4 o = F4{0.f, 0.f, 0.f, 0.f}, d = o;
         if (have) {
             o = lds_get(&L.dq_ro[0][0], j);
@@ -809,9 +896,6 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
 #pragma unroll
         for (uint32_t w = 0; w < PT_NQ; ++w)
             if (lane == w) lds_write(L.dq_head[w], head[w]);
-        Ray ray;
-        uint32_t slot = 0u;
-        bool emit = false, sdone = false;
 #ifdef PT_WPROF
         const uint64_t c1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -823,12 +907,32 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
             slot = f2u(o.w);
             ray.o = mk3(o.x, o.y, o.z);
             ray.d = mk3(d.x, d.y, d.z);
+#if PT_DEFER_ENDS
+            bool miss;
+            emit = vertex_item(P, EmitPath{L, P.S}, slot, ray, f2u(d.w), miss);
+            const bool ended = !emit;
+#else
             emit = shade_item(P, EmitPath{L, P.S}, slot, ray, f2u(d.w), sdone PF_PASS);
+#endif
+#if PT_DEFER_ENDS
+            // (appended below, in lane order)
+            if (ended) slot |= miss ? 0x80000000u : 0u;
+#endif
         }
+#if PT_DEFER_ENDS
+        {
+            const bool ended = have && !emit;
+            const unsigned long long me = __ballot(ended);
+            if (ended) endq[(e_tail + lanes_below(me)) % PT_CMAX] = slot;
+            e_tail += (uint32_t)__popcll(me);
+            have = have && emit;   // (an ended path is not gone: its pixel waits for the fold)
+        }
+#endif
 #ifdef PT_WPROF
-        const uint64_t c2 = __builtin_amdgcn_s_memtime();
+        c2 = __builtin_amdgcn_s_memtime();
         pf_shc += c2 - c1;
 #endif
+        }
         // finished samples for the host's progress bar: a system-scope add per ~4 k
         prog += (uint32_t)__popcll(__ballot(sdone));
         if (P.progress && prog >= 4096u) {

@@ -206,6 +206,7 @@ struct pt_session {
     uint32_t* hid = nullptr;      // n_slots (done.id)
     uint32_t* pidbuf = nullptr;   // 2 * n_slots (fresh queues' plane prims)
     uint32_t* carry = nullptr;    // 2 * carry_cap * carry_words
+    uint32_t* endq = nullptr;     // path_grid * PT_CMAX: the shade waves' ended paths (PT_DEFER_ENDS)
     uint32_t carry_cap = 0, carry_words = 0;
     uint32_t* ctl = nullptr;      // 2 x PT_CTL_SET round counters
     uint32_t* ctl_host = nullptr; // pinned copy of one counter set
@@ -982,6 +983,8 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         ss->path_budget = (uint32_t)std::max(1, tune_int("budget", (int)ss->path_budget));
         const int wg_cu = std::max(1, (int)(PT_PATH_WAVES_PER_EU * 4u / (PT_NQ + 1u)));
         ss->path_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * (uint32_t)std::max(1, tune_int("wg_per_cu", wg_cu));
+        if (hipMalloc(&ss->endq, (size_t)ss->path_grid * PT_CMAX * 4) != hipSuccess)
+            return cleanup(fail(PT_E_OOM, "device allocation failed (ended-path queues)"));
         // a round whose chains are this few runs them to the end of the pass (a few
         // per query wave: rebalancing them costs more rounds than it saves)
         ss->path_runend = ss->path_grid * PT_NQ * 4u;
@@ -1087,6 +1090,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.fq[1] = pt::RayQ{ss->qbuf + 2 * n, ss->qbuf + 3 * n, reinterpret_cast<int*>(ss->pidbuf) + n, ss->qbuf + 9 * n};
     wp.done = pt::DoneQ{ss->qbuf + 4 * n, ss->qbuf + 5 * n, ss->hid};
     wp.ex = pt::RayQ{ss->qbuf + 6 * n, ss->qbuf + 7 * n, nullptr, nullptr};
+    wp.endq = ss->endq;
     wp.cq[0] = ss->carry;
     wp.cq[1] = ss->carry + (size_t)ss->carry_cap * ss->carry_words;
     wp.carry_cap = ss->carry_cap;
@@ -1453,7 +1457,7 @@ void pt_session_free(pt_session* ss) {
     (void)hipFree(ss->tile_order);
     (void)hipFree(ss->gtile_dev);
     (void)hipFree(ss->qbuf); (void)hipFree(ss->hid); (void)hipFree(ss->pidbuf);
-    (void)hipFree(ss->carry); (void)hipFree(ss->ctl);
+    (void)hipFree(ss->carry); (void)hipFree(ss->ctl); (void)hipFree(ss->endq);
     if (ss->ctl_host) (void)hipHostFree(ss->ctl_host);
     if (ss->prog_host) (void)hipHostFree(ss->prog_host);
     if (ss->stream) {
