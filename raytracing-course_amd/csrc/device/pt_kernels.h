@@ -120,6 +120,10 @@ struct WaveParams {
     const uint32_t* tile_order;   // k_wcamera: block b seeds local tile tile_order[b] (null: tile b)
     uint32_t sparse_steps;        // steps per loop trip of the end-of-pass (sparse) kernel
     uint32_t coop_reserve;        // k_wcoop: aux stack words kept free for a depth-first descent (3 (aux depth + 2))
+    // k_wpath's per-trip step mix (the host may change it per round, from the chains left)
+    uint32_t probe_every;         // candidate probes every n-th trip (>= 1) ...
+    uint32_t probe_min;           // ... or whenever this many lanes wait for one
+    uint32_t aux_extra;           // extra aux-node steps per trip for the lanes whose next step is one
 };
 
 // path engine geometry: PT_NQ query waves + 1 shade wave per workgroup; at most
@@ -134,14 +138,11 @@ struct WaveParams {
 #ifndef PT_PATH_WAVES_PER_EU
 #define PT_PATH_WAVES_PER_EU 3u        // k_wpath occupancy (waves per SIMD) the compiler is held to
 #endif
-#ifndef PT_PROBE_EVERY
-#define PT_PROBE_EVERY 3u              // k_wpath: candidate probes every n-th trip (1: every trip; 2 / 4 / 8 measured
+// k_wpath's default step mix (WaveParams probe_every / probe_min / aux_extra)
+#define PT_PROBE_EVERY 3u              // candidate probes every n-th trip (1: every trip; 2 / 4 / 8 measured
                                        // within 1 % of 3, all +8-10 % over 1)
-#endif
-#ifndef PT_AUX2
-#define PT_AUX2 1u                     // k_wpath: extra aux-node steps per trip for the lanes whose next
-                                       // step is one (+4.5 % at rank-of-1; 167 VGPRs)
-#endif
+#define PT_AUX2 1u                     // extra aux-node steps per trip for the lanes whose next step is one
+                                       // (+4.5 % at rank-of-1; 167 VGPRs)
 #ifndef PT_DEFER_ENDS
 #define PT_DEFER_ENDS 1                // k_wpath: the shade wave folds ended paths in batches of their own
 #endif
@@ -149,9 +150,7 @@ struct WaveParams {
 #define PT_END_MIN 64u                 // ... once this many wait (or nothing else is there to shade); 32 / 48
                                        // measured +3.7 % / +5.6 %, 64 +6.2 % over folding in every shade batch
 #endif
-#ifndef PT_PROBE_MIN
 #define PT_PROBE_MIN 16u               // ... or whenever this many lanes wait for one
-#endif
 #ifndef PT_CMAX
 #define PT_CMAX 512u
 #endif

@@ -395,9 +395,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     bool exhausted = false;
     uint32_t wpost = 0u;              // trips since the round's work ran out
     uint32_t trip = 0u;
-#if PT_PROBE_EVERY > 1
-    uint32_t ptrip = 0u;              // trips (for the probe turn)
-#endif
+    uint32_t ptrip = 0u;              // trips since the last probe turn
     const uint32_t wq = qw;                 // this query wave's done ring
     uint32_t rr = 0u;                       // replay step kind served last
     uint32_t dq_res = 0u;                   // done-ring entries written and published
@@ -622,15 +620,14 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 if (pick == 0u && ((present >> c) & 1u)) pick = c;
             }
             if (pick) rr = pick;
-#if PT_PROBE_EVERY > 1
-            // candidate probes (the aux pass's leaf steps) run on every PT_PROBE_EVERY-th trip,
-            // or whenever PT_PROBE_MIN lanes wait for one: the probe code is issued for the
+            // candidate probes (the aux pass's leaf steps) run on every probe_every-th trip,
+            // or whenever probe_min lanes wait for one: the probe code is issued for the
             // whole wave, so a trip that carries it for a few lanes costs every lane
             const bool want_probe = kind == 0u && (q.node & PT_LEAFQ) != 0u;
-            const bool probe_go = (++ptrip % PT_PROBE_EVERY) == 0u ||
-                                  (uint32_t)__popcll(__ballot(want_probe)) >= PT_PROBE_MIN;
+            const bool turn = ++ptrip >= P.probe_every;
+            const bool probe_go = turn || (uint32_t)__popcll(__ballot(want_probe)) >= P.probe_min;
+            if (turn) ptrip = 0u;
             if (want_probe && !probe_go) kind = 7u;
-#endif
 #ifdef PT_WPROF
             if (__ballot(kind == 0u) != 0ull) pf_auxtrips++;
             if (pick) pf_picktrips++;
@@ -688,15 +685,13 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
 #else
             if (kind == 0u || kind == pick) q_step(P.S, q, C, stk);
 #endif
-#if PT_AUX2
-            // PT_AUX2 more aux-node steps in the same trip for the lanes whose next step is one
+            // aux_extra more aux-node steps in the same trip for the lanes whose next step is one
 #pragma unroll 1
-            for (uint32_t x = 0; x < PT_AUX2; ++x) {
+            for (uint32_t x = 0; x < P.aux_extra; ++x) {
                 const bool a2 = active && q.phase == Q_AUX && !(q.node & PT_LEAFQ);
                 if (__ballot(a2) == 0ull) break;
                 if (a2) q_aux_step(P.S, q, C, stk);
             }
-#endif
         }
 #ifdef PT_WPROF
         const uint64_t pf_s1 = __builtin_amdgcn_s_memtime();

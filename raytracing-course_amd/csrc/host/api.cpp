@@ -80,6 +80,11 @@ const Rccl& rccl() {
 //                     per chain) to the end of the pass (0: never)
 //   round_batch=N     path rounds launched per chain count while the chains are far above
 //                     the hand-over (default 1)
+//   probe_every=N, probe_min=N, aux_extra=N
+//                     path engine step mix: candidate probes every N-th trip or with N lanes
+//                     waiting, extra aux-node steps per trip (defaults 3, 16, 1)
+//   lowq=N, lowq_probe_every=N, lowq_probe_min=N, lowq_aux_extra=N
+//                     the step mix of rounds that start with fewer than N chains (default: none)
 //   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
 //   cap=N             chains a workgroup may hold
 //   lstack=N          aux stack words a path-engine query may use (default and maximum PT_LSTACK;
@@ -200,6 +205,10 @@ struct pt_session {
     uint32_t path_grid = 0, path_budget = 1024, path_runend = 0, path_sparse = 0, sparse_steps = 8;
     uint32_t coop_max = 0, coop_grid = 0, coop_reserve = 0;   // cooperative engine (k_wcoop) at the end of a pass
     uint32_t round_batch = 1;     // rounds launched per count while the chains are far above the hand-over
+    // k_wpath's per-trip step mix: {probe_every, probe_min, aux_extra}, and the one of
+    // rounds that start with fewer than lowq chains (latency-bound: few chains per lane)
+    uint32_t mix[3] = {PT_PROBE_EVERY, PT_PROBE_MIN, PT_AUX2}, mix_low[3] = {PT_PROBE_EVERY, PT_PROBE_MIN, PT_AUX2};
+    uint32_t lowq = 0;
     uint32_t coop_team = 8;       // lanes per chain in the cooperative engine (pure-coop rate, teams of
                                   // 64 / 32 / 16 / 8: 283 / 392 / 572 / 815 Mray/s)
     pt::F4* qbuf = nullptr;       // 10 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd, fq0.ri, fq1.ri
@@ -1022,6 +1031,15 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // above the hand-over
         if (ss->coop_max && !tune_has("sparse")) ss->path_sparse = std::min(ss->path_sparse, ss->coop_max);
         ss->round_batch = (uint32_t)std::max(1, tune_int("round_batch", (int)ss->round_batch));
+        {
+            static const char* keys[3] = {"probe_every", "probe_min", "aux_extra"};
+            static const char* lkeys[3] = {"lowq_probe_every", "lowq_probe_min", "lowq_aux_extra"};
+            for (int i = 0; i < 3; ++i) {
+                ss->mix[i] = (uint32_t)std::max(i == 0 ? 1 : 0, tune_int(keys[i], (int)ss->mix[i]));
+                ss->mix_low[i] = (uint32_t)std::max(i == 0 ? 1 : 0, tune_int(lkeys[i], (int)ss->mix[i]));
+            }
+            ss->lowq = (uint32_t)std::max(0, tune_int("lowq", (int)ss->lowq));
+        }
         if (ss->n_tiles_local) {
             // seeding order of the pass: the local tiles sorted by the Z-order (Morton)
             // code of their tile coordinates
@@ -1218,6 +1236,12 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             HIP_TRY(hipEventCreate(&i1));
             ss->pending_isect.emplace_back(i0, i1);
             ss->isect_launches++;
+            {
+                const uint32_t* m = chains < ss->lowq ? ss->mix_low : ss->mix;
+                wp.probe_every = m[0];
+                wp.probe_min = m[1];
+                wp.aux_extra = m[2];
+            }
             HIP_TRY(pt_launch_path_round(wp, ss->path_grid, 64u, ss->stream, sparse, i0, i1));
             if (wp.wg_prof) {
                 uint32_t cnt[2][8];
