@@ -84,7 +84,9 @@ const Rccl& rccl() {
 //                     path engine step mix: candidate probes every N-th trip or with N lanes
 //                     waiting, extra aux-node steps per trip (defaults 3, 16, 1)
 //   lowq=N, lowq_probe_every=N, lowq_probe_min=N, lowq_aux_extra=N
-//                     the step mix of rounds that start with fewer than N chains (default: none)
+//                     the step mix of rounds that start with fewer than N chains (default
+//                     768 per CU; the mix of the other rounds)
+//   lowq_wg=N         ... and their path workgroups per CU (PT_CMAX chains each; default 2)
 //   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
 //   cap=N             chains a workgroup may hold
 //   lstack=N          aux stack words a path-engine query may use (default and maximum PT_LSTACK;
@@ -209,6 +211,7 @@ struct pt_session {
     // rounds that start with fewer than lowq chains (latency-bound: few chains per lane)
     uint32_t mix[3] = {PT_PROBE_EVERY, PT_PROBE_MIN, PT_AUX2}, mix_low[3] = {PT_PROBE_EVERY, PT_PROBE_MIN, PT_AUX2};
     uint32_t lowq = 0;
+    uint32_t low_grid = 0;        // path workgroups of those rounds
     uint32_t coop_team = 8;       // lanes per chain in the cooperative engine (pure-coop rate, teams of
                                   // 64 / 32 / 16 / 8: 283 / 392 / 572 / 815 Mray/s)
     pt::F4* qbuf = nullptr;       // 10 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd, fq0.ri, fq1.ri
@@ -1038,7 +1041,15 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
                 ss->mix[i] = (uint32_t)std::max(i == 0 ? 1 : 0, tune_int(keys[i], (int)ss->mix[i]));
                 ss->mix_low[i] = (uint32_t)std::max(i == 0 ? 1 : 0, tune_int(lkeys[i], (int)ss->mix[i]));
             }
-            ss->lowq = (uint32_t)std::max(0, tune_int("lowq", (int)ss->lowq));
+            // Rounds that start with fewer than 768 chains per CU run on 2 path workgroups
+            // per CU (PT_CMAX chains each) instead of 4: with that few chains the rounds are
+            // bound by each chain's latency, and a query trip's instruction stream shares its
+            // SIMD with fewer waves.  Rank-of-1 / 2 / 4 / 8 (rank 0, three interleaved
+            // repeats, profiles/r03_lowq): +2.3 / +2 / +4 / +3-10 %; 150 k / 250 k chains
+            // within 1 % at ranks of 1-4, and 300 k (every round of a rank of 8, the first
+            // included) -25 % at rank-of-8.
+            ss->lowq = (uint32_t)std::max(0, tune_int("lowq", (int)(cus * 768u)));
+            ss->low_grid = std::min(ss->path_grid, cus * (uint32_t)std::max(1, tune_int("lowq_wg", 2)));
         }
         if (ss->n_tiles_local) {
             // seeding order of the pass: the local tiles sorted by the Z-order (Morton)
@@ -1236,13 +1247,19 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             HIP_TRY(hipEventCreate(&i1));
             ss->pending_isect.emplace_back(i0, i1);
             ss->isect_launches++;
+            uint32_t grid = ss->path_grid;
             {
-                const uint32_t* m = chains < ss->lowq ? ss->mix_low : ss->mix;
+                const bool low = chains < ss->lowq;
+                const uint32_t* m = low ? ss->mix_low : ss->mix;
                 wp.probe_every = m[0];
                 wp.probe_min = m[1];
                 wp.aux_extra = m[2];
+                if (low && ss->low_grid) {
+                    grid = ss->low_grid;
+                    wp.path_cap = PT_CMAX;
+                }
             }
-            HIP_TRY(pt_launch_path_round(wp, ss->path_grid, 64u, ss->stream, sparse, i0, i1));
+            HIP_TRY(pt_launch_path_round(wp, grid, 64u, ss->stream, sparse, i0, i1));
             if (wp.wg_prof) {
                 uint32_t cnt[2][8];
                 HIP_TRY(hipMemcpyAsync(cnt[0], ss->ctl + PT_CTL_SET * p, 32, hipMemcpyDeviceToHost, ss->stream));
