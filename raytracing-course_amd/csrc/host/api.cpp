@@ -87,6 +87,7 @@ const Rccl& rccl() {
 //                     the step mix of rounds that start with fewer than N chains (default
 //                     768 per CU; the mix of the other rounds)
 //   lowq_wg=N         ... and their path workgroups per CU (PT_CMAX chains each; default 2)
+//   lowq2=N, lowq2_wg=N  a second tier below N chains (default: none)
 //   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
 //   cap=N             chains a workgroup may hold
 //   lstack=N          aux stack words a path-engine query may use (default and maximum PT_LSTACK;
@@ -212,6 +213,7 @@ struct pt_session {
     uint32_t mix[3] = {PT_PROBE_EVERY, PT_PROBE_MIN, PT_AUX2}, mix_low[3] = {PT_PROBE_EVERY, PT_PROBE_MIN, PT_AUX2};
     uint32_t lowq = 0;
     uint32_t low_grid = 0;        // path workgroups of those rounds
+    uint32_t lowq2 = 0, low_grid2 = 0;   // (tuning) a second tier: rounds under lowq2 chains on low_grid2
     uint32_t coop_team = 8;       // lanes per chain in the cooperative engine (pure-coop rate, teams of
                                   // 64 / 32 / 16 / 8: 283 / 392 / 572 / 815 Mray/s)
     pt::F4* qbuf = nullptr;       // 10 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd, fq0.ri, fq1.ri
@@ -1050,6 +1052,8 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
             // included) -25 % at rank-of-8.
             ss->lowq = (uint32_t)std::max(0, tune_int("lowq", (int)(cus * 768u)));
             ss->low_grid = std::min(ss->path_grid, cus * (uint32_t)std::max(1, tune_int("lowq_wg", 2)));
+            ss->lowq2 = (uint32_t)std::max(0, tune_int("lowq2", 0));
+            ss->low_grid2 = std::min(ss->path_grid, cus * (uint32_t)std::max(1, tune_int("lowq2_wg", 1)));
         }
         if (ss->n_tiles_local) {
             // seeding order of the pass: the local tiles sorted by the Z-order (Morton)
@@ -1255,7 +1259,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 wp.probe_min = m[1];
                 wp.aux_extra = m[2];
                 if (low && ss->low_grid) {
-                    grid = ss->low_grid;
+                    grid = chains < ss->lowq2 ? ss->low_grid2 : ss->low_grid;
                     wp.path_cap = PT_CMAX;
                 }
             }
