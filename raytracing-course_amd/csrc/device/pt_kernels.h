@@ -124,6 +124,7 @@ struct WaveParams {
     uint32_t probe_every;         // candidate probes every n-th trip (>= 1) ...
     uint32_t probe_min;           // ... or whenever this many lanes wait for one
     uint32_t aux_extra;           // extra aux-node steps per trip for the lanes whose next step is one
+    uint32_t batch;               // k_wpath: round-queue entries a wave takes per pull (at most)
 };
 
 // path engine geometry: PT_NQ query waves + 1 shade wave per workgroup; at most

@@ -273,9 +273,6 @@ __global__ void __launch_bounds__(256) k_wcamera_merge(WaveParams P) {
 }
 
 #define PT_SUSPENDED 0xfffffffeu   // done.id of a query suspended to the next round
-#ifndef PT_BATCH
-#define PT_BATCH 64u        // queue indices a wave takes per atomic
-#endif
 
 // ---- path engine -------------------------------------------------------------
 // k_wpath: persistent and warp-specialised.  A workgroup is PT_NQ query waves
@@ -385,7 +382,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     // suspending gains nothing and costs a round: run them to the end.
     const uint32_t budget = n_total <= P.path_runend ? 0xffffffffu : P.path_budget;
     uint32_t bsz = n_total / n_waves;
-    bsz = bsz < 1u ? 1u : (bsz > PT_BATCH ? PT_BATCH : bsz);
+    bsz = bsz < 1u ? 1u : (bsz > P.batch ? P.batch : bsz);   // queue indices a wave takes per atomic
     const RayQ FQ = P.fq[p];
     const uint32_t* CQ = P.cq[p];
     uint32_t* CQout = P.cq[1u - p];

@@ -90,6 +90,7 @@ const Rccl& rccl() {
 //   lowq2=N, lowq2_wg=N  a second tier below N chains (default: none)
 //   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
 //   cap=N             chains a workgroup may hold
+//   batch=N           round-queue entries a query wave takes per pull (1..64, default 32)
 //   lstack=N          aux stack words a path-engine query may use (default and maximum PT_LSTACK;
 //                     a query needing more takes the exact DFS)
 //   rowmajor=1        seed a pass in row-major tile order instead of Z-order
@@ -1154,6 +1155,10 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.coop_reserve = ss->coop_reserve;
     // aux stack words per query lane (PT_TUNE lstack=N < PT_LSTACK: tests of the exact-DFS
     // hand-over of queries that outgrow it)
+    // round-queue entries a query wave takes per pull: 32 (64 before round 3's low-chain
+    // rounds): a workgroup fills closer to its chain cap in finer pulls; rank-of-1 / 2 / 4 / 8,
+    // two calls: +0.5 / +0.5 / +3.5 / +3 % (8 and 16 the same at ranks of 1-4; profiles/r03_lowq)
+    wp.batch = (uint32_t)std::min(64, std::max(1, tune_int("batch", 32)));
     wp.lstack = std::min<uint32_t>(PT_LSTACK, (uint32_t)std::max(1, tune_int("lstack", (int)PT_LSTACK)));
     if (ss->on_progress && !ss->prog_host) {
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ss->prog_host), 8, hipHostMallocMapped | hipHostMallocCoherent));

@@ -485,3 +485,71 @@ def test_deep_engines_beyond_coop_tables(pt, name, engine, monkeypatch):
     assert st["rays"] == m["rays"]
     if coop:
         assert st["coop_launches"] >= 1
+
+
+# A closed mirror box: every path runs until RAY_DEPTH cuts it, so a pixel's vertex
+# count passes 255 (the packed vertex-count field is 24 bits wide).
+MIRROR_BOX = """DIMENSIONS 8 8
+RAY_DEPTH %d
+SAMPLES 2
+
+BG_COLOR 0.1 0.2 0.3
+
+CAMERA_POSITION 0 0 0
+CAMERA_RIGHT 1 0 0
+CAMERA_UP 0 1 0
+CAMERA_FORWARD 0 0 -1
+CAMERA_FOV_X 1.2
+""" + "".join("""
+NEW_PRIMITIVE
+PLANE %s
+POSITION %s
+COLOR 0.99 0.98 0.97
+METALLIC
+""" % (n, p) for n, p in [("0 1 0", "0 -3 0"), ("0 -1 0", "0 3 0"), ("1 0 0", "-3 0 0"), ("-1 0 0", "3 0 0"),
+                          ("0 0 1", "0 0 -3"), ("0 0 -1", "0 0 3")]) + """
+NEW_PRIMITIVE
+ELLIPSOID 0.15 0.15 0.15
+POSITION 1 1 -2
+COLOR 0 0 0
+EMISSION 40 40 40
+
+NEW_PRIMITIVE
+ELLIPSOID 0.6 0.4 0.5
+POSITION -1 -1 -2
+COLOR 0.9 0.9 0.9
+DIELECTRIC
+IOR 1.5
+
+NEW_PRIMITIVE
+TRIANGLE 0 0 0 1 0 0 0 1 0
+POSITION -0.5 0.5 -2.5
+ROTATION 0 0.3826834 0 0.9238795
+COLOR 0.8 0.6 0.4
+METALLIC
+
+NEW_PRIMITIVE
+BOX 0.3 0.2 0.4
+POSITION 0.8 -1.2 -1.5
+COLOR 0.5 0.5 1.0
+METALLIC
+"""
+
+
+@pytest.mark.parametrize("engine", ["default", "path", "coop8"])
+def test_depth_beyond_255_mirror_box(pt, tmp_path, engine, monkeypatch):
+    """RAY_DEPTH 300 in a closed mirror box (paths of up to 300 vertices): the image, the
+    radiance bits and the ray count equal the oracle's, in each engine."""
+    if engine != "default":
+        monkeypatch.setenv("PT_TUNE", "coop=%s,coop_team=8" % ("100000000" if engine == "coop8" else "0"))
+    path = str(tmp_path / "mirror_box_d300.txt")
+    with open(path, "w") as f:
+        f.write(MIRROR_BOX % 300)
+    orgb, orad, octr = U.OracleScene(path).render()
+    assert octr["rays"] > 64 * 2 * 256   # most paths are longer than 255 vertices
+    with pt.Scene.load(path) as s:
+        rgb, rad, st = s.render(radiance=True)
+    assert st["errors"] == 0
+    assert rad.view(np.uint32).tolist() == orad.view(np.uint32).tolist()
+    assert np.array_equal(rgb, orgb)
+    assert st["rays"] == octr["rays"]
