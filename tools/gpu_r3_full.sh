@@ -10,5 +10,5 @@ bash tools/gpu_profile.sh || { echo PROFILE_FAIL; exit 1; }
 timeout -k 10 600 python3 tools/rank_sim.py --worlds 2 4 8 --ranks all --steps ${STEPS:-4} > $O/ranksim_all.jsonl 2> $O/ranksim_all.err || { echo SIM_FAIL; tail -20 $O/ranksim_all.err; exit 1; }
 grep -E 'min_mray' $O/ranksim_all.jsonl
 for k in 1 2; do
-  PT_TUNE=roundlog=$k timeout -k 10 120 python3 tools/rank_sim.py --worlds 8 --steps 4 > $O/roundlog$k_w8.jsonl 2> $O/roundlog${k}_w8.txt || { echo RL_FAIL; exit 1; }
+  PT_TUNE=roundlog=$k timeout -k 10 120 python3 tools/rank_sim.py --worlds 8 --steps 4 > $O/roundlog${k}_w8.jsonl 2> $O/roundlog${k}_w8.txt || { echo RL_FAIL; exit 1; }
 done
