@@ -274,7 +274,7 @@ def wall_to_ppm(config, ngpu):
     one process drives ngpu GPUs (PT_NGPU) and gathers with RCCL."""
     src = scene_file(config)
     out = os.path.join("/tmp", "pt_bench_%s_%d.ppm" % (config, os.getpid()))
-    env = dict(os.environ, PT_STATS="1", PT_QUIET="1", PT_NGPU=str(ngpu))
+    env = dict(os.environ, PT_STATS="2", PT_QUIET="1", PT_NGPU=str(ngpu))
     if ngpu > 1:
         env["PT_GATHER"] = "rccl"
     t0 = time.perf_counter()
@@ -286,12 +286,25 @@ def wall_to_ppm(config, ngpu):
         raise RuntimeError(r.stderr.strip()[-300:])
     md5 = hashlib.md5(open(out, "rb").read()).hexdigest()
     os.unlink(out)
-    m = dict(re.findall(r"(\w+(?:/\w+)?)=([\d.]+)", r.stderr))
+    stats = [ln for ln in r.stderr.splitlines() if ln.startswith("rays=")]
+    m = dict(re.findall(r"(\w+(?:/\w+)?)=([\d.]+)", stats[-1] if stats else r.stderr))
     rays = int(m["rays"])
+    # PT_STATS=2: the CLI's phases and pt_render's per-rank set-up / render / resolve and the gather
+    phases = {}
+    for ln in r.stderr.splitlines():
+        if ln.startswith("phases_ms:"):
+            phases["cli_ms"] = {k: float(v) for k, v in re.findall(r"(\w+)=([\d.]+)", ln)}
+        elif ln.startswith("pt_render rank"):
+            phases.setdefault("ranks", []).append({k: float(v) for k, v in re.findall(r"(\w+)=([\d.]+)", ln)})
+        elif ln.startswith("pt_render gather_ms"):
+            phases["gather_ms"] = float(re.search(r"gather_ms=([\d.]+)", ln).group(1))
     return {"config": config, "ngpu": ngpu, "seconds": dt, "rays": rays, "mray_s": rays / dt / 1e6,
-            "render_ms": float(m["wall_ms"]), "gather_rccl": int(m.get("gather_rccl", 0)), "ppm_md5": md5,
+            "render_ms": float(m["wall_ms"]), "kernel_ms": float(m["kernel_ms"]),
+            "render_mray_s": rays / float(m["kernel_ms"]) / 1e3 if float(m["kernel_ms"]) > 0 else None,
+            "gather_rccl": int(m.get("gather_rccl", 0)), "ppm_md5": md5, "phases": phases,
             "what": "PT_NGPU=%d run.sh <scene> <out.ppm>: one process, process start to PPM closed "
-                    "(all spp of the config)" % ngpu}
+                    "(all spp of the config); render_ms = pt_render's wall (session set-up, the pass, "
+                    "tonemap, gather), kernel_ms = the pass's kernels (HIP events, slowest GPU)" % ngpu}
 
 
 # -------------------------------------------------------------- roofline --
@@ -546,6 +559,9 @@ def main():
             ngpu = world if not args.same_device else 1
             try:
                 res["wall_to_ppm"] = wall_to_ppm(args.config, ngpu)
+                # the metric's own pass: the whole config (256 spp for c3) as ONE pass, rays over its
+                # kernel time -- beside `value`, whose 16-spp steps coalesce into a pass of steps x 16
+                res["render_256spp_mray_s"] = res["wall_to_ppm"]["render_mray_s"]
             except Exception as e:
                 log("wall-clock run failed:", e)
                 res["wall_to_ppm"] = None

@@ -26,7 +26,11 @@ extern "C" {
 #endif
 
 #define PT_ABI_VERSION 4   /* 2: pt_render_opts.gather; 3: pt_stats per-engine (coop_*) fields;
-                              4: pt_gather_init */
+                              4: pt_gather_init, and the session tile deal changed from tile
+                              t -> rank t % world to tile (tx, ty) -> rank (tx + ty) % world
+                              (local tiles still in ascending tile order): a driver that
+                              un-interleaves packed tiles itself must use pt_unpack_tiles
+                              (or ptrace.rank_tiles), not its own formula */
 
 enum {
     PT_OK = 0,

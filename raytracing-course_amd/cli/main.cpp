@@ -40,7 +40,10 @@ int main(int argc, char** argv) {
     // BVH built, and with several GPUs the RCCL communicator of the framebuffer
     // gather is created there too (errors surface again, from pt_render)
     std::thread warm([&] {
-        for (int g = 0; g < ngpu; ++g) (void)pt_device_init(dev0 + g);
+        // one thread per device: each device's runtime context and code objects at once
+        std::vector<std::thread> di;
+        for (int g = 0; g < ngpu; ++g) di.emplace_back([g, dev0] { (void)pt_device_init(dev0 + g); });
+        for (auto& t : di) t.join();
         t_warm = ms();
         if (ngpu > 1 && !host_gather) (void)pt_gather_init(dev0, ngpu);
         t_comm = ms();

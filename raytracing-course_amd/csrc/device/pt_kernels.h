@@ -90,8 +90,10 @@ enum : uint32_t { C_FRESH = 0u, C_CARRY = 1u, C_DONE = 3u, C_EXACT = 4u, C_FRONT
 
 struct WaveParams {
     SceneView S;
-    const AuxSL* aux;
-    uint32_t n_aux;
+    const AuxSL* top;             // k_wcamera: the wide aux root's entries, then its inner entries' child
+                                  // nodes' (entry k's child at top[PT_AUXW (1 + k)]; host form, f32)
+    uint32_t n_top;               // entries in top
+    uint32_t n_aux;               // wide aux entries in the blob
     CamView cam;
     TileMap tm;
     PixelState st;                // per-slot records (RNG, vertices, samples done, sum) + fold records
@@ -156,7 +158,7 @@ struct WaveParams {
 #define PT_CMAX 512u
 #endif
 // The rings and the query lanes' aux stacks live in LDS (4 workgroups per CU:
-// 38.9 KB each of the CU's 160 KB):
+// 40,768 B each of the CU's 163,840 B; pt_wave.hip static_asserts the fit):
 //   ray ring   PT_CMAX entries (52 B: ray, slot, plane t and prim, q_prep record)
 //   done rings PT_DQN entries per query wave (32 B: ray, slot, closest prim),
 //              flow-controlled (a finished query waits in its lane while its ring is full)

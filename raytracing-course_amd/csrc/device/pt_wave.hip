@@ -237,8 +237,8 @@ __global__ void __launch_bounds__(256) k_wcamera(WaveParams P) {
         // reference root box (root entries +2.6 % over it, two levels +2.5 % more)
         const f3 rinv = mk3(1.f / ray.d.x, 1.f / ray.d.y, 1.f / ray.d.z);
         const f3 oinv = mk3(ray.o.x * rinv.x, ray.o.y * rinv.y, ray.o.z * rinv.z);
-        for (uint32_t k = 0; k < PT_AUXW && k < P.n_aux; ++k) {
-            const AuxSL e = P.aux[k];
+        for (uint32_t k = 0; k < PT_AUXW && k < P.n_top; ++k) {
+            const AuxSL e = P.top[k];
             const uint32_t code = f2u(e.b.w);
             if (code == 0xffffffffu || !aux_box(e.a.x, e.a.y, e.a.z, e.a.w, e.b.x, e.b.y, rinv, oinv)) continue;
             if (code & 0x80000000u) {
@@ -246,7 +246,7 @@ __global__ void __launch_bounds__(256) k_wcamera(WaveParams P) {
                 continue;
             }
             for (uint32_t j = 0; j < PT_AUXW; ++j) {   // one level down
-                const AuxSL c = P.aux[code * PT_AUXW + j];
+                const AuxSL c = P.top[code * PT_AUXW + j];   // (code = 1 + k in the host's top copy)
                 front = front || (f2u(c.b.w) != 0xffffffffu && aux_box(c.a.x, c.a.y, c.a.z, c.a.w, c.b.x, c.b.y, rinv, oinv));
             }
         }
@@ -328,6 +328,11 @@ struct PathLds {
     F4 em[QC_NEM * 5u];
     uint32_t pl_id[QC_NPL];
 };
+// k_wpath's occupancy (PT_PATH_WAVES_PER_EU waves per SIMD, 4 SIMDs per CU) assumes
+// that many workgroups fit the CU's 160 KB of LDS: a bigger ring, stack or table
+// would silently drop a workgroup per CU (every tuning number assumes 4)
+static_assert((PT_PATH_WAVES_PER_EU * 4u / (PT_NQ + 1u)) * sizeof(PathLds) <= 160u * 1024u,
+              "PathLds no longer fits PT_PATH_WAVES_PER_EU*4/(PT_NQ+1) workgroups per CU");
 // the first QC_NPL planes / QC_NEM emitters from the workgroup's LDS copy, any further ones from HBM
 struct PlanesPath {
     const PathLds& L;
@@ -1603,6 +1608,7 @@ __global__ void __launch_bounds__(64) k_wexact(WaveParams P) {
     const uint32_t words = P.max_stack > P.aux_stack ? P.max_stack : P.aux_stack;
     LdsMemN<64u> stk{lds_stack + threadIdx.x, words, words};   // (+ a trash word)
     QCounts C{0u, 0u, 0u, 0u};
+    uint32_t err = 0u;
     for (uint32_t k = blockIdx.x * 64u + threadIdx.x; k < n; k += gridDim.x * 64u) {
         const F4 o = P.ex.ro[k], d = P.ex.rd[k];
         Ray ray;
@@ -1611,6 +1617,10 @@ __global__ void __launch_bounds__(64) k_wexact(WaveParams P) {
         Hit h;
         uint32_t used = 0u;
         const int id = q_run(P.S, ray, stk, h, C, used);
+        // q_run flags a recomputed hit that differs from the query's in the plane count's
+        // top bit (must never happen): an exactness error, not plane tests
+        err += C.planes >> 31;
+        C.planes = 0u;   // (the path engine counted this ray's plane tests when it took it)
         const uint32_t j = f2u(d.w);   // the ray's work index
         P.done.ro[j] = o;
         P.done.rd[j] = F4{d.x, d.y, d.z, 0.f};
@@ -1619,7 +1629,7 @@ __global__ void __launch_bounds__(64) k_wexact(WaveParams P) {
     unsigned long long* ctr = ctr_copy(P.counters);
     wave_add_u64(ctr + 1, C.nodes);
     wave_add_u64(ctr + 2, C.ptests);
-    wave_add_u64(ctr + 3, C.planes);
+    wave_add_u64(ctr + 4, err);
 }
 
 __global__ void __launch_bounds__(256) k_wshade(WaveParams P) {

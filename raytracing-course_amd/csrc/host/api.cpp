@@ -16,6 +16,8 @@
 #include <algorithm>
 #include <array>
 #include <chrono>
+#include <condition_variable>
+#include <memory>
 #include <functional>
 #include <fstream>
 #include <map>
@@ -87,14 +89,11 @@ const Rccl& rccl() {
 //                     the step mix of rounds that start with fewer than N chains (default
 //                     768 per CU; the mix of the other rounds)
 //   lowq_wg=N         ... and their path workgroups per CU (PT_CMAX chains each; default 2)
-//   lowq2=N, lowq2_wg=N  a second tier below N chains (default: none)
 //   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
 //   cap=N             chains a workgroup may hold
 //   batch=N           round-queue entries a query wave takes per pull (1..64, default 32)
 //   lstack=N          aux stack words a path-engine query may use (default and maximum PT_LSTACK;
 //                     a query needing more takes the exact DFS)
-//   rowmajor=1        seed a pass in row-major tile order instead of Z-order
-//   variant=V         megakernel variant bits (1 filtered tests, 2 XCD-banded tiles)
 //   roundlog=1|2      per-round kernel times / pixels' remaining samples on stderr
 //   wgprof=FILE       per-workgroup timelines (-DPT_WPROF builds)
 //   cprof=1           per-phase cycles of the cooperative engine on stderr (-DPT_CPROF builds)
@@ -106,6 +105,16 @@ std::string tune_str(const char* key) {
     static const bool warned = [] {
         for (const char* old : {"PT_ENGINE", "PT_PATH_BUDGET", "PT_STRAGGLER", "PT_QSTATS", "PT_WGPROF", "PT_COOP"})
             if (getenv(old)) fprintf(stderr, "libpt: %s is ignored; use PT_TUNE=\"key=value,...\" (INTEGRATION.md)\n", old);
+        // keys of earlier builds, measured without a gain and removed
+        if (const char* e = getenv("PT_TUNE"))
+            for (const char* old : {"coop_stop", "near_budget", "near_k", "lowq2", "lowq2_wg", "variant", "rowmajor"}) {
+                const std::string k = std::string(old) + "=";
+                for (const char* p = e; (p = strstr(p, k.c_str())) != nullptr; p += k.size())
+                    if (p == e || p[-1] == ',') {
+                        fprintf(stderr, "libpt: PT_TUNE key %s was removed and is ignored (INTEGRATION.md)\n", old);
+                        break;
+                    }
+            }
         return true;
     }();
     (void)warned;
@@ -151,18 +160,31 @@ hipError_t take_stream(int dev, hipStream_t* s) {
             return fail(PT_E_HIP, std::string(#expr " failed: ") + hipGetErrorString(e_));            \
     } while (0)
 
+// A scene's device copy: ONE allocation holding the query blob (which also holds
+// the reference nodes, primitives and ancestor lists the other kernels read:
+// the views below point into it), the shading records, the plane and emitter
+// lists, the gamma thresholds and k_wcamera's copy of the aux BVH's top two
+// levels -- uploaded with one copy from one host image.  The BVH2 aux (the
+// megakernel's traversal) is uploaded on first use only.
 struct DevScene {
-    pt::Node* nodes = nullptr;
-    pt::Prim* prims = nullptr;
-    pt::Shade* shade = nullptr;
-    uint32_t* planes = nullptr;
-    uint32_t* emitters = nullptr;
-    float* thr = nullptr;
-    pt::AuxNode* aux = nullptr;
-    pt::AuxSL* auxsl = nullptr;
-    uint32_t* anc_info = nullptr;
-    uint32_t* anc = nullptr;
-    pt::F4* blob = nullptr;
+    unsigned char* base = nullptr;
+    const pt::F4* blob = nullptr;
+    const pt::Node* nodes = nullptr;
+    const pt::Prim* prims = nullptr;
+    const uint32_t* anc_info = nullptr;
+    const uint32_t* anc = nullptr;
+    const pt::Shade* shade = nullptr;
+    const uint32_t* planes = nullptr;
+    const uint32_t* emitters = nullptr;
+    const float* thr = nullptr;
+    const pt::AuxSL* top = nullptr;   // aux root entries + their child nodes' entries (k_wcamera)
+    uint32_t n_top = 0;
+    pt::AuxNode* aux = nullptr;       // BVH2 aux (megakernel only)
+};
+struct DevEntry {
+    std::mutex mu;                    // this device's upload (devices upload in parallel)
+    bool ready = false;
+    DevScene d;
 };
 
 constexpr uint32_t kCandCap = 24;   // candidate-list words per lane (per replay pass)
@@ -190,13 +212,19 @@ struct pt_scene {
     std::vector<float> regions;   // per reference node: its leaf's hit region {lo, hi} (lo > hi: unbounded)
     uint32_t aux_coarse_leaves = 0;   // leaf entries whose binary16 own box is > 4x wider than the f32 one
     float thr[256];
-    std::map<int, DevScene> dev;
-    std::mutex mu;
+    // the device upload image (built once, on the first upload): section offsets
+    std::vector<unsigned char> image;
+    size_t i_shade = 0, i_planes = 0, i_emit = 0, i_thr = 0, i_top = 0;
+    uint32_t n_top = 0;
+    std::map<int, std::unique_ptr<DevEntry>> dev;
+    std::mutex mu;                    // the image and the device map (not the uploads)
 };
 
 struct pt_session {
     pt_scene* sc = nullptr;
     int dev = 0;
+    const DevScene* ds = nullptr;   // the scene's copy on this device
+    double upload_ms = 0.0;         // time this session spent uploading it (0: already there)
     pt::TileMap tm{};
     uint32_t n_tiles_local = 0, n_slots = 0, depth = 0;
     pt::PixelState st{};          // per-slot records + fold records (device)
@@ -214,14 +242,17 @@ struct pt_session {
     uint32_t mix[3] = {PT_PROBE_EVERY, PT_PROBE_MIN, PT_AUX2}, mix_low[3] = {PT_PROBE_EVERY, PT_PROBE_MIN, PT_AUX2};
     uint32_t lowq = 0;
     uint32_t low_grid = 0;        // path workgroups of those rounds
-    uint32_t lowq2 = 0, low_grid2 = 0;   // (tuning) a second tier: rounds under lowq2 chains on low_grid2
     uint32_t coop_team = 8;       // lanes per chain in the cooperative engine (pure-coop rate, teams of
                                   // 64 / 32 / 16 / 8: 283 / 392 / 572 / 815 Mray/s)
-    pt::F4* qbuf = nullptr;       // 10 * n_slots F4: fq0.ro, fq0.rd, fq1.ro, fq1.rd, done.ro/rd, ex.ro/rd, fq0.ri, fq1.ri
-    uint32_t* hid = nullptr;      // n_slots (done.id)
-    uint32_t* pidbuf = nullptr;   // 2 * n_slots (fresh queues' plane prims)
+    // every device buffer below lives in one allocation (pt_session_create)
+    unsigned char* arena = nullptr;
+    size_t arena_bytes = 0;
+    pt::RayQ fq[2] = {};          // fresh rays (n_slots each)
+    pt::DoneQ done = {};          // exact-DFS results (lane_cap)
+    pt::RayQ ex = {};             // rays handed to the exact DFS (lane_cap)
     uint32_t* carry = nullptr;    // 2 * carry_cap * carry_words
     uint32_t* endq = nullptr;     // path_grid * PT_CMAX: the shade waves' ended paths (PT_DEFER_ENDS)
+    uint32_t lane_cap = 0;        // min(pixels, query lanes): what one round can suspend or hand over
     uint32_t carry_cap = 0, carry_words = 0;
     uint32_t* ctl = nullptr;      // 2 x PT_CTL_SET round counters
     uint32_t* ctl_host = nullptr; // pinned copy of one counter set
@@ -235,7 +266,6 @@ struct pt_session {
     uint32_t deferred_spp = 0;    // wavefront engine: trace() calls not yet run (one pass at the next sync point)
     uint32_t* tile_order = nullptr;   // local tiles in Z-order of their image position (k_wcamera)
     std::vector<uint32_t> gtiles;     // this rank's window tiles (local -> window tile), tm.gtile on the device
-    uint32_t* gtile_dev = nullptr;
     // optional progress report during a pass (pt_render's bar): finished samples,
     // counted by the kernels into host-mapped memory and polled at the round syncs
     std::function<void(uint64_t)> on_progress;
@@ -482,6 +512,9 @@ void build_query_blob(pt_scene* s) {
     b.reserve(s->dnodes.size() * 2 + s->auxsl.size() * 2 + (s->anc_info.size() + s->anc.size()) / 4 +
               s->dprims.size() * (4 + 5 + 4) + 64);
     auto append = [&b](const void* p, size_t bytes) {
+        // sections are addressed by 32-bit byte offsets (and the device forms record
+        // offsets from them in 32 bits): the whole blob must stay below 4 GiB
+        if (b.size() * 16 + bytes >= 0xFFFFFFF0ull) throw std::runtime_error("scene too large for 32-bit query offsets");
         const uint32_t o = (uint32_t)(b.size() * 16);
         const size_t n = (bytes + 15) / 16;
         b.resize(b.size() + n, pt::F4{0.f, 0.f, 0.f, 0.f});
@@ -558,50 +591,143 @@ void build_query_blob(pt_scene* s) {
 }
 
 // ------------------------------------------------------------- devices ---
+// device properties, queried once per device (hipGetDeviceProperties costs
+// milliseconds, and every session creation needs the CU count)
+struct DevProps { bool ok = false; int cus = 0; char arch[64] = {0}; };
+int device_props(int dev, DevProps* out) {
+    static std::mutex mu;
+    static std::map<int, DevProps> cache;
+    static int count = -1;
+    std::lock_guard<std::mutex> lk(mu);
+    if (count < 0) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(PT_E_NO_GPU, "no HIP device visible");
+        count = n;
+    }
+    if (dev < 0 || dev >= count) return fail(PT_E_NO_GPU, "device index out of range");
+    DevProps& p = cache[dev];
+    if (!p.ok) {
+        hipDeviceProp_t pr;
+        HIP_TRY(hipGetDeviceProperties(&pr, dev));
+        p.cus = std::max(1, pr.multiProcessorCount);
+        strncpy(p.arch, pr.gcnArchName, sizeof(p.arch) - 1);
+        p.ok = true;
+    }
+    *out = p;
+    return PT_OK;
+}
+
 int check_device(int dev) {
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(PT_E_NO_GPU, "no HIP device visible");
-    if (dev < 0 || dev >= n) return fail(PT_E_NO_GPU, "device index out of range");
-    hipDeviceProp_t pr;
-    HIP_TRY(hipGetDeviceProperties(&pr, dev));
-    if (strncmp(pr.gcnArchName, "gfx950", 6) != 0)
-        return fail(PT_E_NO_GPU, std::string("device is ") + pr.gcnArchName + ", this build targets gfx950");
+    DevProps p;
+    if (const int rc = device_props(dev, &p)) return rc;
+    if (strncmp(p.arch, "gfx950", 6) != 0)
+        return fail(PT_E_NO_GPU, std::string("device is ") + p.arch + ", this build targets gfx950");
     return PT_OK;
 }
 
-template <class T>
-int upload(T** dst, const std::vector<T>& v) {
-    const size_t bytes = std::max<size_t>(sizeof(T), v.size() * sizeof(T));
-    HIP_TRY(hipMalloc(reinterpret_cast<void**>(dst), bytes));
-    if (!v.empty()) HIP_TRY(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
-    return PT_OK;
+// k_wcamera's costly-class test reads the wide aux root's entries and, for each
+// inner one, its child node's entries (f32 host form): entries 0..W-1 = the root,
+// entries W (1 + k) .. = the child of root entry k, whose code is rewritten to 1 + k
+std::vector<pt::AuxSL> aux_top(const pt_scene* s) {
+    const uint32_t W = PT_AUXW;
+    std::vector<pt::AuxSL> t;
+    if (s->auxsl.size() < W) return t;
+    t.assign(s->auxsl.begin(), s->auxsl.begin() + W);
+    for (uint32_t k = 0; k < W; ++k) {
+        const uint32_t code = pt::f2u(t[k].b.w);
+        if (code == 0xFFFFFFFFu || (code & 0x80000000u)) continue;
+        if ((size_t)(code + 1) * W > s->auxsl.size()) throw std::runtime_error("aux root child out of range");
+        const uint32_t at = (uint32_t)(t.size() / W);
+        t.insert(t.end(), s->auxsl.begin() + (size_t)code * W, s->auxsl.begin() + (size_t)(code + 1) * W);
+        t[k].b.w = pt::u2f(at);
+    }
+    return t;
 }
 
-int ensure_device_scene(pt_scene* s, int dev, DevScene** out) {
-    std::lock_guard<std::mutex> lk(s->mu);
-    auto it = s->dev.find(dev);
-    if (it != s->dev.end()) { *out = &it->second; return PT_OK; }
+// the host image of a device scene (DevScene): sections at 256-B offsets
+void build_upload_image(pt_scene* s) {
+    if (!s->image.empty()) return;
+    const std::vector<pt::AuxSL> top = aux_top(s);
+    size_t at = 0;
+    auto sec = [&at](size_t bytes) {
+        const size_t o = at;
+        at = (at + std::max<size_t>(bytes, 4) + 255) & ~(size_t)255;
+        return o;
+    };
+    sec(s->blob.size() * sizeof(pt::F4));
+    s->i_shade = sec(s->dshade.size() * sizeof(pt::Shade));
+    s->i_planes = sec(s->planes.size() * 4);
+    s->i_emit = sec(s->emitters.size() * 4);
+    s->i_thr = sec(sizeof(s->thr));
+    s->i_top = sec(top.size() * sizeof(pt::AuxSL));
+    s->n_top = (uint32_t)top.size();
+    std::vector<unsigned char> img(at, 0);
+    memcpy(img.data(), s->blob.data(), s->blob.size() * sizeof(pt::F4));
+    if (!s->dshade.empty()) memcpy(img.data() + s->i_shade, s->dshade.data(), s->dshade.size() * sizeof(pt::Shade));
+    if (!s->planes.empty()) memcpy(img.data() + s->i_planes, s->planes.data(), s->planes.size() * 4);
+    if (!s->emitters.empty()) memcpy(img.data() + s->i_emit, s->emitters.data(), s->emitters.size() * 4);
+    memcpy(img.data() + s->i_thr, s->thr, sizeof(s->thr));
+    if (!top.empty()) memcpy(img.data() + s->i_top, top.data(), top.size() * sizeof(pt::AuxSL));
+    s->image.swap(img);
+}
+
+// The scene on device `dev`, uploaded on first use: one allocation and one copy
+// of the upload image.  Devices upload in parallel (a lock per device).  mega:
+// also the BVH2 aux of the megakernel traversal.
+int ensure_device_scene(pt_scene* s, int dev, bool mega, DevScene** out, double* upload_ms) {
+    DevEntry* e;
+    {
+        std::lock_guard<std::mutex> lk(s->mu);
+        try {
+            build_upload_image(s);
+        } catch (const std::exception& x) {
+            return fail(PT_E_SCENE, x.what());
+        }
+        auto& slot = s->dev[dev];
+        if (!slot) slot.reset(new DevEntry());
+        e = slot.get();
+    }
+    std::lock_guard<std::mutex> lk(e->mu);
+    DevScene& d = e->d;
+    *upload_ms = 0.0;
     HIP_TRY(hipSetDevice(dev));
-    DevScene d;
-    int rc;
-    if ((rc = upload(&d.nodes, s->dnodes)) || (rc = upload(&d.prims, s->dprims)) || (rc = upload(&d.shade, s->dshade)) ||
-        (rc = upload(&d.planes, s->planes)) || (rc = upload(&d.emitters, s->emitters)))
-        return rc;
-    std::vector<float> thr(s->thr, s->thr + 256);
-    if ((rc = upload(&d.thr, thr))) return rc;
-    if ((rc = upload(&d.aux, s->aux))) return rc;
-    if ((rc = upload(&d.auxsl, s->auxsl))) return rc;
-    if ((rc = upload(&d.anc_info, s->anc_info)) || (rc = upload(&d.anc, s->anc))) return rc;
-    if ((rc = upload(&d.blob, s->blob))) return rc;
-    s->dev[dev] = d;
-    *out = &s->dev[dev];
+    if (!e->ready) {
+        const auto t0 = std::chrono::steady_clock::now();
+        void* p = nullptr;
+        HIP_TRY(hipMalloc(&p, s->image.size()));
+        if (hipMemcpy(p, s->image.data(), s->image.size(), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipFree(p);
+            return fail(PT_E_HIP, "scene upload failed");
+        }
+        unsigned char* b = static_cast<unsigned char*>(p);
+        d.base = b;
+        d.blob = reinterpret_cast<const pt::F4*>(b);
+        d.nodes = reinterpret_cast<const pt::Node*>(b + s->o_nodes);
+        d.prims = reinterpret_cast<const pt::Prim*>(b + s->o_prim);
+        d.anc_info = reinterpret_cast<const uint32_t*>(b + s->o_ainfo);
+        d.anc = reinterpret_cast<const uint32_t*>(b + s->o_anc);
+        d.shade = reinterpret_cast<const pt::Shade*>(b + s->i_shade);
+        d.planes = reinterpret_cast<const uint32_t*>(b + s->i_planes);
+        d.emitters = reinterpret_cast<const uint32_t*>(b + s->i_emit);
+        d.thr = reinterpret_cast<const float*>(b + s->i_thr);
+        d.top = reinterpret_cast<const pt::AuxSL*>(b + s->i_top);
+        d.n_top = s->n_top;
+        *upload_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        e->ready = true;
+    }
+    if (mega && !d.aux) {
+        const size_t bytes = std::max<size_t>(sizeof(pt::AuxNode), s->aux.size() * sizeof(pt::AuxNode));
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d.aux), bytes));
+        if (!s->aux.empty())
+            HIP_TRY(hipMemcpy(d.aux, s->aux.data(), s->aux.size() * sizeof(pt::AuxNode), hipMemcpyHostToDevice));
+    }
+    *out = &d;
     return PT_OK;
 }
 
 void free_device_scene(DevScene& d) {
-    (void)hipFree(d.nodes); (void)hipFree(d.prims); (void)hipFree(d.shade);
-    (void)hipFree(d.planes); (void)hipFree(d.emitters); (void)hipFree(d.thr); (void)hipFree(d.aux);
-    (void)hipFree(d.auxsl); (void)hipFree(d.anc_info); (void)hipFree(d.anc); (void)hipFree(d.blob);
+    (void)hipFree(d.base);
+    (void)hipFree(d.aux);
 }
 
 // per-lane LDS words: replay needs [aux stack | candidates], the exact DFS its stack
@@ -912,7 +1038,7 @@ void pt_scene_free(pt_scene* s) {
     if (!s) return;
     for (auto& kv : s->dev) {
         (void)hipSetDevice(kv.first);
-        free_device_scene(kv.second);
+        free_device_scene(kv.second->d);
     }
     delete s;
 }
@@ -928,11 +1054,16 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
     if (s->hs.depth >= (1u << 24)) return fail(PT_E_SCENE, "RAY_DEPTH too large (at most 16777215)");
     int rc = check_device(o->device);
     if (rc) return rc;
+    // the megakernel (exact / division-form traversal, PT_TUNE engine=mega) also reads the BVH2 aux
+    const bool mega = o->traversal != PT_TRAVERSAL_REPLAY || tune_str("engine") == "mega";
     DevScene* ds = nullptr;
-    if ((rc = ensure_device_scene(s, o->device, &ds))) return rc;
+    double up_ms = 0.0;
+    if ((rc = ensure_device_scene(s, o->device, mega, &ds, &up_ms))) return rc;
     auto* ss = new pt_session();
     ss->sc = s;
     ss->dev = o->device;
+    ss->ds = ds;
+    ss->upload_ms = up_ms;
     ss->traversal = o->traversal;
     ss->depth = s->hs.depth;
     ss->tm.W = s->hs.W;
@@ -959,47 +1090,32 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         return code;
     };
     if (hipSetDevice(ss->dev) != hipSuccess) return cleanup(fail(PT_E_HIP, "hipSetDevice failed"));
+    DevProps props;
+    if ((rc = device_props(ss->dev, &props))) return cleanup(rc);
+    const uint32_t cus = (uint32_t)props.cus;
     const size_t n = std::max<size_t>(ss->n_slots, 1);
     ss->st.depth = std::max<uint32_t>(ss->depth, 1u);
-    if (!ss->gtiles.empty() &&
-        (hipMalloc(&ss->gtile_dev, ss->gtiles.size() * 4) != hipSuccess ||
-         hipMemcpy(ss->gtile_dev, ss->gtiles.data(), ss->gtiles.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
-        return cleanup(fail(PT_E_OOM, "device allocation failed (tile list)"));
-    ss->tm.gtile = ss->gtile_dev;
-    if (take_stream(ss->dev, &ss->stream) != hipSuccess ||
-        hipMalloc(&ss->st.rec, 2 * n * sizeof(uint4)) != hipSuccess ||
-        hipMalloc(&ss->st.fold, (size_t)ss->st.depth * n * sizeof(uint4)) != hipSuccess ||
-        hipMalloc(&ss->counters, 8 * PT_CTR_COPIES * PT_CTR_STRIDE) != hipSuccess ||
-        hipMalloc(&ss->out, 3 * n) != hipSuccess)
-        return cleanup(fail(PT_E_OOM, "device allocation failed"));
     ss->st.n_slots = ss->n_slots;
     // engine: the wavefront pipeline for the (filtered) replay traversal; the
     // megakernel for the exact DFS and the division-form replay (PT_TUNE engine=mega forces it)
     ss->wave = o->traversal == PT_TRAVERSAL_REPLAY;
     if (tune_str("engine") == "mega") ss->wave = false;
+    std::vector<uint32_t> ord;   // wavefront: the local tiles' seeding order
     if (ss->wave) {
-        // suspended-query records: Query | slot | aux stack, rounded to 16 B
-        ss->carry_words = ((uint32_t)(sizeof(pt::Query) / 4) + 1u + std::max<uint32_t>(s->auxw_stack, 1u) + 3u) & ~3u;
-        // a pixel has at most one ray in flight, so at most n queries are ever
-        // suspended at once: the carry queue can never overflow (an over-full
-        // queue would make its queries run to the end inside the round)
-        ss->carry_cap = (uint32_t)n;
-        if (hipMalloc(&ss->qbuf, 10 * n * 16) != hipSuccess || hipMalloc(&ss->hid, n * 4) != hipSuccess ||
-            hipMalloc(&ss->pidbuf, 2 * n * 4) != hipSuccess ||
-            hipMalloc(&ss->carry, 2ull * ss->carry_cap * ss->carry_words * 4) != hipSuccess ||
-            hipMalloc(&ss->ctl, 8 * PT_CTL_SET) != hipSuccess || hipHostMalloc(&ss->ctl_host, 64) != hipSuccess)
-            return cleanup(fail(PT_E_OOM, "device allocation failed (wavefront buffers)"));
-        hipDeviceProp_t pr;
-        if (hipGetDeviceProperties(&pr, ss->dev) != hipSuccess) return cleanup(fail(PT_E_HIP, "device query failed"));
-        ss->shade_grid = std::min<uint32_t>((uint32_t)std::max(1, pr.multiProcessorCount) * 8u,
-                                            std::max(1u, ss->n_tiles_local));
+        ss->shade_grid = std::min<uint32_t>(cus * 8u, std::max(1u, ss->n_tiles_local));
         // path engine: PT_NQ query waves + 1 shade wave per workgroup, as many workgroups
         // per CU as its waves-per-SIMD occupancy holds (4 SIMDs per CU)
         ss->path_budget = (uint32_t)std::max(1, tune_int("budget", (int)ss->path_budget));
         const int wg_cu = std::max(1, (int)(PT_PATH_WAVES_PER_EU * 4u / (PT_NQ + 1u)));
-        ss->path_grid = (uint32_t)std::max(1, pr.multiProcessorCount) * (uint32_t)std::max(1, tune_int("wg_per_cu", wg_cu));
-        if (hipMalloc(&ss->endq, (size_t)ss->path_grid * PT_CMAX * 4) != hipSuccess)
-            return cleanup(fail(PT_E_OOM, "device allocation failed (ended-path queues)"));
+        ss->path_grid = cus * (uint32_t)std::max(1, tune_int("wg_per_cu", wg_cu));
+        // suspended-query records: Query | slot | aux stack, rounded to 16 B.  Only a
+        // query lane suspends (one query at round end), and a pixel has at most one ray
+        // in flight, so a round appends at most min(pixels, query lanes) of them: the
+        // carry queue can never overflow.  The exact-DFS hand-over queues (ex, done)
+        // have the same bound.
+        ss->carry_words = ((uint32_t)(sizeof(pt::Query) / 4) + 1u + std::max<uint32_t>(s->auxw_stack, 1u) + 3u) & ~3u;
+        ss->lane_cap = (uint32_t)std::min<uint64_t>(n, (uint64_t)ss->path_grid * PT_NQ * 64u);
+        ss->carry_cap = ss->lane_cap;
         // a round whose chains are this few runs them to the end of the pass (a few
         // per query wave: rebalancing them costs more rounds than it saves)
         ss->path_runend = ss->path_grid * PT_NQ * 4u;
@@ -1011,7 +1127,6 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // a round whose chains are at most this many runs the cooperative engine (one
         // wave per chain) to the end of the pass; it needs a wave's aux stack to hold
         // a depth-first descent below its expansion limit, and lane 0's exact DFS stack
-        const uint32_t cus = (uint32_t)std::max(1, pr.multiProcessorCount);
         // 49,152 on the 256-CU part (2 query waves per shade wave, hit-region query; rank-of-4 /
         // rank-of-8 per GPU, teams of 8, two runs each: 32 k 2,758-2,782 / 2,348-2,396, 49 k
         // 2,754-2,774 / 2,377-2,421, 65 k 2,731-2,763 / 2,318-2,338, 98 k 2,695-2,699 / 2,220-2,324,
@@ -1053,8 +1168,6 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
             // included) -25 % at rank-of-8.
             ss->lowq = (uint32_t)std::max(0, tune_int("lowq", (int)(cus * 768u)));
             ss->low_grid = std::min(ss->path_grid, cus * (uint32_t)std::max(1, tune_int("lowq_wg", 2)));
-            ss->lowq2 = (uint32_t)std::max(0, tune_int("lowq2", 0));
-            ss->low_grid2 = std::min(ss->path_grid, cus * (uint32_t)std::max(1, tune_int("lowq2_wg", 1)));
         }
         if (ss->n_tiles_local) {
             // seeding order of the pass: the local tiles sorted by the Z-order (Morton)
@@ -1069,12 +1182,71 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
                 key[t] = {m, t};
             }
             std::sort(key.begin(), key.end());
-            std::vector<uint32_t> ord(ss->n_tiles_local);
+            ord.resize(ss->n_tiles_local);
             for (uint32_t t = 0; t < ss->n_tiles_local; ++t) ord[t] = key[t].second;
-            if (hipMalloc(&ss->tile_order, ord.size() * 4) != hipSuccess ||
-                hipMemcpy(ss->tile_order, ord.data(), ord.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
-                return cleanup(fail(PT_E_OOM, "device allocation failed (tile order)"));
         }
+    }
+    // Every device buffer of the session in ONE allocation (sections at 256-B
+    // offsets), and the two small host-made tables with one copy: session set-up is
+    // a handful of runtime calls, whatever the pixel count.
+    {
+        size_t at = 0;
+        auto sec = [&at](size_t bytes) {
+            const size_t o = at;
+            at = (at + std::max<size_t>(bytes, 16) + 255) & ~(size_t)255;
+            return o;
+        };
+        const size_t tables = sec((ss->gtiles.size() + ord.size()) * 4);
+        const size_t a_rec = sec(2 * n * sizeof(uint4)), a_fold = sec((size_t)ss->st.depth * n * sizeof(uint4));
+        const size_t a_ctr = sec(8 * PT_CTR_COPIES * PT_CTR_STRIDE), a_out = sec(3 * n);
+        size_t a_fq[2][3] = {{0, 0, 0}, {0, 0, 0}}, a_pid = 0, a_dq[2] = {0, 0}, a_ex[2] = {0, 0}, a_hid = 0;
+        size_t a_carry = 0, a_ctl = 0, a_endq = 0;
+        const size_t lanes = ss->lane_cap;
+        if (ss->wave) {
+            for (int q = 0; q < 2; ++q)
+                for (int k = 0; k < 3; ++k) a_fq[q][k] = sec(n * 16);
+            a_pid = sec(2 * n * 4);
+            for (int k = 0; k < 2; ++k) { a_dq[k] = sec(lanes * 16); a_ex[k] = sec(lanes * 16); }
+            a_hid = sec(lanes * 4);
+            a_carry = sec(2ull * ss->carry_cap * ss->carry_words * 4);
+            a_ctl = sec(8 * PT_CTL_SET);
+            a_endq = sec((size_t)ss->path_grid * PT_CMAX * 4);
+        }
+        if (take_stream(ss->dev, &ss->stream) != hipSuccess) return cleanup(fail(PT_E_HIP, "stream creation failed"));
+        void* p = nullptr;
+        if (hipMalloc(&p, at) != hipSuccess) return cleanup(fail(PT_E_OOM, "device allocation failed (session buffers)"));
+        ss->arena = static_cast<unsigned char*>(p);
+        unsigned char* A = ss->arena;
+        if (!ss->gtiles.empty()) {
+            std::vector<uint32_t> t(ss->gtiles);
+            t.insert(t.end(), ord.begin(), ord.end());
+            if (hipMemcpy(A + tables, t.data(), t.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+                return cleanup(fail(PT_E_HIP, "tile tables upload failed"));
+            ss->tm.gtile = reinterpret_cast<const uint32_t*>(A + tables);
+            if (!ord.empty()) ss->tile_order = reinterpret_cast<uint32_t*>(A + tables) + ss->gtiles.size();
+        }
+        ss->st.rec = reinterpret_cast<uint4*>(A + a_rec);
+        ss->st.fold = reinterpret_cast<uint4*>(A + a_fold);
+        ss->counters = reinterpret_cast<unsigned long long*>(A + a_ctr);
+        ss->out = A + a_out;
+        if (ss->wave) {
+            for (int q = 0; q < 2; ++q) {
+                ss->fq[q].ro = reinterpret_cast<pt::F4*>(A + a_fq[q][0]);
+                ss->fq[q].rd = reinterpret_cast<pt::F4*>(A + a_fq[q][1]);
+                ss->fq[q].ri = reinterpret_cast<pt::F4*>(A + a_fq[q][2]);
+                ss->fq[q].pid = reinterpret_cast<int*>(A + a_pid) + q * n;
+            }
+            ss->done = pt::DoneQ{reinterpret_cast<pt::F4*>(A + a_dq[0]), reinterpret_cast<pt::F4*>(A + a_dq[1]),
+                                 reinterpret_cast<uint32_t*>(A + a_hid)};
+            ss->ex = pt::RayQ{reinterpret_cast<pt::F4*>(A + a_ex[0]), reinterpret_cast<pt::F4*>(A + a_ex[1]), nullptr,
+                              nullptr};
+            ss->carry = reinterpret_cast<uint32_t*>(A + a_carry);
+            ss->ctl = reinterpret_cast<uint32_t*>(A + a_ctl);
+            ss->endq = reinterpret_cast<uint32_t*>(A + a_endq);
+            if (hipHostMalloc(&ss->ctl_host, 64) != hipSuccess)
+                return cleanup(fail(PT_E_OOM, "host allocation failed (round counters)"));
+        }
+        ss->arena_bytes = at;
     }
     if (hipMemsetAsync(ss->counters, 0, 8 * PT_CTR_COPIES * PT_CTR_STRIDE, ss->stream) != hipSuccess) return cleanup(fail(PT_E_HIP, "memset failed"));
     if (ss->n_tiles_local) {
@@ -1097,7 +1269,7 @@ int pt_session_layout(const pt_session* ss, uint32_t* n_tiles, uint64_t* packed_
 
 namespace {
 int trace_wave(pt_session* ss, uint32_t spp) {
-    DevScene& ds = ss->sc->dev[ss->dev];
+    const DevScene& ds = *ss->ds;
     const pt_scene* s = ss->sc;
     pt::WaveParams wp;
     memset(&wp, 0, sizeof(wp));
@@ -1114,16 +1286,16 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.S.anc_info = ds.anc_info;
     wp.S.anc = ds.anc;
     set_blob(wp.S, s, ds.blob);
-    wp.aux = ds.auxsl;
+    wp.top = ds.top;
+    wp.n_top = ds.n_top;
     wp.n_aux = (uint32_t)s->auxsl.size();
     wp.cam = ss->cam;
     wp.tm = ss->tm;
     wp.st = ss->st;
-    const size_t n = std::max<size_t>(ss->n_slots, 1);
-    wp.fq[0] = pt::RayQ{ss->qbuf, ss->qbuf + n, reinterpret_cast<int*>(ss->pidbuf), ss->qbuf + 8 * n};
-    wp.fq[1] = pt::RayQ{ss->qbuf + 2 * n, ss->qbuf + 3 * n, reinterpret_cast<int*>(ss->pidbuf) + n, ss->qbuf + 9 * n};
-    wp.done = pt::DoneQ{ss->qbuf + 4 * n, ss->qbuf + 5 * n, ss->hid};
-    wp.ex = pt::RayQ{ss->qbuf + 6 * n, ss->qbuf + 7 * n, nullptr, nullptr};
+    wp.fq[0] = ss->fq[0];
+    wp.fq[1] = ss->fq[1];
+    wp.done = ss->done;
+    wp.ex = ss->ex;
     wp.endq = ss->endq;
     wp.cq[0] = ss->carry;
     wp.cq[1] = ss->carry + (size_t)ss->carry_cap * ss->carry_words;
@@ -1150,7 +1322,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
         wp.path_cap = (uint32_t)std::min<uint64_t>(PT_CMAX, std::max<uint64_t>(256u, share * 5u / 8u));
     }
     if (tune_has("cap")) wp.path_cap = std::min<uint32_t>(PT_CMAX, (uint32_t)std::max(64, tune_int("cap", 0)));
-    wp.tile_order = tune_int("rowmajor", 0) ? nullptr : ss->tile_order;
+    wp.tile_order = ss->tile_order;
     wp.sparse_steps = ss->sparse_steps;
     wp.coop_reserve = ss->coop_reserve;
     // aux stack words per query lane (PT_TUNE lstack=N < PT_LSTACK: tests of the exact-DFS
@@ -1264,8 +1436,8 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 wp.probe_min = m[1];
                 wp.aux_extra = m[2];
                 if (low && ss->low_grid) {
-                    grid = chains < ss->lowq2 ? ss->low_grid2 : ss->low_grid;
-                    wp.path_cap = PT_CMAX;
+                    grid = ss->low_grid;
+                    if (!tune_has("cap")) wp.path_cap = PT_CMAX;   // (an explicit cap=N stays)
                 }
             }
             HIP_TRY(pt_launch_path_round(wp, grid, 64u, ss->stream, sparse, i0, i1));
@@ -1350,7 +1522,7 @@ int pt_session_trace(pt_session* ss, uint32_t spp) {
         return PT_OK;
     }
     HIP_TRY(hipSetDevice(ss->dev));
-    DevScene& ds = ss->sc->dev[ss->dev];
+    const DevScene& ds = *ss->ds;
     pt::TraceParams tp;
     const pt_scene* s = ss->sc;
     tp.S.aux = ss->traversal == PT_TRAVERSAL_EXACT ? nullptr : ds.aux;
@@ -1374,11 +1546,8 @@ int pt_session_trace(pt_session* ss, uint32_t spp) {
     tp.spp = spp;
     tp.n_tiles_local = ss->n_tiles_local;
     tp.wg_prof = nullptr;
-    // kernel variant: filtered tests unless the division form was asked for;
-    // XCD-banded tile order by default (PT_TUNE variant=<0..3> overrides, for A/B runs)
-    int variant = (ss->traversal == PT_TRAVERSAL_REPLAY ? 1 : 0) | 2;
-    if (tune_has("variant")) variant = tune_int("variant", 0) & 3;
-    if (ss->traversal == PT_TRAVERSAL_EXACT) variant &= 2;
+    // kernel variant: filtered tests unless the division form was asked for; XCD-banded tile order
+    const int variant = (ss->traversal == PT_TRAVERSAL_REPLAY ? 1 : 0) | 2;
     const std::string wgps = tune_str("wgprof");
     const char* wgp = wgps.c_str();
     if (*wgp) {
@@ -1416,7 +1585,7 @@ int pt_session_resolve(pt_session* ss, uint8_t* dev_out, float* dev_radiance) {
     HIP_TRY(hipSetDevice(ss->dev));
     pt::ResolveParams rp;
     rp.st = ss->st;
-    rp.thr = ss->sc->dev[ss->dev].thr;
+    rp.thr = ss->ds->thr;
     rp.out = dev_out ? dev_out : ss->out;
     rp.rad = dev_radiance;
     rp.samples = (uint32_t)ss->samples_done;
@@ -1502,12 +1671,8 @@ void pt_session_free(pt_session* ss) {
     (void)hipSetDevice(ss->dev);
     if (ss->stream) (void)hipStreamSynchronize(ss->stream);
     finish_pending(ss);
-    (void)hipFree(ss->st.rec); (void)hipFree(ss->st.fold); (void)hipFree(ss->counters);
-    (void)hipFree(ss->out); (void)hipFree(ss->rad); (void)hipFree(ss->wg_prof);
-    (void)hipFree(ss->tile_order);
-    (void)hipFree(ss->gtile_dev);
-    (void)hipFree(ss->qbuf); (void)hipFree(ss->hid); (void)hipFree(ss->pidbuf);
-    (void)hipFree(ss->carry); (void)hipFree(ss->ctl); (void)hipFree(ss->endq);
+    (void)hipFree(ss->arena);
+    (void)hipFree(ss->rad); (void)hipFree(ss->wg_prof);
     if (ss->ctl_host) (void)hipHostFree(ss->ctl_host);
     if (ss->prog_host) (void)hipHostFree(ss->prog_host);
     if (ss->stream) {
@@ -1650,6 +1815,9 @@ void pt_render_opts_default(pt_render_opts* o) {
 
 int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radiance, pt_stats* stats) {
     const auto t0 = std::chrono::steady_clock::now();
+    auto ms_since = [](std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    };
     if (!s) return fail(PT_E_INVALID, "null scene");
     pt_render_opts o;
     pt_render_opts_default(&o);
@@ -1664,8 +1832,33 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
         for (auto* x : sess) pt_session_free(x);
         return code;
     };
-    const bool same = same_device();
-    for (int g = 0; g < ngpu; ++g) {
+    // PT_TUNE same_device=1 (test-only): the ngpu sessions all on o.device, rendering
+    // at once; same_device=2: the same, but the ranks render one after another once
+    // every session is set up, so each rank's render time is its time alone on a GPU
+    // (the per-rank phase times of PT_STATS=2 then project an ngpu-GPU run)
+    const int same = tune_int("same_device", 0);
+    // samples per trace call: one pass for all of them (a pass ends with its slowest
+    // pixel, so every extra sync costs a tail).  The wavefront engine reports the
+    // bar from inside the pass; the exact-traversal renderer takes ~20 passes.
+    int last = 0;
+    const bool wave = o.traversal == PT_TRAVERSAL_REPLAY && tune_str("engine") != "mega";
+    const bool in_pass = o.progress && wave;
+    const uint32_t chunk = o.spp_per_launch ? o.spp_per_launch
+                           : o.progress && !in_pass ? std::max(1u, (S + 19u) / 20u) : std::max(S, 1u);
+    // One host thread per GPU sets up its session (the device's scene upload and the
+    // session buffers: devices in parallel) and drives it (the wavefront rounds sync
+    // on their own stream) through the resolve; thread 0 reports progress.
+    std::vector<int> trc((size_t)ngpu, PT_OK);
+    std::vector<std::string> terr((size_t)ngpu);
+    std::vector<float*> drads((size_t)ngpu, nullptr);
+    struct Phase { double setup = 0, upload = 0, wait = 0, render = 0, resolve = 0; };
+    std::vector<Phase> ph((size_t)ngpu);
+    std::mutex turn_mu;
+    std::condition_variable turn_cv;
+    int created = 0, turn = 0;
+    auto work = [&](int g) {
+        Phase& f = ph[(size_t)g];
+        auto t_g = std::chrono::steady_clock::now();
         pt_session_opts so;
         so.device = same ? o.device : o.device + g;
         so.rank = (uint32_t)g;
@@ -1675,57 +1868,72 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
         so.win_y0 = o.win_y0;
         so.win_w = o.win_w;
         so.win_h = o.win_h;
-        if ((rc = pt_session_create(s, &so, &sess[(size_t)g]))) return cleanup(rc);
-    }
-    // samples per trace call: one pass for all of them (a pass ends with its slowest
-    // pixel, so every extra sync costs a tail).  The wavefront engine reports the
-    // bar from inside the pass; the exact-traversal renderer takes ~20 passes.
-    int last = 0;
-    const bool in_pass = o.progress && sess[0]->wave;
-    const uint32_t chunk = o.spp_per_launch ? o.spp_per_launch
-                           : o.progress && !in_pass ? std::max(1u, (S + 19u) / 20u) : std::max(S, 1u);
-    if (in_pass) {
-        const uint64_t total = owned_pixels(sess[0]) * S;
-        sess[0]->on_progress = [&last, total](uint64_t n) { progress_bar(std::min(n, total), total, last); };
-    }
-    // one host thread per GPU drives its session (the wavefront rounds sync on
-    // their own stream); thread 0 reports progress
-    std::vector<int> trc((size_t)ngpu, PT_OK);
-    std::vector<std::string> terr((size_t)ngpu);
-    auto drive = [&](int g) {
+        int r = pt_session_create(s, &so, &sess[(size_t)g]);
         pt_session* x = sess[(size_t)g];
-        for (uint32_t done = 0; done < S;) {
+        if (!r) r = pt_session_sync(x);   // (the session's init kernel)
+        f.setup = ms_since(t_g);
+        if (x) f.upload = x->upload_ms;
+        if (same == 2) {
+            // every session set up, then the ranks' renders one at a time, in rank order
+            std::unique_lock<std::mutex> lk(turn_mu);
+            ++created;
+            turn_cv.notify_all();
+            const auto tw = std::chrono::steady_clock::now();
+            turn_cv.wait(lk, [&] { return created == ngpu && turn == g; });
+            f.wait = ms_since(tw);
+        }
+        const auto t_r = std::chrono::steady_clock::now();
+        if (!r && g == 0 && in_pass) {
+            const uint64_t total = owned_pixels(x) * S;
+            x->on_progress = [&last, total](uint64_t k) { progress_bar(std::min(k, total), total, last); };
+        }
+        for (uint32_t done = 0; !r && done < S;) {
             const uint32_t k = std::min(chunk, S - done);
-            int r = pt_session_trace(x, k);
+            r = pt_session_trace(x, k);
             if (!r && (o.progress || ngpu > 1)) r = pt_session_sync(x);
-            if (r) { trc[(size_t)g] = r; terr[(size_t)g] = pt_last_error(); return; }
             done += k;
-            if (g == 0 && o.progress) progress_bar(done, S, last);
+            if (!r && g == 0 && o.progress) progress_bar(done, S, last);
+        }
+        if (!r) r = pt_session_sync(x);
+        f.render = ms_since(t_r);
+        if (same == 2) {
+            std::lock_guard<std::mutex> lk(turn_mu);
+            ++turn;
+            turn_cv.notify_all();
+        }
+        // resolve on the device (tonemap + quantise into the packed 8-bit tiles)
+        const auto t_v = std::chrono::steady_clock::now();
+        if (!r && radiance && x->n_slots) {
+            if (hipMalloc(&x->rad, 12ull * x->n_slots) != hipSuccess) r = fail(PT_E_OOM, "radiance buffer");
+            drads[(size_t)g] = x->rad;
+        }
+        if (!r) r = pt_session_resolve(x, nullptr, drads[(size_t)g]);
+        f.resolve = ms_since(t_v);
+        if (r) {
+            trc[(size_t)g] = r;
+            terr[(size_t)g] = pt_last_error();
+            if (same == 2) {
+                // (a failed rank must not leave the others waiting for their turn)
+                std::lock_guard<std::mutex> lk(turn_mu);
+                created = ngpu;
+                turn = ngpu;
+                turn_cv.notify_all();
+            }
         }
     };
     if (ngpu == 1) {
-        drive(0);
+        work(0);
     } else {
         std::vector<std::thread> th;
-        for (int g = 0; g < ngpu; ++g) th.emplace_back(drive, g);
+        for (int g = 0; g < ngpu; ++g) th.emplace_back(work, g);
         for (auto& t : th) t.join();
     }
     for (int g = 0; g < ngpu; ++g)
         if (trc[(size_t)g]) return cleanup(fail(trc[(size_t)g], terr[(size_t)g]));
-    // resolve per device (tonemap + quantise on the GPU), then gather the packed
-    // 8-bit tiles: over RCCL to device `o.device` when ngpu > 1, else one copy
+    // gather the packed 8-bit tiles: over RCCL to device `o.device` when ngpu > 1, else one copy
     pt_stats agg;
     memset(&agg, 0, sizeof(agg));
-    std::vector<float*> drads((size_t)ngpu, nullptr);
-    for (int g = 0; g < ngpu; ++g) {
-        pt_session* x = sess[(size_t)g];
-        if ((rc = pt_session_sync(x))) return cleanup(rc);
-        if (radiance && x->n_slots) {
-            if (hipMalloc(&x->rad, 12ull * x->n_slots) != hipSuccess) return cleanup(fail(PT_E_OOM, "radiance buffer"));
-            drads[(size_t)g] = x->rad;
-        }
-        if ((rc = pt_session_resolve(x, nullptr, drads[(size_t)g]))) return cleanup(rc);
-    }
+    const auto t_gather = std::chrono::steady_clock::now();
     if (rgb) {
         // PT_GATHER_AUTO: RCCL when ngpu > 1 (host fallback with a warning);
         // PT_GATHER_RCCL: RCCL at any ngpu, an error if it fails; PT_GATHER_HOST: never RCCL
@@ -1744,6 +1952,16 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
                 pt_unpack_tiles(W, H, (uint32_t)g, (uint32_t)ngpu, packed.data(), rgb);
             }
         }
+    }
+    const double gather_ms = ms_since(t_gather);
+    if (const char* e = getenv("PT_STATS"); e && atoi(e) >= 2) {
+        // per-rank phase times (the CLI's PT_STATS=2): set-up = the device's scene upload (if
+        // this session did it) + the session's buffers and init kernel
+        for (int g = 0; g < ngpu; ++g)
+            fprintf(stderr, "pt_render rank %d/%d: setup_ms=%.1f scene_upload_ms=%.1f wait_ms=%.1f render_ms=%.1f "
+                    "resolve_ms=%.1f\n", g, ngpu, ph[(size_t)g].setup, ph[(size_t)g].upload, ph[(size_t)g].wait,
+                    ph[(size_t)g].render, ph[(size_t)g].resolve);
+        fprintf(stderr, "pt_render gather_ms=%.1f path=%s\n", gather_ms, agg.gather_rccl ? "rccl" : "host");
     }
     for (int g = 0; g < ngpu; ++g) {
         pt_session* x = sess[(size_t)g];

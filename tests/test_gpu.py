@@ -311,14 +311,16 @@ def test_render_gather_paths(pt, ngpu_gather):
     assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
 
 
+@pytest.mark.parametrize("mode", ["1", "2"])
 @pytest.mark.parametrize("ngpu", [2, 3, 8])
 @pytest.mark.parametrize("cfg", ["c1", "c2"])
-def test_render_ngpu_sessions_on_one_device(pt, cfg, ngpu, monkeypatch):
-    """pt_render(ngpu = n): n host threads and n tile sessions (rank g of n) --
-    the drop-in's own multi-GPU path -- run here with every session on device 0
-    (PT_TUNE same_device=1, framebuffer through the host).  The gathered image and
-    the summed ray count must equal the reference's (= ngpu 1)."""
-    monkeypatch.setenv("PT_TUNE", "same_device=1")
+def test_render_ngpu_sessions_on_one_device(pt, cfg, ngpu, mode, monkeypatch):
+    """pt_render(ngpu = n): n host threads, each setting up its own tile session
+    (rank g of n) and driving it -- the drop-in's own multi-GPU path -- run here with
+    every session on device 0 (PT_TUNE same_device=1, framebuffer through the host;
+    same_device=2: the ranks render one after another once all are set up).  The
+    gathered image and the summed ray count must equal the reference's (= ngpu 1)."""
+    monkeypatch.setenv("PT_TUNE", "same_device=" + mode)
     full = M["full"][cfg]
     with pt.Scene.load(U.scene_path(cfg)) as s:
         rgb, _, st = s.render(ngpu=ngpu)
@@ -328,18 +330,52 @@ def test_render_ngpu_sessions_on_one_device(pt, cfg, ngpu, monkeypatch):
     assert st["rays"] == full["rays"] and st["errors"] == 0 and st["gather_rccl"] == 0
 
 
-def test_cli_ngpu_sessions_on_one_device(pt, tmp_path):
-    """The CLI with PT_NGPU=4 (4 sessions on device 0, PT_TUNE same_device=1): the
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_cli_ngpu_sessions_on_one_device(pt, tmp_path, mode):
+    """The CLI with PT_NGPU=4 (4 sessions on device 0, PT_TUNE same_device=1 or 2): the
     reference's config-1 bytes; the communicator set-up is done on the start-up
-    thread (phases_ms comm_init), not after the render."""
+    thread (phases_ms comm_init), not after the render; PT_STATS=2 prints every
+    rank's set-up / render / resolve times and the gather's."""
+    import re
     import subprocess
     out = tmp_path / "c1.ppm"
     exe = U.os.path.join(U.PKG, "build", "pt_render")
     r = subprocess.run([exe, U.scene_path("c1"), str(out)], capture_output=True, text=True, timeout=300,
-                       env=dict(U.os.environ, PT_QUIET="1", PT_STATS="2", PT_NGPU="4", PT_TUNE="same_device=1"))
+                       env=dict(U.os.environ, PT_QUIET="1", PT_STATS="2", PT_NGPU="4", PT_TUNE="same_device=" + mode))
     assert r.returncode == 0, r.stderr
     assert "ngpu=4" in r.stderr and "comm_init=" in r.stderr, r.stderr
+    ranks = re.findall(r"pt_render rank (\d)/4: setup_ms=[\d.]+ scene_upload_ms=([\d.]+) wait_ms=[\d.]+ "
+                       r"render_ms=[\d.]+ resolve_ms=[\d.]+", r.stderr)
+    assert sorted(int(g) for g, _ in ranks) == [0, 1, 2, 3], r.stderr
+    # one device: exactly one session uploads the scene
+    assert sum(float(u) > 0 for _, u in ranks) == 1, r.stderr
+    assert "pt_render gather_ms=" in r.stderr
     assert U.md5(out.read_bytes()) == M["full"]["c1"]["md5"]
+
+
+# Every scheduling knob of PT_TUNE (INTEGRATION.md §4) must leave the bytes alone: a
+# knob changes which chains run where and when, never a pixel's stream or its float
+# order.  Each runs the path engine (coop=0, budget=2: many rounds, suspensions) on a
+# dragon window against the reference's fixture.  (engine, budget, runend, sparse,
+# coop, coop_team, lstack, same_device: the tests above.)
+TUNE_KEYS = ["wg_per_cu=2", "wg_per_cu=1", "runend=1000000", "sparse_steps=2", "sparse_steps=16", "round_batch=4",
+             "probe_every=1", "probe_min=1", "aux_extra=0", "aux_extra=3", "lowq=0", "lowq=100000000",
+             "lowq=100000000,lowq_wg=1", "lowq=100000000,lowq_probe_every=1,lowq_probe_min=2,lowq_aux_extra=2",
+             "cap=64", "batch=1", "batch=64", "roundlog=1", "roundlog=2", "prepstats=1"]
+
+
+@pytest.mark.parametrize("tune", TUNE_KEYS)
+@pytest.mark.parametrize("name", ["dragon_64x64x16", "c2_win_240_200_24x24"])
+def test_tuning_keys_bit_exact(pt, name, tune, monkeypatch):
+    monkeypatch.setenv("PT_TUNE", "coop=0,budget=2," + tune)
+    m, img, rad = U.golden_image(name)
+    with pt.Scene.load(U.golden_scene_path(name)) as s:
+        s.prepare()
+        win = tuple(m["window"]) if m["window"] else None
+        rgb, r, st = s.render(radiance=True, window=win, traversal=0)
+    assert st["errors"] == 0
+    assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
+    assert np.array_equal(rgb, img)
 
 
 def test_gather_init_one_rank(pt):
