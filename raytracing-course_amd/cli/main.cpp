@@ -84,9 +84,14 @@ int main(int argc, char** argv) {
         return 1;
     }
     t_write = ms();
-    if (env_int("PT_STATS", 0) >= 2)
+    if (env_int("PT_STATS", 0) >= 2) {
         fprintf(stderr, "phases_ms: device_init=%.1f comm_init=%.1f load_prepare=%.1f join=%.1f render=%.1f write=%.1f\n",
                 t_warm, t_comm, t_load, t_join, t_render, t_write);
+        // wall-clock stamps of main()'s start and of the PPM closed (the caller's clock brackets
+        // process start-up before main and the exit after it)
+        const double unix_now = std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+        fprintf(stderr, "unix_main=%.6f unix_written=%.6f\n", unix_now - ms() / 1e3, unix_now);
+    }
     if (env_int("PT_STATS", 0)) {
         fprintf(stderr, "rays=%llu samples=%llu kernel_ms=%.3f wall_ms=%.3f Mray/s=%.3f ngpu=%d gather_rccl=%llu "
                 "fallbacks=%llu rounds=%llu\n",

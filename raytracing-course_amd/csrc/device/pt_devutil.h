@@ -63,8 +63,8 @@ struct PixelHot {
     uint32_t nv;      // vertices of the current path (fold records written; 24 bits: RAY_DEPTH < 2^24)
     uint32_t done;    // samples completed in this session
 };
-__device__ __forceinline__ PixelHot load_hot(const PixelState& st, uint32_t slot) {
-    const uint4 v = st.rec[2u * slot];
+// its 16-B form (rec[2 slot], and k_wpath's LDS pixel table)
+__device__ __forceinline__ PixelHot hot_unpack(uint4 v) {
     PixelHot h;
     h.R.x = v.x;
     h.R.saved = u2f(v.y);
@@ -73,8 +73,12 @@ __device__ __forceinline__ PixelHot load_hot(const PixelState& st, uint32_t slot
     h.done = v.w;
     return h;
 }
+__device__ __forceinline__ uint4 hot_pack(const PixelHot& h) {
+    return make_uint4(h.R.x, f2u(h.R.saved), (h.R.saved_ok & 1u) | (h.nv << 8), h.done);
+}
+__device__ __forceinline__ PixelHot load_hot(const PixelState& st, uint32_t slot) { return hot_unpack(st.rec[2u * slot]); }
 __device__ __forceinline__ void store_hot(const PixelState& st, uint32_t slot, const PixelHot& h) {
-    st.rec[2u * slot] = make_uint4(h.R.x, f2u(h.R.saved), (h.R.saved_ok & 1u) | (h.nv << 8), h.done);
+    st.rec[2u * slot] = hot_pack(h);
 }
 __device__ __forceinline__ f3 load_sum(const PixelState& st, uint32_t slot) {
     const uint4 v = st.rec[2u * slot + 1u];

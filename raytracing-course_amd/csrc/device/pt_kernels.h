@@ -102,7 +102,8 @@ struct WaveParams {
     uint32_t carry_cap, carry_words;
     DoneQ done;
     RayQ ex;                      // rays handed to the exact DFS this round
-    uint32_t* endq;               // per path workgroup PT_CMAX words: its shade wave's ended paths (PT_DEFER_ENDS)
+    uint2* endq;                  // per path workgroup PT_CMAX entries: its shade wave's ended paths
+                                  // {slot | miss << 31, LDS pixel-table entry}
     uint32_t* ctl;                // 2 x PT_CTL_SET round counters
     unsigned long long* counters; // rays, nodes, prim tests, plane tests, errors, aux visits, fallbacks, ray fallbacks
     uint32_t depth;
@@ -127,7 +128,12 @@ struct WaveParams {
     uint32_t probe_min;           // ... or whenever this many lanes wait for one
     uint32_t aux_extra;           // extra aux-node steps per trip for the lanes whose next step is one
     uint32_t batch;               // k_wpath: round-queue entries a wave takes per pull (at most)
+    // k_wcoop's intake order (null: queue order): the round's work items by the pixels'
+    // remaining samples, most first (k_coop_order); `order_cur` = its 256 bucket cursors
+    uint32_t* order;
+    uint32_t* order_cur;
 };
+#define PT_ORDER_BUCKETS 256u
 
 // path engine geometry: PT_NQ query waves + 1 shade wave per workgroup; at most
 // PT_CMAX chains resident per workgroup (= the capacity of its ray ring).
@@ -146,25 +152,25 @@ struct WaveParams {
                                        // within 1 % of 3, all +8-10 % over 1)
 #define PT_AUX2 1u                     // extra aux-node steps per trip for the lanes whose next step is one
                                        // (+4.5 % at rank-of-1; 167 VGPRs)
-#ifndef PT_DEFER_ENDS
-#define PT_DEFER_ENDS 1                // k_wpath: the shade wave folds ended paths in batches of their own
-#endif
 #ifndef PT_END_MIN
-#define PT_END_MIN 64u                 // ... once this many wait (or nothing else is there to shade); 32 / 48
-                                       // measured +3.7 % / +5.6 %, 64 +6.2 % over folding in every shade batch
+#define PT_END_MIN 64u                 // k_wpath: the shade wave folds ended paths in batches of their own, once
+                                       // this many wait (or nothing else is there to shade); 32 / 48 measured
+                                       // +3.7 % / +5.6 %, 64 +6.2 % over folding in every shade batch
 #endif
 #define PT_PROBE_MIN 16u               // ... or whenever this many lanes wait for one
 #ifndef PT_CMAX
-#define PT_CMAX 512u
+#define PT_CMAX 384u                   // (512 until round 3; the LDS pixel table took the room)
 #endif
-// The rings and the query lanes' aux stacks live in LDS (4 workgroups per CU:
-// 40,768 B each of the CU's 163,840 B; pt_wave.hip static_asserts the fit):
-//   ray ring   PT_CMAX entries (52 B: ray, slot, plane t and prim, q_prep record)
-//   done rings PT_DQN entries per query wave (32 B: ray, slot, closest prim),
+// The rings, the query lanes' aux stacks and the resident chains' pixel records
+// live in LDS (4 workgroups per CU; pt_wave.hip static_asserts the fit):
+//   pixel table PT_CMAX entries (16 B: RNG, vertex count, samples done -- rec[2 slot]
+//              while the chain stays in the workgroup) and their free ring
+//   ray ring   PT_CMAX entries (54 B: ray, slot, plane t and prim, q_prep record, table entry)
+//   done rings PT_DQN entries per query wave (34 B: ray, slot, closest prim, table entry),
 //              flow-controlled (a finished query waits in its lane while its ring is full)
 //   aux stack  PT_LSTACK words per query lane; a query that would need more takes the
 //              exact DFS (none of 10^6 measured queries needed more than 11)
-#define PT_DQN 64u
+#define PT_DQN 48u                     // (64 until round 3; the LDS pixel table took the room)
 #define PT_LSTACK 16u                  // (+1 word per lane: the stack's trash word)
 
 // cooperative engine (k_wcoop, the end of a pass): one wave per chain, QC_WAVES
@@ -173,6 +179,10 @@ struct WaveParams {
 #define QC_WAVES 4u
 #endif
 #define QC_SCAP_MIN 128u           // aux stack words per team (the smallest; also the exact DFS stack)
+#ifndef QC_EPL
+#define QC_EPL 1u                  // aux entries a team lane tests per expansion round (nodes per round:
+                                   // QC_EPL x team / 4)
+#endif
 #define QC_FOLD 6u                 // fold records held in LDS per chain (deeper vertices: HBM fold records)
 #define QC_NPL 8u                  // plane records copied to LDS per workgroup (further planes: from HBM)
 #define QC_NEM 8u                  // emitter records copied to LDS per workgroup (further emitters: from HBM)
@@ -200,6 +210,9 @@ hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s);
 // sparse: the end-of-pass kernel (few chains: every step kind and several steps per trip)
 hipError_t pt_launch_path_round(pt::WaveParams p, uint32_t path_grid, uint32_t shade_grid, hipStream_t s, bool sparse,
                                 hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+// the cooperative engine's intake order (WaveParams::order): the round's n work items
+// counting-sorted by their pixels' remaining samples, most first
+hipError_t pt_launch_coop_order(pt::WaveParams p, uint32_t n, hipStream_t s);
 // cooperative engine: one launch runs every remaining chain of the pass to its end
 // team = lanes per chain (8 -- the default --, 16, 32 or 64)
 // big: the scene exceeds the LDS tables (QC_FOLD / QC_NPL / QC_NEM; team 8 or 64 then)

@@ -158,7 +158,8 @@ struct Query {
     uint32_t len : 7;           // walk: ancestor list length
     uint32_t nh : 4;            // hitting leaves in the list (<= PT_QHK)
     uint32_t ne : 4;            // ... of which the first ne are decided and entered (the recorded hits)
-    uint32_t spare : 23;        // (fills the word: a narrower unit is accessed bytewise, which keeps
+    uint32_t cid : 10;          // k_wpath: the chain's entry in its workgroup's LDS pixel table
+    uint32_t spare : 13;        // (fills the word: a narrower unit is accessed bytewise, which keeps
                                 //  the whole Query out of registers)
     uint32_t node;              // Q_AUX: aux node, or PT_LEAFQ | ordinal of the leaf being probed
     uint32_t lb;                // every hitting leaf below lb has been decided

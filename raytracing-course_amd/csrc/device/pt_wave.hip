@@ -28,24 +28,9 @@
 #include "pt_kernels.h"
 #include "pt_coop.h"
 #include "pt_query.h"
+#include "pt_wprof.h"
 
 namespace pt {
-
-#ifdef PT_WPROF
-// diagnostics builds: shader-clock stamp that no memory operation crosses
-__device__ __forceinline__ uint64_t pf_now() {
-    uint64_t t;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    return t;
-}
-#define PF_WAIT4(a) asm volatile("" ::"v"((a).x), "v"((a).y), "v"((a).z), "v"((a).w) : "memory")
-#define PF_ARGS , uint64_t* pf
-#define PF_PASS , pf
-#else
-#define PF_ARGS
-#define PF_PASS
-#endif
-
 
 // enqueue a fresh ray with its plane result (RayIntersection's plane loop)
 __device__ __forceinline__ void push_ray(const WaveParams& P, const RayQ& Q, uint32_t qi, const Ray& ray,
@@ -74,14 +59,8 @@ __device__ __forceinline__ Ray camera_sample(const CamView& cam, Rng& R, uint32_
 // `sdone` returns whether a sample of the pixel ended here.
 template <class EM>
 __device__ __forceinline__ bool shade_item(const WaveParams& P, const EM& em, uint32_t slot, Ray& ray, uint32_t hid,
-                                           bool& sdone PF_ARGS) {
+                                           bool& sdone) {
     bool emit = false;
-#ifdef PT_WPROF
-    uint64_t pt0 = pf_now();
-#define PF_MARK(i) do { const uint64_t n_ = pf_now(); pf[i] += n_ - pt0; pt0 = n_; } while (0)
-#else
-#define PF_MARK(i) (void)0
-#endif
     PixelHot hot = load_hot(P.st, slot);     // one 16-B load: RNG, vertex count, samples done
     uint32_t nv = hot.nv;
     uint32_t end = PE_LIVE;
@@ -93,11 +72,9 @@ __device__ __forceinline__ bool shade_item(const WaveParams& P, const EM& em, ui
         // (the query's own test, same operations -> same bits)
         Hit h;
         (void)prim_intersect(P.S.prims[hid], ray, h);
-        PF_MARK(0);   // pixel record + prim loads, the hit recomputed
         uint32_t idm;
         float s1, s2;
         const bool cont = shade_vertex_e(P.S, em, P.S.shade[hid], R, ray, h, (int)hid, idm, s1, s2);
-        PF_MARK(1);   // the vertex: material, sampling, pdfs
         HbmVStore vs = fold_store(P.st, slot);
         vs.put(nv, idm, s1, s2);
         ++nv;
@@ -119,7 +96,6 @@ __device__ __forceinline__ bool shade_item(const WaveParams& P, const EM& em, ui
         uint32_t pix;
         const f3 sum = load_sum_pix(P.st, slot, pix);
         store_sum(P.st, slot, sum + L, pix);   // src/scene.cpp:198 sum += RayTrace(...)
-        PF_MARK(2);   // backward fold + sum
         const uint32_t done = hot.done + 1u;
         hot.done = done;
         nv = 0u;
@@ -132,71 +108,8 @@ __device__ __forceinline__ bool shade_item(const WaveParams& P, const EM& em, ui
     hot.nv = nv;
     hot.R = R;
     store_hot(P.st, slot, hot);               // one 16-B store
-    PF_MARK(3);   // next sample's camera ray, record store
     return emit;
 }
-#undef PF_MARK
-
-#if PT_DEFER_ENDS
-// shade_item in two halves (the shade wave's deferred path ends): the vertex half
-// returns true with `ray` = the child ray, or false when the path ended (the miss,
-// or the vertex ends it) with the pixel record updated (RNG, vertex count) and
-// `miss` telling how; the end half -- the backward fold into the sum, the next
-// sample's camera ray -- runs later in a batch of ended paths (end_item).  The
-// pixel's operations and their order are shade_item's: a pixel has one chain, and
-// its next sample starts only from end_item.
-template <class EM>
-__device__ __forceinline__ bool vertex_item(const WaveParams& P, const EM& em, uint32_t slot, Ray& ray, uint32_t hid,
-                                            bool& miss) {
-    PixelHot hot = load_hot(P.st, slot);
-    uint32_t nv = hot.nv;
-    Rng R = hot.R;
-    bool live = false;
-    miss = hid == 0xffffffffu;
-    if (!miss) {
-        Hit h;
-        (void)prim_intersect(P.S.prims[hid], ray, h);
-        uint32_t idm;
-        float s1, s2;
-        const bool cont = shade_vertex_e(P.S, em, P.S.shade[hid], R, ray, h, (int)hid, idm, s1, s2);
-        HbmVStore vs = fold_store(P.st, slot);
-        vs.put(nv, idm, s1, s2);
-        ++nv;
-        live = cont && nv < P.depth;   // RayTrace(.., 0) = 0
-    }
-    hot.nv = nv;
-    hot.R = R;
-    store_hot(P.st, slot, hot);
-    return live;
-}
-// src/scene.cpp:198 sum += RayTrace(...), then the next sample's camera ray
-// (returns true with `ray` set) unless the pixel has reached the pass target
-__device__ __forceinline__ bool end_item(const WaveParams& P, uint32_t slot, bool miss, Ray& ray) {
-    PixelHot hot = load_hot(P.st, slot);
-    Rng R = hot.R;
-    f3 L = miss ? P.S.bg : mk3(0.f, 0.f, 0.f);
-    HbmVStore vs = fold_store(P.st, slot);
-    for (uint32_t k = hot.nv; k > 0u; --k) {
-        uint32_t idm;
-        float s1, s2;
-        vs.get(k - 1u, idm, s1, s2);
-        L = fold_vertex(P.S, L, idm, s1, s2);
-    }
-    uint32_t pix;
-    const f3 sum = load_sum_pix(P.st, slot, pix);
-    store_sum(P.st, slot, sum + L, pix);
-    hot.done += 1u;
-    hot.nv = 0u;
-    bool emit = false;
-    if (hot.done < P.target) {
-        ray = camera_sample(P.cam, R, pix % P.tm.W, pix / P.tm.W);
-        emit = true;
-    }
-    hot.R = R;
-    store_hot(P.st, slot, hot);
-    return emit;
-}
-#endif
 
 __global__ void __launch_bounds__(256) k_wcamera(WaveParams P) {
     // blocks append in about block order: the queue follows tile_order (Z-order of
@@ -302,6 +215,66 @@ __device__ __forceinline__ T lds_get(const T* a, uint32_t i) { return ((const PT
 template <class T>
 __device__ __forceinline__ void lds_put(T* a, uint32_t i, const T& v) { ((PT_LDS T*)a)[i] = v; }
 
+// The shade wave's halves of shade_item, with the pixel record in the workgroup's
+// LDS table (entry cid, PathLds::H) instead of HBM.  vertex_item: the vertex
+// (src/scene.cpp:91-177) and its fold record; true with `ray` = the child ray, or
+// false when the path ended (the miss, or the vertex ends it), `miss` telling how.
+// end_item: the backward fold into the sum (src/scene.cpp:198) and the next sample's
+// camera ray, run later in a batch of ended paths; false = the pixel reached the
+// pass target (its record is then written back to HBM).  A pixel has one chain, and
+// its next sample starts only from end_item, so its operations keep shade_item's order.
+template <class EM>
+__device__ __forceinline__ bool vertex_item(const WaveParams& P, const EM& em, uint4* H, uint32_t cid, uint32_t slot,
+                                            Ray& ray, uint32_t hid, bool& miss) {
+    PixelHot hot = hot_unpack(lds_get(H, cid));
+    uint32_t nv = hot.nv;
+    Rng R = hot.R;
+    bool live = false;
+    miss = hid == 0xffffffffu;
+    if (!miss) {
+        Hit h;
+        (void)prim_intersect(P.S.prims[hid], ray, h);
+        uint32_t idm;
+        float s1, s2;
+        const bool cont = shade_vertex_e(P.S, em, P.S.shade[hid], R, ray, h, (int)hid, idm, s1, s2);
+        HbmVStore vs = fold_store(P.st, slot);
+        vs.put(nv, idm, s1, s2);
+        ++nv;
+        live = cont && nv < P.depth;   // RayTrace(.., 0) = 0
+    }
+    hot.nv = nv;
+    hot.R = R;
+    lds_put(H, cid, hot_pack(hot));
+    return live;
+}
+__device__ __forceinline__ bool end_item(const WaveParams& P, uint4* H, uint32_t cid, uint32_t slot, bool miss,
+                                         Ray& ray) {
+    PixelHot hot = hot_unpack(lds_get(H, cid));
+    Rng R = hot.R;
+    f3 L = miss ? P.S.bg : mk3(0.f, 0.f, 0.f);
+    HbmVStore vs = fold_store(P.st, slot);
+    for (uint32_t k = hot.nv; k > 0u; --k) {
+        uint32_t idm;
+        float s1, s2;
+        vs.get(k - 1u, idm, s1, s2);
+        L = fold_vertex(P.S, L, idm, s1, s2);
+    }
+    uint32_t pix;
+    const f3 sum = load_sum_pix(P.st, slot, pix);
+    store_sum(P.st, slot, sum + L, pix);
+    hot.done += 1u;
+    hot.nv = 0u;
+    bool emit = false;
+    if (hot.done < P.target) {
+        ray = camera_sample(P.cam, R, pix % P.tm.W, pix / P.tm.W);
+        emit = true;
+    }
+    hot.R = R;
+    if (emit) lds_put(H, cid, hot_pack(hot));
+    else store_hot(P.st, slot, hot);   // the pixel leaves the workgroup
+    return emit;
+}
+
 // Rings: entries and positions in LDS, ordered by workgroup-scope release/acquire
 // fences.  Every ring has ONE producer, which publishes its entries in order, so a
 // consumer takes a contiguous range: the ray ring is written by the shade wave, and
@@ -313,21 +286,33 @@ struct PathLds {
     uint32_t rq_head;             // next ray-ring entry to take (query waves, CAS)
     uint32_t rq_tail;             // ray-ring entries published (shade wave)
     uint32_t resident;            // chains held by this workgroup
+    uint32_t leaked;              // chains handed to the exact DFS (their table entries stay taken)
     uint32_t qw_done;             // query waves that have left
+    uint32_t f_head;              // pixel-table entries taken from the free ring (query waves, atomic)
     uint32_t dq_tail[PT_NQ];      // done-ring entries published, per query wave
     uint32_t dq_head[PT_NQ];      // done-ring entries read by the shade wave (free space for the producer)
+    // The resident chains' pixel records (rec[2 slot]: RNG, vertex count, samples
+    // done): a chain takes an entry when it joins the workgroup (query wave intake)
+    // and its record lives here, not in HBM, until it leaves -- its pixel reaches the
+    // pass target (the shade wave writes it back and frees the entry), or the round
+    // ends or the exact DFS takes its ray (written back, the entry stays taken).
+    uint4 H[PT_CMAX];
+    uint16_t F[PT_CMAX];          // free entries (ring: taken at f_head, returned by the shade wave)
     F4 rq_ro[PT_CMAX];            // ray ring: {o.xyz, slot}
     F4 rq_rd[PT_CMAX];            //           {d.xyz, P}
     F4 rq_ri[PT_CMAX];            //           q_prep record
     int rq_pid[PT_CMAX];          //           closest plane
+    uint16_t rq_cid[PT_CMAX];     //           pixel-table entry
     F4 dq_ro[PT_NQ][PT_DQN];      // done rings: {o.xyz, slot}
     F4 dq_rd[PT_NQ][PT_DQN];      //             {d.xyz, u32 closest prim | 0xffffffff}
+    uint16_t dq_cid[PT_NQ][PT_DQN];   //         pixel-table entry
     uint32_t stk[(PT_LSTACK + 1u) * 64u * PT_NQ];   // query lanes' aux stacks, [word][lane] (+ a trash word)
-    // the shade wave's copies of the first planes and emitters (any further ones: HBM)
+    // the shade wave's copies of the first planes and emitters (any further ones: HBM);
+    // a plane's record carries its prim index in p2.w (unused by a plane)
     F4 pl[QC_NPL * 5u];
     F4 em[QC_NEM * 5u];
-    uint32_t pl_id[QC_NPL];
 };
+static_assert(PT_CMAX <= 1024u, "Query::cid is a 10-bit field");
 // k_wpath's occupancy (PT_PATH_WAVES_PER_EU waves per SIMD, 4 SIMDs per CU) assumes
 // that many workgroups fit the CU's 160 KB of LDS: a bigger ring, stack or table
 // would silently drop a workgroup per CU (every tuning number assumes 4)
@@ -339,10 +324,11 @@ struct PlanesPath {
     const SceneView& S;
     __device__ Prim operator()(uint32_t k, uint32_t& pi) const {
         if (k < QC_NPL) {
-            pi = lds_get(L.pl_id, k);
             Prim p;
             p.p0 = lds_get(L.pl, 5u * k); p.p1 = lds_get(L.pl, 5u * k + 1u); p.p2 = lds_get(L.pl, 5u * k + 2u);
             p.p3 = lds_get(L.pl, 5u * k + 3u); p.p4 = lds_get(L.pl, 5u * k + 4u);
+            pi = f2u(p.p2.w);
+            p.p2.w = 0.f;
             return p;
         }
         pi = S.planes[k];
@@ -407,32 +393,11 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     QCounts C{0u, 0u, 0u, 0u};
     // wave-level counters (scalar registers; per-lane ones would cost VGPRs)
     uint64_t rays = 0u, fallbacks = 0u, init_exact = 0u, planes = 0u;
-#ifdef PT_WPROF
-    uint64_t pf_trips = 0, pf_act = 0, pf_sleep = 0, pf_ring = 0, pf_pulled = 0, pf_exit_budget = 0, pf_res = 0,
-             pf_dq = 0, pf_rq = 0, pf_tripcyc = 0, pf_qlat = 0, pf_qn = 0, pf_qsteps = 0, pf_refillcyc = 0;
-    uint64_t pf_stepcyc = 0, pf_auxtrips = 0, pf_picktrips = 0, pf_stepped = 0, pf_donecyc = 0;
-    uint64_t pf_ldcyc = 0, pf_excyc = 0, pf_rfdata = 0, pf_rftrips = 0;
-#ifdef PT_QPROF
-    uint64_t pf_kind[6] = {0, 0, 0, 0, 0, 0}, pf_kindn[5] = {0, 0, 0, 0, 0};
-#endif
-    uint64_t pf_t0 = __builtin_amdgcn_s_memtime(), pf_qstart = 0;
-    uint32_t pf_qs = 0;
-#endif
+    QProf pf;                         // (diagnostics builds only: PT_WPROF)
     for (;;) {
         const unsigned long long idle = __ballot(!active);
         const uint32_t nidle = (uint32_t)__popcll(idle);
-#ifdef PT_WPROF
-        {
-            const uint64_t t = __builtin_amdgcn_s_memtime();
-            pf_tripcyc += t - pf_t0;
-            pf_t0 = t;
-        }
-        pf_trips++;
-        pf_act += 64u - nidle;
-        pf_res += lds_read(L.resident);
-        pf_dq += lds_read(L.dq_tail[wq]) - lds_read(L.dq_head[wq]);
-        pf_rq += lds_read(L.rq_tail) - lds_read(L.rq_head);
-#endif
+        pf.trip(nidle, L, wq);
         if (!exhausted && (++trip & 15u) == 0u) {
             // A wave whose lanes stay busy with its workgroup's chains does not pull,
             // so it would never find the round's work used up and would run its
@@ -455,12 +420,11 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                     uint32_t* tail = w + sizeof(Query) / 4u;
                     tail[0] = slot;
                     for (uint32_t j = 0; j < q.sp; ++j) tail[1u + j] = stk.get(j);
+                    P.st.rec[2u * slot] = lds_get(L.H, (uint32_t)q.cid);   // the chain leaves the workgroup
                 }
                 const uint32_t ns = (uint32_t)__popcll(__ballot(active));
                 if (lane_id() == 0u && ns) atomicSub(&L.resident, ns);
-#ifdef PT_WPROF
-                pf_exit_budget = 1;
-#endif
+                pf.exit_budget();
                 break;
             }
             if (nidle == 64u && lds_read(L.resident) == 0u) break;   // no chain left anywhere
@@ -491,14 +455,12 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 take = __builtin_amdgcn_readfirstlane(take);
                 if (!active && pos >= given && pos < given + take) { src = 2u; gi = (h + pos - given) % PT_CMAX; }
                 given += take;
-#ifdef PT_WPROF
-                pf_ring += take;
-#endif
+                pf.ring(take);
             }
             while (given < nidle && !exhausted) {
                 uint32_t v = PT_NOWORK, cnt = 0u;
                 if (lane_id() == 0u) {
-                    if (atomicAdd(&L.resident, bsz) + bsz > P.path_cap) {
+                    if (atomicAdd(&L.resident, bsz) + bsz + lds_read(L.leaked) > P.path_cap) {
                         atomicSub(&L.resident, bsz);   // workgroup full: its chains first
                         v = PT_CAPPED;
                     } else {
@@ -523,20 +485,27 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 if (v == PT_NOWORK) { exhausted = true; break; }
                 bbase = v;
                 bleft = cnt;
-#ifdef PT_WPROF
-                pf_pulled += cnt;
-#endif
+                pf.pulled(cnt);
                 const uint32_t take = nidle - given < bleft ? nidle - given : bleft;
                 if (!active && pos >= given && pos < given + take) { src = 1u; gi = bbase + pos - given; }
                 bbase += take;
                 bleft -= take;
                 given += take;
             }
-            if (src == 2u) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            // chains joining the workgroup (src 1: the round's work) take a pixel-table
+            // entry from the free ring (there are enough: the entries taken never exceed
+            // resident + leaked <= path_cap <= PT_CMAX); ray-ring chains bring theirs
+            const unsigned long long mjoin = __ballot(src == 1u);
+            uint32_t fh = 0u;
+            if (mjoin) {
+                if (lane_id() == 0u) fh = atomicAdd(&L.f_head, (uint32_t)__popcll(mjoin));
+                fh = __builtin_amdgcn_readfirstlane(fh);
+            }
+            if (src != 0u) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            uint32_t cid = 0u;
+            if (src == 1u) cid = lds_get(L.F, (fh + lanes_below(mjoin)) % PT_CMAX);
+            if (src == 2u) cid = lds_get(L.rq_cid, gi);
             bool took = false;   // a fresh ray (not a resumed query) started in this lane
-#ifdef PT_WPROF
-            const uint64_t pf_r0 = __ballot(src != 0u) ? pf_now() : 0;
-#endif
             if (src == 1u && gi < n_carry) {
                 // resume a suspended query: state, slot, then its aux stack into LDS
                 const uint32_t* w = CQ + (size_t)gi * P.carry_words;
@@ -544,6 +513,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 const uint32_t* tail = w + sizeof(Query) / 4u;
                 slot = tail[0];
                 for (uint32_t k = 0; k < q.sp; ++k) stk.set(k, tail[1u + k]);
+                lds_put(L.H, cid, P.st.rec[2u * slot]);   // its pixel record, for its stay here
                 active = true;
             } else if (src != 0u) {
                 // a fresh ray of the round, or a chain's next ray from the ray ring
@@ -561,45 +531,27 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                     pid = lds_get(L.rq_pid, gi);
                     pre = lds_get(L.rq_ri, gi);
                 }
-#ifdef PT_WPROF
-                PF_WAIT4(o); PF_WAIT4(d); PF_WAIT4(pre);
-#endif
                 Ray ray;
                 ray.o = mk3(o.x, o.y, o.z);
                 ray.d = mk3(d.x, d.y, d.z);
                 slot = f2u(o.w);
                 took = true;
-#ifdef PT_WPROF
-                pf_qstart = __builtin_amdgcn_s_memtime();
-                pf_qs = 0;
-#endif
+                pf.query_start();
                 q_init_pre(ray, d.w, pid, pre, q);
+                if (src == 1u) lds_put(L.H, cid, P.st.rec[2u * slot]);   // its pixel record, for its stay here
                 active = true;
             }
+            if (src != 0u) q.cid = cid;
             const uint32_t ntook = (uint32_t)__popcll(__ballot(took));
             rays += ntook;
             planes += (uint64_t)ntook * P.S.n_planes;
             init_exact += (uint32_t)__popcll(__ballot(took && q.phase == Q_EXACT));
-#ifdef PT_WPROF
-            if (pf_r0) {
-                pf_rfdata += pf_now() - pf_r0;
-                pf_rftrips++;
-            }
-#endif
         }
         if (__ballot(active) == 0ull) {
-#ifdef PT_WPROF
-            pf_sleep++;
-#endif
+            pf.sleep();
             __builtin_amdgcn_s_sleep(2);   // nothing to run: chains are being shaded (no `continue`:
         }                                  // a second back edge costs ~30 VGPRs)
-#ifdef PT_WPROF
-        pf_refillcyc += __builtin_amdgcn_s_memtime() - pf_t0;
-        if (active) pf_qs++;
-#endif
-#ifdef PT_WPROF
-        const uint64_t pf_s0 = __builtin_amdgcn_s_memtime();
-#endif
+        pf.refill_end(active);
         if constexpr (SPARSE) {
 #pragma unroll 1
             for (uint32_t it = 0; it < P.sparse_steps; ++it) {
@@ -630,63 +582,8 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
             const bool probe_go = turn || (uint32_t)__popcll(__ballot(want_probe)) >= P.probe_min;
             if (turn) ptrip = 0u;
             if (want_probe && !probe_go) kind = 7u;
-#ifdef PT_WPROF
-            if (__ballot(kind == 0u) != 0ull) pf_auxtrips++;
-            if (pick) pf_picktrips++;
-            pf_stepped += (uint64_t)__popcll(__ballot(kind == 0u || kind == pick));
-#endif
-#ifdef PT_WPROF
-            if (kind == 0u || kind == pick) {
-                const uint64_t ta = pf_now();
-                uint32_t off[8];
-                q_addr(P.S, q, off);
-                F4 r[8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) r[k] = blob_piece(P.S, off[k]);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) PF_WAIT4(r[k]);
-                const uint64_t tb = pf_now();
-#ifdef PT_QPROF_DEV
-                uint32_t qp[5] = {0u, 0u, 0u, 0u, 0u};
-                q_exec(P.S, q, C, stk, r, qp);
-#else
-                q_exec(P.S, q, C, stk, r);
-#endif
-                const uint64_t tc = pf_now();
-                pf_ldcyc += tb - ta;
-                pf_excyc += tc - tb;
-#ifdef PT_QPROF_DEV
-                {
-                    // each kind's stamp (wave max), then durations in program order
-                    uint32_t ts[6];
-#pragma unroll
-                    for (int i = 0; i < 5; ++i) {
-                        uint32_t v = qp[i];
-                        for (int off = 32; off >= 1; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off, 64));
-                        ts[i] = __builtin_amdgcn_readfirstlane(v);
-                    }
-                    // (the compiler lays the kinds' blocks out in its own order: each executed
-                    // kind runs until the next later stamp, or the end of the step)
-                    const uint32_t t0 = (uint32_t)tb, t1 = (uint32_t)tc;
-                    uint32_t first = t1;
-#pragma unroll
-                    for (int i = 0; i < 5; ++i) {
-                        if (ts[i] == 0u) continue;
-                        uint32_t nx = t1;
-#pragma unroll
-                        for (int j = 0; j < 5; ++j)
-                            if (ts[j] != 0u && ts[j] - t0 > ts[i] - t0 && ts[j] - t0 < nx - t0) nx = ts[j];
-                        pf_kind[i] += nx - ts[i];
-                        pf_kindn[i]++;
-                        if (ts[i] - t0 < first - t0) first = ts[i];
-                    }
-                    pf_kind[5] += first - t0;   // before the first kind's stamp
-                }
-#endif
-            }
-#else
+            pf.kinds(kind == 0u, pick != 0u, kind == 0u || kind == pick);
             if (kind == 0u || kind == pick) q_step(P.S, q, C, stk);
-#endif
             // aux_extra more aux-node steps in the same trip for the lanes whose next step is one
 #pragma unroll 1
             for (uint32_t x = 0; x < P.aux_extra; ++x) {
@@ -695,10 +592,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 if (a2) q_aux_step(P.S, q, C, stk);
             }
         }
-#ifdef PT_WPROF
-        const uint64_t pf_s1 = __builtin_amdgcn_s_memtime();
-        pf_stepcyc += pf_s1 - pf_s0;
-#endif
+        pf.step_end();
         // finished queries -> this wave's done ring, in lane order, as far as it has room
         // (the shade wave recomputes t, n and side from the prim); the others wait in
         // their lanes (phase Q_DONE) for the next trip
@@ -716,19 +610,16 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 lds_put(&L.dq_ro[0][0], j, F4{q.ray.o.x, q.ray.o.y, q.ray.o.z, u2f(slot)});
                 lds_put(&L.dq_rd[0][0], j,
                         F4{q.ray.d.x, q.ray.d.y, q.ray.d.z, u2f(q.res_id < 0 ? 0xffffffffu : (uint32_t)q.res_id)});
+                lds_put(&L.dq_cid[0][0], j, (uint16_t)q.cid);
                 active = false;
-#ifdef PT_WPROF
-                if (pf_qstart) {
-                    pf_qlat += __builtin_amdgcn_s_memtime() - pf_qstart;
-                    pf_qn++;
-                    pf_qsteps += pf_qs;
-                }
-#endif
+                pf.query_done();
             } else if (q.phase == Q_EXACT) {
                 // rare: the exact stack DFS after this kernel; the chain leaves the workgroup
                 const uint32_t k = atomicAdd(out + C_EXACT, 1u);
                 P.ex.ro[k] = F4{q.ray.o.x, q.ray.o.y, q.ray.o.z, u2f(slot)};
                 P.ex.rd[k] = F4{q.ray.d.x, q.ray.d.y, q.ray.d.z, u2f(k)};
+                P.st.rec[2u * slot] = lds_get(L.H, (uint32_t)q.cid);   // (k_wshade shades it from HBM)
+                atomicAdd(&L.leaked, 1u);   // (its table entry stays taken for the round)
                 atomicSub(&L.resident, 1u);
                 active = false;
             }
@@ -737,9 +628,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane_id() == 0u) lds_write(L.dq_tail[wq], dq_res);
         }
-#ifdef PT_WPROF
-        pf_donecyc += __builtin_amdgcn_s_memtime() - pf_s1;
-#endif
+        pf.done_end();
     }
     unsigned long long* ctr = ctr_copy(P.counters);
     wave_add_u64(ctr + 1, C.nodes);
@@ -751,42 +640,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
         if (fallbacks) atomicAdd(ctr + 6, (unsigned long long)fallbacks);
         if (init_exact) atomicAdd(ctr + 7, (unsigned long long)init_exact);
     }
-#ifdef PT_WPROF
-    if (P.wg_prof && lane_id() == 0u) {
-        unsigned long long* w = P.wg_prof + 64ull * blockIdx.x;
-        atomicAdd(w + 2, pf_trips);
-        atomicAdd(w + 3, pf_act);
-        atomicAdd(w + 4, pf_sleep);
-        atomicAdd(w + 5, pf_ring);
-        atomicAdd(w + 6, (unsigned long long)rays);
-        atomicAdd(w + 11, pf_pulled);
-        atomicAdd(w + 12, pf_exit_budget);
-        atomicAdd(w + 13, pf_res);
-        atomicAdd(w + 14, pf_dq);
-        atomicAdd(w + 15, pf_rq);
-        atomicAdd(w + 16, pf_tripcyc);
-        atomicAdd(w + 21, pf_refillcyc);
-        atomicAdd(w + 22, pf_stepcyc);
-        atomicAdd(w + 23, pf_auxtrips);
-        atomicAdd(w + 24, pf_picktrips);
-        atomicAdd(w + 25, pf_stepped);
-        atomicAdd(w + 26, pf_donecyc);
-        atomicAdd(w + 32, pf_ldcyc);
-        atomicAdd(w + 33, pf_excyc);
-        atomicAdd(w + 34, pf_rfdata);
-        atomicAdd(w + 35, pf_rftrips);
-#ifdef PT_QPROF
-        for (int i = 0; i < 6; ++i) atomicAdd(w + 48 + i, pf_kind[i]);
-        for (int i = 0; i < 5; ++i) atomicAdd(w + 54 + i, pf_kindn[i]);
-#endif
-    }
-    if (P.wg_prof) {
-        unsigned long long* w = P.wg_prof + 64ull * blockIdx.x;
-        wave_add_u64(w + 17, pf_qlat);
-        wave_add_u64(w + 18, pf_qn);
-        wave_add_u64(w + 19, pf_qsteps);
-    }
-#endif
+    pf.store(P.wg_prof, rays);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane_id() == 0u) atomicAdd(&L.qw_done, 1u);
 }
@@ -799,16 +653,12 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
 #pragma unroll
     for (uint32_t w = 0; w < PT_NQ; ++w) head[w] = 0u;
     uint32_t tail = 0u;               // ray ring published
-#ifdef PT_WPROF
-    uint64_t pf_batches = 0, pf_items = 0, pf_spin = 0, pf_cyc = 0, pf_shc = 0, pf_pushc = 0, pf_rdc = 0;
-    uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // shade_item phases
-#endif
+    uint32_t f_tail = PT_CMAX;        // pixel-table free ring: entries returned (this wave only)
+    SProf pf;                         // (diagnostics builds only: PT_WPROF)
     uint32_t prog = 0u;               // finished samples not yet added to P.progress
-#if PT_DEFER_ENDS
-    // ended paths waiting for their fold (this wave's own queue: slot | miss << 31)
-    uint32_t* endq = P.endq + (size_t)blockIdx.x * PT_CMAX;
+    // ended paths waiting for their fold (this wave's own queue: {slot | miss << 31, table entry})
+    uint2* endq = P.endq + (size_t)blockIdx.x * PT_CMAX;
     uint32_t e_head = 0u, e_tail = 0u;
-#endif
     for (;;) {
         // published entries of the done rings (ring indices are compile-time: no scratch)
         uint32_t av[PT_NQ], total = 0u;
@@ -818,27 +668,23 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
             total += av[w];
         }
         Ray ray;
-        uint32_t slot = 0u;
+        uint32_t slot = 0u, cid = 0u;
         bool emit = false, sdone = false, have = false;
-#ifdef PT_WPROF
-        uint64_t c0 = __builtin_amdgcn_s_memtime(), c2 = c0;
-#endif
-#if PT_DEFER_ENDS
+        pf.begin();
         const uint32_t pend = e_tail - e_head;
         if (pend >= PT_END_MIN || (total == 0u && pend > 0u)) {
             // a batch of ended paths: folds, sums, the next samples' camera rays
             const uint32_t n = pend < 64u ? pend : 64u;
             have = lane < n;
             if (have) {
-                const uint32_t v = endq[(e_head + lane) % PT_CMAX];
-                slot = v & 0x7fffffffu;
-                emit = end_item(P, slot, (v >> 31) != 0u, ray);
+                const uint2 v = endq[(e_head + lane) % PT_CMAX];
+                slot = v.x & 0x7fffffffu;
+                cid = v.y;
+                emit = end_item(P, L.H, cid, slot, (v.x >> 31) != 0u, ray);
                 sdone = true;
             }
             e_head += n;
-        } else
-#endif
-        if (total == 0u) {
+        } else if (total == 0u) {
             if (lds_read(L.qw_done) == PT_NQ) {
                 // every query wave has left (and published): one more look, then done
                 uint32_t left = 0u;
@@ -847,88 +693,62 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
                 if (__builtin_amdgcn_readfirstlane(left) == 0u) break;   // (no ended path waits: see above)
                 continue;
             }
-#ifdef PT_WPROF
-            pf_spin++;
-#endif
+            pf.spin();
             __builtin_amdgcn_s_sleep(1);
             continue;
         } else {
-        // up to 64 of them: a fair share of each ring first (a full ring holds back its
-        // producer's finished queries), then the rest in ring order
-        uint32_t take[PT_NQ], n = 0u;
+            // up to 64 of them: a fair share of each ring first (a full ring holds back its
+            // producer's finished queries), then the rest in ring order
+            uint32_t take[PT_NQ], n = 0u;
 #pragma unroll
-        for (uint32_t w = 0; w < PT_NQ; ++w) {
-            take[w] = av[w] < 64u / PT_NQ ? av[w] : 64u / PT_NQ;
-            n += take[w];
-        }
+            for (uint32_t w = 0; w < PT_NQ; ++w) {
+                take[w] = av[w] < 64u / PT_NQ ? av[w] : 64u / PT_NQ;
+                n += take[w];
+            }
 #pragma unroll
-        for (uint32_t w = 0; w < PT_NQ; ++w) {
-            const uint32_t x = av[w] - take[w] < 64u - n ? av[w] - take[w] : 64u - n;
-            take[w] += x;
-            n += x;
-        }
-#ifdef PT_WPROF
-        c0 = __builtin_amdgcn_s_memtime();
-        pf_batches++;
-        pf_items += n;
-#endif
-        // this lane's entry: ring w, position head[w] + (lane - entries of the rings before w)
-        uint32_t j = 0u, before = 0u;
+            for (uint32_t w = 0; w < PT_NQ; ++w) {
+                const uint32_t x = av[w] - take[w] < 64u - n ? av[w] - take[w] : 64u - n;
+                take[w] += x;
+                n += x;
+            }
+            pf.batch(n);
+            // this lane's entry: ring w, position head[w] + (lane - entries of the rings before w)
+            uint32_t j = 0u, before = 0u;
 #pragma unroll
-        for (uint32_t w = 0; w < PT_NQ; ++w) {
-            if (lane >= before && lane < before + take[w]) j = w * PT_DQN + (head[w] + lane - before) % PT_DQN;
-            before += take[w];
-        }
+            for (uint32_t w = 0; w < PT_NQ; ++w) {
+                if (lane >= before && lane < before + take[w]) j = w * PT_DQN + (head[w] + lane - before) % PT_DQN;
+                before += take[w];
+            }
 #pragma unroll
-        for (uint32_t w = 0; w < PT_NQ; ++w) head[w] += take[w];
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        have = lane < n;
-        F4 o = F4{0.f, 0.f, 0.f, 0.f}, d = o;
-        if (have) {
-            o = lds_get(&L.dq_ro[0][0], j);
-            d = lds_get(&L.dq_rd[0][0], j);
-        }
-        // the entries are in registers: their slots go back to the producers
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            for (uint32_t w = 0; w < PT_NQ; ++w) head[w] += take[w];
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            have = lane < n;
+            F4 o = F4{0.f, 0.f, 0.f, 0.f}, d = o;
+            if (have) {
+                o = lds_get(&L.dq_ro[0][0], j);
+                d = lds_get(&L.dq_rd[0][0], j);
+                cid = lds_get(&L.dq_cid[0][0], j);
+            }
+            // the entries are in registers: their slots go back to the producers
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 #pragma unroll
-        for (uint32_t w = 0; w < PT_NQ; ++w)
-            if (lane == w) lds_write(L.dq_head[w], head[w]);
-#ifdef PT_WPROF
-        const uint64_t c1 = __builtin_amdgcn_s_memtime();
-#endif
-        if (have) {
-#ifdef PT_WPROF
-            PF_WAIT4(o); PF_WAIT4(d);
-            pf_rdc += pf_now() - c1;
-#endif
-            slot = f2u(o.w);
-            ray.o = mk3(o.x, o.y, o.z);
-            ray.d = mk3(d.x, d.y, d.z);
-#if PT_DEFER_ENDS
-            bool miss;
-            emit = vertex_item(P, EmitPath{L, P.S}, slot, ray, f2u(d.w), miss);
-            const bool ended = !emit;
-#else
-            emit = shade_item(P, EmitPath{L, P.S}, slot, ray, f2u(d.w), sdone PF_PASS);
-#endif
-#if PT_DEFER_ENDS
-            // (appended below, in lane order)
-            if (ended) slot |= miss ? 0x80000000u : 0u;
-#endif
-        }
-#if PT_DEFER_ENDS
-        {
+            for (uint32_t w = 0; w < PT_NQ; ++w)
+                if (lane == w) lds_write(L.dq_head[w], head[w]);
+            pf.read_done();
+            bool miss = false;
+            if (have) {
+                slot = f2u(o.w);
+                ray.o = mk3(o.x, o.y, o.z);
+                ray.d = mk3(d.x, d.y, d.z);
+                emit = vertex_item(P, EmitPath{L, P.S}, L.H, cid, slot, ray, f2u(d.w), miss);
+            }
+            // ended paths wait for a fold batch of their own (appended in lane order)
             const bool ended = have && !emit;
             const unsigned long long me = __ballot(ended);
-            if (ended) endq[(e_tail + lanes_below(me)) % PT_CMAX] = slot;
+            if (ended) endq[(e_tail + lanes_below(me)) % PT_CMAX] = make_uint2(slot | (miss ? 0x80000000u : 0u), cid);
             e_tail += (uint32_t)__popcll(me);
             have = have && emit;   // (an ended path is not gone: its pixel waits for the fold)
-        }
-#endif
-#ifdef PT_WPROF
-        c2 = __builtin_amdgcn_s_memtime();
-        pf_shc += c2 - c1;
-#endif
+            pf.shaded();
         }
         // finished samples for the host's progress bar: a system-scope add per ~4 k
         prog += (uint32_t)__popcll(__ballot(sdone));
@@ -938,11 +758,20 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
         }
         const bool flush = __builtin_amdgcn_readfirstlane(lds_read(L.qw_done)) == PT_NQ;
         const unsigned long long me = __ballot(emit);
-        uint32_t gone = (uint32_t)__popcll(__ballot(have && !emit));   // pixels done with this pass
+        // pixels done with this pass (end_item wrote their records back): their table entries are free
+        const bool fin = have && !emit;
+        const unsigned long long mf = __ballot(fin);
+        uint32_t gone = (uint32_t)__popcll(mf);
+        if (fin) lds_put(L.F, (f_tail + lanes_below(mf)) % PT_CMAX, (uint16_t)cid);
+        f_tail += gone;
         if (flush) {
-            // no query wave left to take it: the next round's fresh queue
+            // no query wave left to take it: the next round's fresh queue (the chain leaves
+            // the workgroup with its pixel record)
             const uint32_t k = wave_append(out + C_FRESH, emit);
-            if (emit) push_ray(P, N, k, ray, slot);
+            if (emit) {
+                push_ray(P, N, k, ray, slot);
+                P.st.rec[2u * slot] = lds_get(L.H, cid);
+            }
             gone += (uint32_t)__popcll(me);
         } else {
             if (emit) {
@@ -955,36 +784,22 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
                 lds_put(L.rq_rd, e, F4{ray.d.x, ray.d.y, ray.d.z, pt});
                 lds_put(L.rq_pid, e, pid);
                 lds_put(L.rq_ri, e, q_prep(P.S, ray));
+                lds_put(L.rq_cid, e, (uint16_t)cid);
             }
             tail += (uint32_t)__popcll(me);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0u) lds_write(L.rq_tail, tail);
         }
+        // (the freed table entries are written before the decrement that lets a query wave take them)
+        if (gone) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0u && gone) atomicSub(&L.resident, gone);
-#ifdef PT_WPROF
-        const uint64_t c3 = __builtin_amdgcn_s_memtime();
-        pf_pushc += c3 - c2;
-        pf_cyc += c3 - c0;
-#endif
+        pf.end();
     }
-#ifdef PT_WPROF
-    if (P.wg_prof && lane == 0u) {
-        unsigned long long* w = P.wg_prof + 64ull * blockIdx.x;
-        w[7] = pf_batches;
-        w[8] = pf_items;
-        w[9] = pf_spin;
-        w[10] = pf_cyc;
-        w[27] = pf_shc;
-        w[28] = pf_pushc;
-        w[36] = pf_rdc;
-        for (int i = 0; i < 8; ++i) w[40 + i] = pf[i];
-
-        w[1] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
+    pf.store(P.wg_prof);
     if (P.progress && prog && lane == 0u)
         __hip_atomic_fetch_add(P.progress, (unsigned long long)prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    // the ray ring's leftovers (no query wave takes from it any more) -> next round
+    // the ray ring's leftovers (no query wave takes from it any more) -> next round, with
+    // their pixel records
     const uint32_t h = lds_read(L.rq_head);
     for (uint32_t b = h; b < tail; b += 64u) {
         const uint32_t i = b + lane;
@@ -993,10 +808,12 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
         const uint32_t k = wave_append(out + C_FRESH, has);
         if (has) {
             const uint32_t e = i % PT_CMAX;
-            N.ro[k] = lds_get(L.rq_ro, e);
+            const F4 ro = lds_get(L.rq_ro, e);
+            N.ro[k] = ro;
             N.rd[k] = lds_get(L.rq_rd, e);
             N.pid[k] = lds_get(L.rq_pid, e);
             N.ri[k] = lds_get(L.rq_ri, e);
+            P.st.rec[2u * f2u(ro.w)] = lds_get(L.H, (uint32_t)lds_get(L.rq_cid, e));
         }
     }
 }
@@ -1008,19 +825,21 @@ __global__ void __launch_bounds__(PT_PATH_WG) __attribute__((amdgpu_waves_per_eu
         // the first planes and emitters (the shade wave's plane tests and light sampling)
         const uint32_t npl = (P.S.n_planes < QC_NPL ? P.S.n_planes : QC_NPL) * 5u;
         const uint32_t nem = (P.S.n_emitters < QC_NEM ? P.S.n_emitters : QC_NEM) * 5u;
-        for (uint32_t i = threadIdx.x; i < npl; i += blockDim.x)
-            lds_put(L.pl, i, reinterpret_cast<const F4*>(P.S.prims + P.S.planes[i / 5u])[i % 5u]);
+        for (uint32_t i = threadIdx.x; i < npl; i += blockDim.x) {
+            const uint32_t pi = P.S.planes[i / 5u];
+            F4 v = reinterpret_cast<const F4*>(P.S.prims + pi)[i % 5u];
+            if (i % 5u == 2u) v.w = u2f(pi);
+            lds_put(L.pl, i, v);
+        }
         for (uint32_t i = threadIdx.x; i < nem; i += blockDim.x)
             lds_put(L.em, i, reinterpret_cast<const F4*>(P.S.prims + P.S.emitters[i / 5u])[i % 5u]);
-        if (threadIdx.x < npl / 5u) lds_put(L.pl_id, threadIdx.x, P.S.planes[threadIdx.x]);
     }
     if (threadIdx.x == 0u) {
-        L.rq_head = L.rq_tail = L.resident = L.qw_done = 0u;
+        L.rq_head = L.rq_tail = L.resident = L.qw_done = L.leaked = L.f_head = 0u;
     }
     if (threadIdx.x < PT_NQ) L.dq_tail[threadIdx.x] = L.dq_head[threadIdx.x] = 0u;
-#ifdef PT_WPROF
-    if (P.wg_prof && threadIdx.x == 0u) P.wg_prof[64ull * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-#endif
+    for (uint32_t i = threadIdx.x; i < PT_CMAX; i += blockDim.x) lds_put(L.F, i, (uint16_t)i);   // every entry free
+    wprof_start(P.wg_prof);
     __syncthreads();
     // waves 0 .. PT_NQ-1 query, wave PT_NQ shades
     const uint32_t wave = threadIdx.x >> 6;
@@ -1055,6 +874,8 @@ struct QcTeamLds {
     uint32_t r_idx[HCAP], r_t[HCAP];   // entered hits so far (preorder)
     Shade fold_sh[QC_FOLD];        // the chain's fold records: the vertex prim's shading record ...
     uint4 fold[QC_FOLD];           // ... and {idm, s1, s2, -}
+    uint4 sum;                     // the pixel's sum.rgb and global index (rec[2 slot + 1]) while the team
+                                   // owns it (touched at path ends only: registers would spill)
 };
 // per workgroup: the records every chain cycle reads, copied once per launch
 struct QcScene {
@@ -1198,38 +1019,47 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
         if (__ballot(expand) == 0ull) break;
         uint32_t k = slim > ns ? (slim - ns) / 3u : 0u;
         k = k < 1u ? 1u : k;
-        // 1. breadth-first expansion of the wide aux BVH: one node per PT_AUXW team
-        //    lanes, a lane per entry (a round's instructions test one entry, not PT_AUXW)
-        constexpr uint32_t KN = T / PT_AUXW;
+        // 1. breadth-first expansion of the wide aux BVH: QC_EPL nodes per PT_AUXW team
+        //    lanes, a lane per entry of each (a round's instructions test QC_EPL entries,
+        //    their loads issued together: the round's latency is one load's)
+        constexpr uint32_t KN = T / PT_AUXW * QC_EPL;
         k = k > KN ? KN : k;
         k = k > ns ? ns : k;
         if (!expand) k = 0u;
         if (ns + 3u * k > SCAP) { ovf = true; k = 0u; }   // cannot happen with the host's reserve (checked)
         ns -= k;
         {
-            const uint32_t ni = tl / PT_AUXW, e = tl % PT_AUXW;
-            const bool act = ni < k;
-            const uint32_t node = act ? L.stk[ns + ni] : 0u;
-            C.aux += act && e == 0u ? 1u : 0u;
-            F4 ea, eb;
-            if (node < QC_TOPN) {
-                ea = Q.top[node * PT_AUXW + e].a;
-                eb = Q.top[node * PT_AUXW + e].b;
-            } else {
-                const uint32_t b = S.o_aux + (node * PT_AUXW + e) * (uint32_t)sizeof(AuxSL);
-                ea = blob_piece(S, b);
-                eb = blob_piece(S, b + 16u);
+            const uint32_t e = tl % PT_AUXW;
+            F4 ea[QC_EPL], eb[QC_EPL];
+            bool act[QC_EPL];
+#pragma unroll
+            for (uint32_t j = 0; j < QC_EPL; ++j) {
+                const uint32_t ni = tl / PT_AUXW + j * (T / PT_AUXW);
+                act[j] = ni < k;
+                const uint32_t node = act[j] ? L.stk[ns + ni] : 0u;
+                C.aux += act[j] && e == 0u ? 1u : 0u;
+                if (node < QC_TOPN) {
+                    ea[j] = Q.top[node * PT_AUXW + e].a;
+                    eb[j] = Q.top[node * PT_AUXW + e].b;
+                } else {
+                    const uint32_t b = S.o_aux + (node * PT_AUXW + e) * (uint32_t)sizeof(AuxSL);
+                    ea[j] = blob_piece(S, b);
+                    eb[j] = blob_piece(S, b + 16u);
+                }
             }
-            const uint32_t code = f2u(eb.w);
-            bool h = act && code != 0xffffffffu;
-            if (h) h = aux_entry_hit(ea, eb, ray, inv, oinv, pre.w);
-            const bool leaf = h && (code & 0x80000000u) != 0u;
-            const bool inner = h && (code & 0x80000000u) == 0u;
-            const unsigned long long mi = __ballot(inner) & tmask, ml = __ballot(leaf) & tmask;
-            if (inner) L.stk[ns + lanes_below(mi)] = code;
-            if (leaf) L.cand[nc + lanes_below(ml)] = code & 0x7fffffffu;
-            ns += (uint32_t)__popcll(mi);
-            nc += (uint32_t)__popcll(ml);
+#pragma unroll
+            for (uint32_t j = 0; j < QC_EPL; ++j) {
+                const uint32_t code = f2u(eb[j].w);
+                bool h = act[j] && code != 0xffffffffu;
+                if (h) h = aux_entry_hit(ea[j], eb[j], ray, inv, oinv, pre.w);
+                const bool leaf = h && (code & 0x80000000u) != 0u;
+                const bool inner = h && (code & 0x80000000u) == 0u;
+                const unsigned long long mi = __ballot(inner) & tmask, ml = __ballot(leaf) & tmask;
+                if (inner) L.stk[ns + lanes_below(mi)] = code;
+                if (leaf) L.cand[nc + lanes_below(ml)] = code & 0x7fffffffu;
+                ns += (uint32_t)__popcll(mi);
+                nc += (uint32_t)__popcll(ml);
+            }
         }
     }
     QC_TICK(0);
@@ -1343,12 +1173,11 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
     return on ? res : -1;
 }
 
-// the chain's pixel state while a team owns it (its first lane's registers)
+// the chain's pixel state while a team owns it (its first lane's registers; the sum
+// and the global pixel index in the team's LDS, QcTeamLds::sum)
 struct CoopPixel {
     Rng R;
     uint32_t nv, done;
-    f3 sum;
-    uint32_t pix;   // global pixel index y*W + x
 };
 
 // shade_item for the cooperative engine (a team's first lane): the same vertex /
@@ -1391,11 +1220,13 @@ __device__ __forceinline__ bool coop_shade(const WaveParams& P, const QcScene& Q
                 Lr = fold_vertex_sh(P.S.shade[f.x & 0x3fffffffu], Lr, f.x, u2f(f.y), u2f(f.z));
             }
         }
-        px.sum = px.sum + Lr;
+        const uint4 sp = L.sum;
+        const f3 sum = mk3(u2f(sp.x), u2f(sp.y), u2f(sp.z)) + Lr;   // src/scene.cpp:198 sum += ...
+        L.sum = make_uint4(f2u(sum.x), f2u(sum.y), f2u(sum.z), sp.w);
         px.done += 1u;
         px.nv = 0u;
         if (px.done < P.target) {
-            ray = camera_sample(P.cam, px.R, px.pix % P.tm.W, px.pix / P.tm.W);
+            ray = camera_sample(P.cam, px.R, sp.w % P.tm.W, sp.w / P.tm.W);
             emit = true;
         }
     }
@@ -1453,8 +1284,6 @@ k_wcoop(WaveParams P) {
     px.R.saved = 0.f;
     px.R.saved_ok = 0u;
     px.nv = px.done = 0u;
-    px.sum = mk3(0.f, 0.f, 0.f);
-    px.pix = 0u;
     for (;;) {
         // teams without a chain take the next one (queue order: carry, then fresh)
         const bool need = !have && !exhausted;
@@ -1465,6 +1294,7 @@ k_wcoop(WaveParams P) {
                 if (gi >= n_total) {
                     exhausted = true;
                 } else {
+                    if (P.order) gi = P.order[gi];   // the pixels furthest from the target first
                     have = true;
 #ifdef PT_CPROF
                     if (tl == 0u) cp[6]++;
@@ -1494,7 +1324,7 @@ k_wcoop(WaveParams P) {
                     px.R = hot.R;
                     px.nv = hot.nv;
                     px.done = hot.done;
-                    px.sum = load_sum_pix(P.st, slot, px.pix);
+                    if (tl == 0u) L.sum = P.st.rec[2u * slot + 1u];
                     if (tl < hot.nv && (!BIG || tl < QC_FOLD)) {
                         // the current path's vertices so far (written by the path engine; any
                         // beyond QC_FOLD stay in HBM)
@@ -1545,7 +1375,7 @@ k_wcoop(WaveParams P) {
                 hot.nv = px.nv;
                 hot.done = px.done;
                 store_hot(P.st, slot, hot);
-                store_sum(P.st, slot, px.sum, px.pix);
+                P.st.rec[2u * slot + 1u] = L.sum;
             }
             have = false;
         }
@@ -1594,6 +1424,50 @@ k_wcoop(WaveParams P) {
 #endif
 }
 
+// The cooperative engine's intake order.  Its launch runs until the pixel with the
+// most work left reaches the pass target, and a chain keeps its team to the end, so
+// with more chains than teams (a hand-over at 49 k chains, 24.6 k resident teams
+// of 8) the chains that wait for a team must be the ones with the least left.  A
+// counting sort of the round's work items (suspended queries, then fresh rays) by
+// their pixels' remaining samples, in PT_ORDER_BUCKETS buckets, most first.
+__device__ __forceinline__ uint32_t coop_order_bucket(const WaveParams& P, uint32_t gi, uint32_t n_carry) {
+    const uint32_t slot = gi < n_carry ? P.cq[P.parity][(size_t)gi * P.carry_words + sizeof(Query) / 4u]
+                                       : f2u(P.fq[P.parity].ro[gi - n_carry].w);
+    const uint32_t done = P.st.rec[2u * slot].w;
+    const uint32_t rem = done < P.target ? P.target - done : 0u;
+    const uint64_t b = (uint64_t)rem * PT_ORDER_BUCKETS / ((uint64_t)P.target + 1u);
+    return PT_ORDER_BUCKETS - 1u - (uint32_t)b;   // bucket 0 = the most samples left
+}
+__global__ void __launch_bounds__(256) k_coop_hist(WaveParams P) {
+    __shared__ uint32_t h[PT_ORDER_BUCKETS];
+    const uint32_t* in = P.ctl + PT_CTL_SET * P.parity;
+    const uint32_t n_carry = in[C_CARRY], n = in[C_FRESH] + n_carry;
+    h[threadIdx.x] = 0u;
+    __syncthreads();
+    for (uint32_t gi = blockIdx.x * 256u + threadIdx.x; gi < n; gi += gridDim.x * 256u)
+        atomicAdd(&h[coop_order_bucket(P, gi, n_carry)], 1u);
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(P.order_cur + PT_ORDER_BUCKETS + threadIdx.x, h[threadIdx.x]);
+}
+__global__ void __launch_bounds__(256) k_coop_scatter(WaveParams P) {
+    __shared__ uint32_t base[PT_ORDER_BUCKETS];
+    const uint32_t* in = P.ctl + PT_CTL_SET * P.parity;
+    const uint32_t n_carry = in[C_CARRY], n = in[C_FRESH] + n_carry;
+    if (threadIdx.x == 0u) {
+        // (every block scans the 256 counts itself)
+        uint32_t t = 0u;
+        for (uint32_t b = 0; b < PT_ORDER_BUCKETS; ++b) {
+            base[b] = t;
+            t += P.order_cur[PT_ORDER_BUCKETS + b];
+        }
+    }
+    __syncthreads();
+    for (uint32_t gi = blockIdx.x * 256u + threadIdx.x; gi < n; gi += gridDim.x * 256u) {
+        const uint32_t b = coop_order_bucket(P, gi, n_carry);
+        P.order[base[b] + atomicAdd(P.order_cur + b, 1u)] = gi;
+    }
+}
+
 // The rays the path engine hands back (Q_EXACT: an aux stack deeper than the
 // engine's LDS stack, a hitting-leaf list full of entered hits, non-finite
 // components); 64-lane workgroups, one ray per lane, stack in LDS.  The replay
@@ -1634,9 +1508,6 @@ __global__ void __launch_bounds__(64) k_wexact(WaveParams P) {
 
 __global__ void __launch_bounds__(256) k_wshade(WaveParams P) {
     __shared__ uint32_t agg[5];
-#ifdef PT_WPROF
-    uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
     uint32_t* out = P.ctl + PT_CTL_SET * (1u - P.parity);
     // the exact-DFS results of this round (the path engine shades everything else itself)
     const uint32_t n = out[C_EXACT];
@@ -1654,7 +1525,7 @@ __global__ void __launch_bounds__(256) k_wshade(WaveParams P) {
             slot = f2u(o.w);
             ray.o = mk3(o.x, o.y, o.z);
             ray.d = mk3(d.x, d.y, d.z);
-            emit = shade_item(P, EmitGlobal{P.S}, slot, ray, hid, sdone PF_PASS);
+            emit = shade_item(P, EmitGlobal{P.S}, slot, ray, hid, sdone);
         }
         if (P.progress) {
             const uint32_t nd = (uint32_t)__popcll(__ballot(sdone));
@@ -1681,6 +1552,15 @@ hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s) {
     p.parity = 0u;
     hipLaunchKernelGGL(pt::k_wcamera, dim3(p.n_tiles_local), dim3(256), 0, s, p);
     hipLaunchKernelGGL(pt::k_wcamera_merge, dim3(p.n_tiles_local < 1024u ? p.n_tiles_local : 1024u), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_coop_order(pt::WaveParams p, uint32_t n, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(p.order_cur, 0, 2u * PT_ORDER_BUCKETS * 4u, s);
+    if (e != hipSuccess) return e;
+    const uint32_t grid = n / 256u + 1u < 1024u ? n / 256u + 1u : 1024u;
+    hipLaunchKernelGGL(pt::k_coop_hist, dim3(grid), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(pt::k_coop_scatter, dim3(grid), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 

@@ -90,6 +90,8 @@ const Rccl& rccl() {
 //                     768 per CU; the mix of the other rounds)
 //   lowq_wg=N         ... and their path workgroups per CU (PT_CMAX chains each; default 2)
 //   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
+//   coop_order=0      the cooperative engine takes its chains in queue order (default: the pixels
+//                     with the most samples left first)
 //   cap=N             chains a workgroup may hold
 //   batch=N           round-queue entries a query wave takes per pull (1..64, default 32)
 //   lstack=N          aux stack words a path-engine query may use (default and maximum PT_LSTACK;
@@ -212,8 +214,7 @@ struct pt_scene {
     std::vector<float> regions;   // per reference node: its leaf's hit region {lo, hi} (lo > hi: unbounded)
     uint32_t aux_coarse_leaves = 0;   // leaf entries whose binary16 own box is > 4x wider than the f32 one
     float thr[256];
-    // the device upload image (built once, on the first upload): section offsets
-    std::vector<unsigned char> image;
+    // the device-only sections of the blob (byte offsets; the device copy is the blob)
     size_t i_shade = 0, i_planes = 0, i_emit = 0, i_thr = 0, i_top = 0;
     uint32_t n_top = 0;
     std::map<int, std::unique_ptr<DevEntry>> dev;
@@ -242,6 +243,8 @@ struct pt_session {
     uint32_t mix[3] = {PT_PROBE_EVERY, PT_PROBE_MIN, PT_AUX2}, mix_low[3] = {PT_PROBE_EVERY, PT_PROBE_MIN, PT_AUX2};
     uint32_t lowq = 0;
     uint32_t low_grid = 0;        // path workgroups of those rounds
+    bool coop_order = true;       // the cooperative engine takes the pixels furthest from the target first
+    uint32_t* order = nullptr;    // its intake order (min(pixels, coop_max) entries) + 2 x 256 bucket counters
     uint32_t coop_team = 8;       // lanes per chain in the cooperative engine (pure-coop rate, teams of
                                   // 64 / 32 / 16 / 8: 283 / 392 / 572 / 815 Mray/s)
     // every device buffer below lives in one allocation (pt_session_create)
@@ -251,7 +254,7 @@ struct pt_session {
     pt::DoneQ done = {};          // exact-DFS results (lane_cap)
     pt::RayQ ex = {};             // rays handed to the exact DFS (lane_cap)
     uint32_t* carry = nullptr;    // 2 * carry_cap * carry_words
-    uint32_t* endq = nullptr;     // path_grid * PT_CMAX: the shade waves' ended paths (PT_DEFER_ENDS)
+    uint2* endq = nullptr;        // path_grid * PT_CMAX: the shade waves' ended paths
     uint32_t lane_cap = 0;        // min(pixels, query lanes): what one round can suspend or hand over
     uint32_t carry_cap = 0, carry_words = 0;
     uint32_t* ctl = nullptr;      // 2 x PT_CTL_SET round counters
@@ -421,6 +424,19 @@ bool leaf_hit_region(const pt_scene* s, uint32_t leaf, float lo[3], float hi[3])
     return true;
 }
 
+// fn(begin, end, part) over [0, n) in at most `parts` contiguous chunks, one thread each
+// (host preparation loops whose items are independent)
+template <class F>
+void parallel_chunks(size_t n, unsigned parts, F fn) {
+    parts = std::max(1u, std::min<unsigned>(parts, (unsigned)((n + 8191) / 8192)));
+    if (parts == 1) { fn((size_t)0, n, 0u); return; }
+    std::vector<std::thread> th;
+    for (unsigned k = 0; k < parts; ++k)
+        th.emplace_back(fn, n * k / parts, n * (k + 1) / parts, k);
+    for (auto& t : th) t.join();
+}
+unsigned prep_threads() { return std::max(1u, std::min(16u, std::thread::hardware_concurrency())); }
+
 // binary16 bits of x rounded toward -inf (down) or +inf (up)
 uint32_t f16_out(float x, bool up) {
     const _Float16 h = (_Float16)x;
@@ -468,8 +484,11 @@ void encode_aux_entries(pt_scene* s, std::vector<pt::AuxSL>& aux) {
     // binary16 keeps parity (outward rounding) but not culling: past |x| = 65504 a bound
     // becomes infinite, and its step is 2 or more above 2048 -- leaf boxes much smaller
     // than that step are then visited by far more rays (counted, warned about once)
+    const unsigned parts = prep_threads();
+    std::vector<size_t> coarse_k(parts, 0), leaves_k(parts, 0);
+    parallel_chunks(aux.size(), parts, [&](size_t i0, size_t i1, unsigned part) {
     size_t coarse = 0, leaves = 0;
-    for (size_t i = 0; i < aux.size(); ++i) {
+    for (size_t i = i0; i < i1; ++i) {
         pt::AuxSL& e = aux[i];
         if (pt::f2u(e.b.w) == 0xFFFFFFFFu) continue;
         const float A[6] = {e.a.x, e.a.y, e.a.z, e.a.w, e.b.x, e.b.y};
@@ -496,21 +515,49 @@ void encode_aux_entries(pt_scene* s, std::vector<pt::AuxSL>& aux) {
                      pt::u2f(h[6] | h[7] << 16)};
         e.b = pt::F4{pt::u2f(h[8] | h[9] << 16), pt::u2f(h[10] | h[11] << 16), pt::u2f(range), pt::u2f(code)};
     }
+    coarse_k[part] = coarse;
+    leaves_k[part] = leaves;
+    });
+    size_t coarse = 0, leaves = 0;
+    for (unsigned k = 0; k < parts; ++k) { coarse += coarse_k[k]; leaves += leaves_k[k]; }
     s->aux_coarse_leaves = (uint32_t)coarse;
     if (leaves && coarse * 100 > leaves)
         fprintf(stderr, "pt: %zu of %zu leaf boxes are more than 4x wider in the binary16 aux BVH (coordinates "
                         "beyond ~2048 or +-65504): results stay exact, traversal visits more nodes\n", coarse, leaves);
 }
 
+// k_wcamera's costly-class test reads the wide aux root's entries and, for each
+// inner one, its child node's entries (f32 host form): entries 0..W-1 = the root,
+// entries W (1 + k) .. = the child of root entry k, whose code is rewritten to 1 + k
+std::vector<pt::AuxSL> aux_top(const pt_scene* s) {
+    const uint32_t W = PT_AUXW;
+    std::vector<pt::AuxSL> t;
+    if (s->auxsl.size() < W) return t;
+    t.assign(s->auxsl.begin(), s->auxsl.begin() + W);
+    for (uint32_t k = 0; k < W; ++k) {
+        const uint32_t code = pt::f2u(t[k].b.w);
+        if (code == 0xFFFFFFFFu || (code & 0x80000000u)) continue;
+        if ((size_t)(code + 1) * W > s->auxsl.size()) throw std::runtime_error("aux root child out of range");
+        const uint32_t at = (uint32_t)(t.size() / W);
+        t.insert(t.end(), s->auxsl.begin() + (size_t)code * W, s->auxsl.begin() + (size_t)(code + 1) * W);
+        t[k].b.w = pt::u2f(at);
+    }
+    return t;
+}
+
 // one 16-B-aligned blob holding every array the wavefront query reads
 // (SceneView::blob; 32-bit byte offsets).  The compact primitive records
 // (pt_query.h qprim_expand) are built here.
-void build_query_blob(pt_scene* s) {
+void build_query_blob(pt_scene* s, const std::function<void(const char*)>& tick) {
     std::vector<pt::F4>& b = s->blob;
     b.clear();
-    // every section's 16-B pieces, reserved at once (the blob is tens of MB)
-    b.reserve(s->dnodes.size() * 2 + s->auxsl.size() * 2 + (s->anc_info.size() + s->anc.size()) / 4 +
-              s->dprims.size() * (4 + 5 + 4) + 64);
+    // every section's 16-B pieces, reserved at once (the blob is tens of MB; a
+    // reallocation would copy it): nodes, aux, ancestor lists, compact primitives (4),
+    // full primitives (5), shading records (2), leaf bundles (6 per leaf), the small
+    // device-only tables and the 256-B section padding
+    b.reserve(s->dnodes.size() * 2 + s->auxsl.size() * 2 + (s->anc_info.size() + s->anc.size()) / 4 + 4 +
+              s->dprims.size() * (4 + 5 + 2) + (s->dnodes.size() / 2 + 1) * 6 +
+              (s->planes.size() + s->emitters.size()) / 4 + 64 + 2 * 5 * PT_AUXW + 16 * 12);
     auto append = [&b](const void* p, size_t bytes) {
         // sections are addressed by 32-bit byte offsets (and the device forms record
         // offsets from them in 32 bits): the whole blob must stay below 4 GiB
@@ -537,13 +584,16 @@ void build_query_blob(pt_scene* s) {
         e.b.z = pt::u2f((uint32_t)leaves.size());
         leaves.push_back(leaf);
     }
+    tick("blob: leaf ordinals");
     encode_aux_entries(s, aux);
+    tick("blob: aux encode");
     s->o_nodes = append(s->dnodes.data(), s->dnodes.size() * sizeof(pt::Node));
     s->o_aux = append(aux.data(), aux.size() * sizeof(pt::AuxSL));
     s->o_ainfo = append(s->anc_info.data(), s->anc_info.size() * 4);
     s->o_anc = append(s->anc.data(), s->anc.size() * 4);
     std::vector<pt::F4> qp(4 * s->dprims.size());
-    for (size_t i = 0; i < s->dprims.size(); ++i) {
+    parallel_chunks(s->dprims.size(), prep_threads(), [&](size_t i0, size_t i1, unsigned) {
+    for (size_t i = i0; i < i1; ++i) {
         const pt::Prim& P = s->dprims[i];
         const uint32_t type = pt::f2u(P.p0.w);
         const bool pos0 = pt::f2u(P.p0.x) == 0u && pt::f2u(P.p0.y) == 0u && pt::f2u(P.p0.z) == 0u;
@@ -568,6 +618,8 @@ void build_query_blob(pt_scene* s) {
             r[1] = r[2] = r[3] = pt::F4{0.f, 0.f, 0.f, 0.f};
         }
     }
+    });
+    tick("blob: sections + qprims");
     s->o_qprim = append(qp.data(), qp.size() * sizeof(pt::F4));
     // leaf bundles (pt_query.h): the compact record of the leaf's first primitive
     // (pieces 0-2), then {leaf node index, first primitive, primitive count, its n.z}
@@ -587,6 +639,19 @@ void build_query_blob(pt_scene* s) {
     }
     s->o_bundle = append(bu.data(), bu.size() * sizeof(pt::F4));
     s->o_prim = append(s->dprims.data(), s->dprims.size() * sizeof(pt::Prim));
+    tick("blob: bundles + prims");
+    // The device copy is the blob itself plus the tables only the kernels read (shading
+    // records, plane and emitter lists, gamma thresholds, k_wcamera's top aux levels),
+    // each at a 256-B offset: one host image, uploaded with one copy (ensure_device_scene)
+    auto align256 = [&b] { b.resize((b.size() + 15) & ~(size_t)15, pt::F4{0.f, 0.f, 0.f, 0.f}); };
+    const std::vector<pt::AuxSL> top = aux_top(s);
+    align256(); s->i_shade = append(s->dshade.data(), s->dshade.size() * sizeof(pt::Shade));
+    align256(); s->i_planes = append(s->planes.data(), s->planes.size() * 4);
+    align256(); s->i_emit = append(s->emitters.data(), s->emitters.size() * 4);
+    align256(); s->i_thr = append(s->thr, sizeof(s->thr));
+    align256(); s->i_top = append(top.data(), top.size() * sizeof(pt::AuxSL));
+    s->n_top = (uint32_t)top.size();
+    align256();
     if (b.size() * 16 >= 0xFFFFFFF0ull) throw std::runtime_error("scene too large for 32-bit query offsets");
 }
 
@@ -625,52 +690,6 @@ int check_device(int dev) {
     return PT_OK;
 }
 
-// k_wcamera's costly-class test reads the wide aux root's entries and, for each
-// inner one, its child node's entries (f32 host form): entries 0..W-1 = the root,
-// entries W (1 + k) .. = the child of root entry k, whose code is rewritten to 1 + k
-std::vector<pt::AuxSL> aux_top(const pt_scene* s) {
-    const uint32_t W = PT_AUXW;
-    std::vector<pt::AuxSL> t;
-    if (s->auxsl.size() < W) return t;
-    t.assign(s->auxsl.begin(), s->auxsl.begin() + W);
-    for (uint32_t k = 0; k < W; ++k) {
-        const uint32_t code = pt::f2u(t[k].b.w);
-        if (code == 0xFFFFFFFFu || (code & 0x80000000u)) continue;
-        if ((size_t)(code + 1) * W > s->auxsl.size()) throw std::runtime_error("aux root child out of range");
-        const uint32_t at = (uint32_t)(t.size() / W);
-        t.insert(t.end(), s->auxsl.begin() + (size_t)code * W, s->auxsl.begin() + (size_t)(code + 1) * W);
-        t[k].b.w = pt::u2f(at);
-    }
-    return t;
-}
-
-// the host image of a device scene (DevScene): sections at 256-B offsets
-void build_upload_image(pt_scene* s) {
-    if (!s->image.empty()) return;
-    const std::vector<pt::AuxSL> top = aux_top(s);
-    size_t at = 0;
-    auto sec = [&at](size_t bytes) {
-        const size_t o = at;
-        at = (at + std::max<size_t>(bytes, 4) + 255) & ~(size_t)255;
-        return o;
-    };
-    sec(s->blob.size() * sizeof(pt::F4));
-    s->i_shade = sec(s->dshade.size() * sizeof(pt::Shade));
-    s->i_planes = sec(s->planes.size() * 4);
-    s->i_emit = sec(s->emitters.size() * 4);
-    s->i_thr = sec(sizeof(s->thr));
-    s->i_top = sec(top.size() * sizeof(pt::AuxSL));
-    s->n_top = (uint32_t)top.size();
-    std::vector<unsigned char> img(at, 0);
-    memcpy(img.data(), s->blob.data(), s->blob.size() * sizeof(pt::F4));
-    if (!s->dshade.empty()) memcpy(img.data() + s->i_shade, s->dshade.data(), s->dshade.size() * sizeof(pt::Shade));
-    if (!s->planes.empty()) memcpy(img.data() + s->i_planes, s->planes.data(), s->planes.size() * 4);
-    if (!s->emitters.empty()) memcpy(img.data() + s->i_emit, s->emitters.data(), s->emitters.size() * 4);
-    memcpy(img.data() + s->i_thr, s->thr, sizeof(s->thr));
-    if (!top.empty()) memcpy(img.data() + s->i_top, top.data(), top.size() * sizeof(pt::AuxSL));
-    s->image.swap(img);
-}
-
 // The scene on device `dev`, uploaded on first use: one allocation and one copy
 // of the upload image.  Devices upload in parallel (a lock per device).  mega:
 // also the BVH2 aux of the megakernel traversal.
@@ -678,11 +697,6 @@ int ensure_device_scene(pt_scene* s, int dev, bool mega, DevScene** out, double*
     DevEntry* e;
     {
         std::lock_guard<std::mutex> lk(s->mu);
-        try {
-            build_upload_image(s);
-        } catch (const std::exception& x) {
-            return fail(PT_E_SCENE, x.what());
-        }
         auto& slot = s->dev[dev];
         if (!slot) slot.reset(new DevEntry());
         e = slot.get();
@@ -694,8 +708,9 @@ int ensure_device_scene(pt_scene* s, int dev, bool mega, DevScene** out, double*
     if (!e->ready) {
         const auto t0 = std::chrono::steady_clock::now();
         void* p = nullptr;
-        HIP_TRY(hipMalloc(&p, s->image.size()));
-        if (hipMemcpy(p, s->image.data(), s->image.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        const size_t bytes = s->blob.size() * sizeof(pt::F4);
+        HIP_TRY(hipMalloc(&p, bytes));
+        if (hipMemcpy(p, s->blob.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
             (void)hipFree(p);
             return fail(PT_E_HIP, "scene upload failed");
         }
@@ -977,9 +992,9 @@ int pt_scene_prepare(pt_scene* s) {
         if (s->auxw_stack > PT_QUERY_SP_MAX)
             throw std::runtime_error("auxiliary BVH too deep for the query's stack counter");
         tick("aux wide + ranges");
-        build_query_blob(s);
-        tick("query blob");
         pth::build_gamma_thresholds(s->thr);
+        build_query_blob(s, tick);
+        tick("query blob");
     } catch (const std::exception& e) {
         return fail(PT_E_SCENE, e.what());
     }
@@ -1152,6 +1167,7 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // above the hand-over
         if (ss->coop_max && !tune_has("sparse")) ss->path_sparse = std::min(ss->path_sparse, ss->coop_max);
         ss->round_batch = (uint32_t)std::max(1, tune_int("round_batch", (int)ss->round_batch));
+        ss->coop_order = tune_int("coop_order", 1) != 0;
         {
             static const char* keys[3] = {"probe_every", "probe_min", "aux_extra"};
             static const char* lkeys[3] = {"lowq_probe_every", "lowq_probe_min", "lowq_aux_extra"};
@@ -1200,7 +1216,7 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         const size_t a_rec = sec(2 * n * sizeof(uint4)), a_fold = sec((size_t)ss->st.depth * n * sizeof(uint4));
         const size_t a_ctr = sec(8 * PT_CTR_COPIES * PT_CTR_STRIDE), a_out = sec(3 * n);
         size_t a_fq[2][3] = {{0, 0, 0}, {0, 0, 0}}, a_pid = 0, a_dq[2] = {0, 0}, a_ex[2] = {0, 0}, a_hid = 0;
-        size_t a_carry = 0, a_ctl = 0, a_endq = 0;
+        size_t a_carry = 0, a_ctl = 0, a_endq = 0, a_order = 0;
         const size_t lanes = ss->lane_cap;
         if (ss->wave) {
             for (int q = 0; q < 2; ++q)
@@ -1210,7 +1226,8 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
             a_hid = sec(lanes * 4);
             a_carry = sec(2ull * ss->carry_cap * ss->carry_words * 4);
             a_ctl = sec(8 * PT_CTL_SET);
-            a_endq = sec((size_t)ss->path_grid * PT_CMAX * 4);
+            a_endq = sec((size_t)ss->path_grid * PT_CMAX * sizeof(uint2));
+            a_order = sec((std::min<size_t>(n, std::max<uint32_t>(ss->coop_max, 1u)) + 2 * PT_ORDER_BUCKETS) * 4);
         }
         if (take_stream(ss->dev, &ss->stream) != hipSuccess) return cleanup(fail(PT_E_HIP, "stream creation failed"));
         void* p = nullptr;
@@ -1242,7 +1259,8 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
                               nullptr};
             ss->carry = reinterpret_cast<uint32_t*>(A + a_carry);
             ss->ctl = reinterpret_cast<uint32_t*>(A + a_ctl);
-            ss->endq = reinterpret_cast<uint32_t*>(A + a_endq);
+            ss->endq = reinterpret_cast<uint2*>(A + a_endq);
+            ss->order = reinterpret_cast<uint32_t*>(A + a_order);
             if (hipHostMalloc(&ss->ctl_host, 64) != hipSuccess)
                 return cleanup(fail(PT_E_OOM, "host allocation failed (round counters)"));
         }
@@ -1377,7 +1395,16 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                     HIP_TRY(hipMemsetAsync(ss->wg_prof, 0, 512, ss->stream));
                     wp.wg_prof = ss->wg_prof;
                 }
+                if (ss->coop_order) {
+                    const size_t cap = std::min<size_t>(std::max<size_t>(ss->n_slots, 1),
+                                                        std::max<uint32_t>(ss->coop_max, 1u));
+                    if (chains > cap) return fail(PT_E_HIP, "cooperative intake order: more chains than entries");
+                    wp.order_cur = ss->order;
+                    wp.order = ss->order + 2 * PT_ORDER_BUCKETS;
+                    HIP_TRY(pt_launch_coop_order(wp, chains, ss->stream));
+                }
                 HIP_TRY(pt_launch_coop(wp, grid, team, big, ss->stream, i0, i1));
+                wp.order = wp.order_cur = nullptr;
                 if (cprof) {
                     unsigned long long cp[64];
                     HIP_TRY(hipMemcpyAsync(cp, wp.wg_prof, 512, hipMemcpyDeviceToHost, ss->stream));

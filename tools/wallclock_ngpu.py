@@ -37,8 +37,14 @@ def run(src, n, tune):
         env["PT_TUNE"] = tune
         env["PT_GATHER"] = "host"
     t0 = time.perf_counter()
+    u0 = time.time()
     r = subprocess.run([os.path.join(REPO, "run.sh"), src, out], env=env, capture_output=True, text=True, timeout=300)
     wall = time.perf_counter() - t0
+    u1 = time.time()
+    um = re.search(r"unix_main=([\d.]+) unix_written=([\d.]+)", r.stderr)
+    # before main(): exec + dynamic loading; after the PPM is closed: process exit (the runtime's teardown)
+    before_main = float(um.group(1)) - u0 if um else None
+    after_write = u1 - float(um.group(2)) if um else None
     if r.returncode != 0:
         raise RuntimeError(r.stderr[-400:])
     md5 = hashlib.md5(open(out, "rb").read()).hexdigest()
@@ -54,6 +60,7 @@ def run(src, n, tune):
     renders = [x["render_ms"] for x in ranks]
     proj = wall - sum(renders) / 1e3 + max(renders) / 1e3
     return {"ngpu": n, "wall_s": wall, "projected_wall_s": proj, "rays": int(st["rays"]), "ppm_md5": md5,
+            "before_main_s": before_main, "after_ppm_s": after_write,
             "cli_phases_ms": cli, "gather_ms": float(g.group(1)) if g else None,
             "setup_ms_max": max(x["setup_ms"] for x in ranks), "setup_ms": [x["setup_ms"] for x in ranks],
             "scene_upload_ms": [x["scene_upload_ms"] for x in ranks], "render_ms": renders,
