@@ -132,6 +132,11 @@ struct WaveParams {
     // remaining samples, most first (k_coop_order); `order_cur` = its 256 bucket cursors
     uint32_t* order;
     uint32_t* order_cur;
+    // k_wpath's intake through an index list (null: the queues in order): work item i of
+    // the round is queue item pin[i], i < pin_n (the round after an early cooperative
+    // launch took the first entries of the intake order)
+    const uint32_t* pin;
+    uint32_t pin_n;
 };
 #define PT_ORDER_BUCKETS 256u
 
@@ -213,6 +218,12 @@ hipError_t pt_launch_path_round(pt::WaveParams p, uint32_t path_grid, uint32_t s
 // the cooperative engine's intake order (WaveParams::order): the round's n work items
 // counting-sorted by their pixels' remaining samples, most first
 hipError_t pt_launch_coop_order(pt::WaveParams p, uint32_t n, hipStream_t s);
+// the early cooperative launch's queue: the first k items of p.order (the pixels with the
+// most samples left) copied into `side` -- fresh rays as they are, suspended queries as
+// restart records (their ray and slot) -- whose round counters side_ctl[C_CARRY / C_FRESH]
+// count them (zeroed by the caller)
+hipError_t pt_launch_side_take(pt::WaveParams p, uint32_t k, pt::RayQ side, uint32_t* side_carry, uint32_t* side_ctl,
+                               hipStream_t s);
 // cooperative engine: one launch runs every remaining chain of the pass to its end
 // team = lanes per chain (8 -- the default --, 16, 32 or 64)
 // big: the scene exceeds the LDS tables (QC_FOLD / QC_NPL / QC_NEM; team 8 or 64 then)

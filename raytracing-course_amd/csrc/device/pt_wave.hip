@@ -366,7 +366,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     const uint32_t p = P.parity;
     const uint32_t* in = P.ctl + PT_CTL_SET * p;
     uint32_t* out = P.ctl + PT_CTL_SET * (1u - p);
-    const uint32_t n_carry = in[C_CARRY], n_total = in[C_FRESH] + n_carry;
+    const uint32_t n_carry = in[C_CARRY], n_total = P.pin ? P.pin_n : in[C_FRESH] + n_carry;
     const uint32_t n_waves = gridDim.x * PT_NQ;
     // Rounds exist to rebalance chains between workgroups.  Once the round's chains
     // fit in the query lanes (the tail of a pass: only the slowest pixels are left)
@@ -505,6 +505,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
             uint32_t cid = 0u;
             if (src == 1u) cid = lds_get(L.F, (fh + lanes_below(mjoin)) % PT_CMAX);
             if (src == 2u) cid = lds_get(L.rq_cid, gi);
+            if (src == 1u && P.pin) gi = P.pin[gi];   // (the early cooperative launch took the other items)
             bool took = false;   // a fresh ray (not a resumed query) started in this lane
             if (src == 1u && gi < n_carry) {
                 // resume a suspended query: state, slot, then its aux stack into LDS
@@ -912,10 +913,8 @@ struct EmitLds {
 // t, nor the sign of dn that picks the normal's side (pt_query.h probe) -- and its
 // normal goes through the same last step, normalize(qrot(rotation, n)), so the Hit
 // has the full test's bits; other records expand to the full form.
-__device__ __forceinline__ bool qc_prim_hit(const SceneView& S, uint32_t i, const Ray& ray, Hit& h) {
-    const uint32_t o = S.o_qprim + PT_QPRIM_BYTES * i;
-    const F4 r0 = blob_piece(S, o), r1 = blob_piece(S, o + 16u), r2 = blob_piece(S, o + 32u),
-             r3 = blob_piece(S, o + 48u);
+__device__ __forceinline__ bool qc_prim_hit_rec(const SceneView& S, uint32_t i, F4 r0, F4 r1, F4 r2, F4 r3,
+                                                const Ray& ray, Hit& h) {
     const uint32_t ty = f2u(r0.w);
     if (ty == T_TRIANGLE) {
         if (!isect_triangle_n(ray, mk3(r0.x, r0.y, r0.z), mk3(r1.x, r1.y, r1.z), mk3(r2.x, r2.y, r2.z),
@@ -928,6 +927,11 @@ __device__ __forceinline__ bool qc_prim_hit(const SceneView& S, uint32_t i, cons
     }
     if (ty & PT_QP_FULL) return bvh_prim_intersect(S.prims[i], ray, h);
     return bvh_prim_intersect(qprim_expand(r0, r1, r2), ray, h);
+}
+__device__ __forceinline__ bool qc_prim_hit(const SceneView& S, uint32_t i, const Ray& ray, Hit& h) {
+    const uint32_t o = S.o_qprim + PT_QPRIM_BYTES * i;
+    return qc_prim_hit_rec(S, i, blob_piece(S, o), blob_piece(S, o + 16u), blob_piece(S, o + 32u),
+                           blob_piece(S, o + 48u), ray, h);
 }
 
 #ifdef PT_CPROF
@@ -977,18 +981,32 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
             const uint32_t take = want ? (nc < T ? nc : T) : 0u;
             nc -= take;
             const bool act = tl < take;
-            const uint32_t c = act ? L.cand[nc + tl] : 0u;
-            const Node nd = S.nodes[c];
-            const uint32_t ainfo = S.anc_info[c];
+            // a candidate is its leaf's bundle (pt_query.h: the leaf's node box, its primitive
+            // range and its first primitive's compact record): the slab test and the first
+            // primitive's test take one round of independent loads
+            const uint32_t ord = act ? L.cand[nc + tl] : 0u;
+            const uint32_t bo = S.o_bundle + PT_BUNDLE_BYTES * ord;
+            const F4 b0 = blob_piece(S, bo), b1 = blob_piece(S, bo + 16u), b2 = blob_piece(S, bo + 32u),
+                     b3 = blob_piece(S, bo + 48u), b4 = blob_piece(S, bo + 64u), b5 = blob_piece(S, bo + 80u);
+            const uint32_t c = f2u(b3.x);          // the reference leaf
+            const uint32_t ainfo = act ? S.anc_info[c] : 0u;
+            Node nd;
+            nd.a = b4;                             // the leaf's node record: {c.xyz, s.x}, {s.y, s.z, first, count}
+            nd.b = F4{b5.x, b5.y, b3.y, b3.z};
             C.nodes += act ? 1u : 0u;
             const bool hb = act && qc_slab_hit(nd, ray, inv, par);
-            const uint32_t ref = f2u(nd.b.z), cnt = hb ? f2u(nd.b.w) : 0u;
+            const uint32_t ref = f2u(b3.y), cnt = hb ? f2u(b3.z) : 0u;
             Hit best;
             best.t = PT_INF;
             best.n = mk3(0.f, 0.f, 0.f);
             best.interior = 0u;
             int lid = -1;
-            for (uint32_t i = 0; __ballot(i < cnt) != 0ull; ++i) {
+            if (cnt) {
+                Hit hh;
+                C.ptests++;
+                if (qc_prim_hit_rec(S, ref, b0, b1, b2, F4{b3.w, 0.f, 0.f, 0.f}, ray, hh)) { best = hh; lid = (int)ref; }
+            }
+            for (uint32_t i = 1; __ballot(i < cnt) != 0ull; ++i) {
                 if (i < cnt) {
                     Hit hh;
                     C.ptests++;
@@ -1056,7 +1074,7 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
                 const bool inner = h && (code & 0x80000000u) == 0u;
                 const unsigned long long mi = __ballot(inner) & tmask, ml = __ballot(leaf) & tmask;
                 if (inner) L.stk[ns + lanes_below(mi)] = code;
-                if (leaf) L.cand[nc + lanes_below(ml)] = code & 0x7fffffffu;
+                if (leaf) L.cand[nc + lanes_below(ml)] = f2u(eb[j].z);   // (a leaf entry's range: its bundle)
                 ns += (uint32_t)__popcll(mi);
                 nc += (uint32_t)__popcll(ml);
             }
@@ -1468,6 +1486,36 @@ __global__ void __launch_bounds__(256) k_coop_scatter(WaveParams P) {
     }
 }
 
+// The early cooperative launch's queue (pt_launch_side_take): item j < k of the
+// intake order, a fresh ray copied as it is, a suspended query as a restart record
+// (the cooperative engine restarts a query from its ray and slot alone).  side_ctl's
+// C_CARRY / C_FRESH count the two kinds as they are appended (the launch's round
+// counters: carry records first in its work numbering, as in every round).
+__global__ void __launch_bounds__(256) k_side_take(WaveParams P, uint32_t k, RayQ side, uint32_t* side_carry,
+                                                   uint32_t* side_ctl) {
+    const uint32_t* in = P.ctl + PT_CTL_SET * P.parity;
+    const uint32_t n_carry = in[C_CARRY];
+    const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+    const bool on = j < k;
+    const uint32_t gi = on ? P.order[j] : 0u;
+    const bool carry = on && gi < n_carry;
+    const uint32_t kc = wave_append(side_ctl + C_CARRY, carry);
+    const uint32_t kf = wave_append(side_ctl + C_FRESH, on && !carry);
+    if (carry) {
+        const uint32_t* w = P.cq[P.parity] + (size_t)gi * P.carry_words;
+        uint32_t* d = side_carry + (size_t)kc * P.carry_words;
+        *reinterpret_cast<Ray*>(d) = reinterpret_cast<const Query*>(w)->ray;
+        d[sizeof(Query) / 4u] = w[sizeof(Query) / 4u];
+    } else if (on) {
+        const RayQ& F = P.fq[P.parity];
+        const uint32_t fi = gi - n_carry;
+        side.ro[kf] = F.ro[fi];
+        side.rd[kf] = F.rd[fi];
+        side.pid[kf] = F.pid[fi];
+        side.ri[kf] = F.ri[fi];
+    }
+}
+
 // The rays the path engine hands back (Q_EXACT: an aux stack deeper than the
 // engine's LDS stack, a hitting-leaf list full of entered hits, non-finite
 // components); 64-lane workgroups, one ray per lane, stack in LDS.  The replay
@@ -1561,6 +1609,13 @@ hipError_t pt_launch_coop_order(pt::WaveParams p, uint32_t n, hipStream_t s) {
     const uint32_t grid = n / 256u + 1u < 1024u ? n / 256u + 1u : 1024u;
     hipLaunchKernelGGL(pt::k_coop_hist, dim3(grid), dim3(256), 0, s, p);
     hipLaunchKernelGGL(pt::k_coop_scatter, dim3(grid), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_side_take(pt::WaveParams p, uint32_t k, pt::RayQ side, uint32_t* side_carry, uint32_t* side_ctl,
+                               hipStream_t s) {
+    if (k == 0u) return hipSuccess;
+    hipLaunchKernelGGL(pt::k_side_take, dim3((k + 255u) / 256u), dim3(256), 0, s, p, k, side, side_carry, side_ctl);
     return hipGetLastError();
 }
 

@@ -92,6 +92,10 @@ const Rccl& rccl() {
 //   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
 //   coop_order=0      the cooperative engine takes its chains in queue order (default: the pixels
 //                     with the most samples left first)
+//   early=K, early_at=N, early_wg=W
+//                     once a pass's chains fall below N (default 768 per CU), its K heaviest chains
+//                     (1: what W cooperative workgroups per CU hold) run in a cooperative launch on a
+//                     second stream beside the path rounds, to the end of the pass (default: off)
 //   cap=N             chains a workgroup may hold
 //   batch=N           round-queue entries a query wave takes per pull (1..64, default 32)
 //   lstack=N          aux stack words a path-engine query may use (default and maximum PT_LSTACK;
@@ -244,7 +248,15 @@ struct pt_session {
     uint32_t lowq = 0;
     uint32_t low_grid = 0;        // path workgroups of those rounds
     bool coop_order = true;       // the cooperative engine takes the pixels furthest from the target first
-    uint32_t* order = nullptr;    // its intake order (min(pixels, coop_max) entries) + 2 x 256 bucket counters
+    uint32_t* order = nullptr;    // 2 x 256 bucket counters + the intake order (a round's work: <= pixels)
+    // early cooperative launch: once a pass's chains fall below early_at, the early_k chains
+    // with the most samples left run in a cooperative launch on a second stream (early_wg
+    // workgroups per CU, beside the path engine's low-chain rounds) to the end of the pass
+    uint32_t early_k = 0, early_at = 0, early_wg = 1;
+    pt::RayQ side = {};           // its queue (early_k entries) ...
+    uint32_t* side_carry = nullptr;   // ... its suspended queries' restart records (early_k x carry_words)
+    uint32_t* side_ctl = nullptr;     // ... and its two round-counter sets
+    hipStream_t side_stream = nullptr;
     uint32_t coop_team = 8;       // lanes per chain in the cooperative engine (pure-coop rate, teams of
                                   // 64 / 32 / 16 / 8: 283 / 392 / 572 / 815 Mray/s)
     // every device buffer below lives in one allocation (pt_session_create)
@@ -1168,6 +1180,14 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         if (ss->coop_max && !tune_has("sparse")) ss->path_sparse = std::min(ss->path_sparse, ss->coop_max);
         ss->round_batch = (uint32_t)std::max(1, tune_int("round_batch", (int)ss->round_batch));
         ss->coop_order = tune_int("coop_order", 1) != 0;
+        // Early cooperative launch (teams of 8, QC_WAVES waves per workgroup: 32 chains each):
+        // the low-chain rounds leave each CU room for one more workgroup, which the heaviest
+        // chains use from then on instead of waiting for the final hand-over
+        ss->early_wg = (uint32_t)std::max(1, tune_int("early_wg", 1));
+        ss->early_at = (uint32_t)std::max(0, tune_int("early_at", (int)(cus * 768u)));
+        ss->early_k = (uint32_t)std::max(0, tune_int("early", 0));
+        if (ss->early_k == 1u) ss->early_k = cus * ss->early_wg * QC_WAVES * 8u;   // early=1: what the launch holds
+        if (!ss->coop_max || ss->coop_team != 8u) ss->early_k = 0;
         {
             static const char* keys[3] = {"probe_every", "probe_min", "aux_extra"};
             static const char* lkeys[3] = {"lowq_probe_every", "lowq_probe_min", "lowq_aux_extra"};
@@ -1216,7 +1236,7 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         const size_t a_rec = sec(2 * n * sizeof(uint4)), a_fold = sec((size_t)ss->st.depth * n * sizeof(uint4));
         const size_t a_ctr = sec(8 * PT_CTR_COPIES * PT_CTR_STRIDE), a_out = sec(3 * n);
         size_t a_fq[2][3] = {{0, 0, 0}, {0, 0, 0}}, a_pid = 0, a_dq[2] = {0, 0}, a_ex[2] = {0, 0}, a_hid = 0;
-        size_t a_carry = 0, a_ctl = 0, a_endq = 0, a_order = 0;
+        size_t a_carry = 0, a_ctl = 0, a_endq = 0, a_order = 0, a_side[6] = {0, 0, 0, 0, 0, 0};
         const size_t lanes = ss->lane_cap;
         if (ss->wave) {
             for (int q = 0; q < 2; ++q)
@@ -1227,7 +1247,13 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
             a_carry = sec(2ull * ss->carry_cap * ss->carry_words * 4);
             a_ctl = sec(8 * PT_CTL_SET);
             a_endq = sec((size_t)ss->path_grid * PT_CMAX * sizeof(uint2));
-            a_order = sec((std::min<size_t>(n, std::max<uint32_t>(ss->coop_max, 1u)) + 2 * PT_ORDER_BUCKETS) * 4);
+            a_order = sec((n + 2 * PT_ORDER_BUCKETS) * 4);
+            if (ss->early_k) {
+                for (int k = 0; k < 3; ++k) a_side[k] = sec((size_t)ss->early_k * 16);
+                a_side[3] = sec((size_t)ss->early_k * 4);
+                a_side[4] = sec((size_t)ss->early_k * ss->carry_words * 4);
+                a_side[5] = sec(8 * PT_CTL_SET);
+            }
         }
         if (take_stream(ss->dev, &ss->stream) != hipSuccess) return cleanup(fail(PT_E_HIP, "stream creation failed"));
         void* p = nullptr;
@@ -1261,6 +1287,14 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
             ss->ctl = reinterpret_cast<uint32_t*>(A + a_ctl);
             ss->endq = reinterpret_cast<uint2*>(A + a_endq);
             ss->order = reinterpret_cast<uint32_t*>(A + a_order);
+            if (ss->early_k) {
+                ss->side.ro = reinterpret_cast<pt::F4*>(A + a_side[0]);
+                ss->side.rd = reinterpret_cast<pt::F4*>(A + a_side[1]);
+                ss->side.ri = reinterpret_cast<pt::F4*>(A + a_side[2]);
+                ss->side.pid = reinterpret_cast<int*>(A + a_side[3]);
+                ss->side_carry = reinterpret_cast<uint32_t*>(A + a_side[4]);
+                ss->side_ctl = reinterpret_cast<uint32_t*>(A + a_side[5]);
+            }
             if (hipHostMalloc(&ss->ctl_host, 64) != hipSuccess)
                 return cleanup(fail(PT_E_OOM, "host allocation failed (round counters)"));
         }
@@ -1371,6 +1405,8 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     bool sparse = ss->n_slots < ss->path_sparse;
     // the cooperative engine once the chains are few (before the first count: the pixels)
     uint32_t chains = ss->n_slots;
+    bool early_done = false, counted = false;
+    hipEvent_t early_end = nullptr, early_taken = nullptr;
     for (uint32_t guard = 0;; ++guard) {
         if (chains <= ss->coop_max) {
             // the cooperative engine runs every remaining chain to the end of the pass, one launch
@@ -1439,6 +1475,53 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             }
             break;
         }
+        // the early cooperative launch (once per pass): the heaviest chains leave the path
+        // engine for a cooperative launch on the second stream, which runs them to the end
+        // of the pass beside the path rounds (those take the rest through wp.pin)
+        // (only after a count: before the first one `chains` is the slot count, not the
+        // queue's, and every pixel has the same samples left)
+        if (ss->early_k && counted && !early_done && chains < ss->early_at && chains > ss->coop_max) {
+            early_done = true;
+            const uint32_t k = std::min(ss->early_k, chains / 4u);
+            if (k) {
+                if (!ss->side_stream && take_stream(ss->dev, &ss->side_stream) != hipSuccess)
+                    return fail(PT_E_HIP, "stream creation failed");
+                wp.parity = p;
+                wp.order_cur = ss->order;
+                wp.order = ss->order + 2 * PT_ORDER_BUCKETS;
+                HIP_TRY(pt_launch_coop_order(wp, chains, ss->stream));
+                HIP_TRY(hipMemsetAsync(ss->side_ctl, 0, 8 * PT_CTL_SET, ss->stream));
+                HIP_TRY(pt_launch_side_take(wp, k, ss->side, ss->side_carry, ss->side_ctl, ss->stream));
+                // (the event lives until the pass ends: the side stream's wait must not
+                // outlive it)
+                HIP_TRY(hipEventCreateWithFlags(&early_taken, hipEventDisableTiming));
+                HIP_TRY(hipEventRecord(early_taken, ss->stream));
+                HIP_TRY(hipStreamWaitEvent(ss->side_stream, early_taken, 0));
+                pt::WaveParams sp = wp;
+                sp.fq[0] = ss->side;
+                sp.cq[0] = ss->side_carry;
+                sp.ctl = ss->side_ctl;
+                sp.parity = 0u;
+                sp.order = sp.order_cur = nullptr;
+                sp.pin = nullptr;
+                hipEvent_t i0, i1;
+                HIP_TRY(hipEventCreate(&i0));
+                HIP_TRY(hipEventCreate(&i1));
+                ss->pending_isect.emplace_back(i0, i1);
+                ss->pending_isect_coop.resize(ss->pending_isect.size(), false);
+                ss->pending_isect_coop.back() = true;
+                ss->isect_launches++;
+                ss->coop_launches++;
+                const bool big = ss->depth > QC_FOLD || s->planes.size() > QC_NPL || s->emitters.size() > QC_NEM;
+                HIP_TRY(pt_launch_coop(sp, ss->early_wg * (ss->coop_grid / 8u), 8u, big, ss->side_stream, i0, i1));
+                if (!early_end) HIP_TRY(hipEventCreateWithFlags(&early_end, hipEventDisableTiming));
+                HIP_TRY(hipEventRecord(early_end, ss->side_stream));
+                // the next path round takes the other chains: items k .. chains of the order
+                wp.pin = wp.order + k;
+                wp.pin_n = chains - k;
+                wp.order = wp.order_cur = nullptr;
+            }
+        }
         for (uint32_t r = 0; r < batch; ++r) {
             wp.parity = p;
             const std::string wgps = tune_str("wgprof");
@@ -1468,6 +1551,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 }
             }
             HIP_TRY(pt_launch_path_round(wp, grid, 64u, ss->stream, sparse, i0, i1));
+            wp.pin = nullptr;   // (only the round right after the early launch skips its chains)
             if (wp.wg_prof) {
                 uint32_t cnt[2][8];
                 HIP_TRY(hipMemcpyAsync(cnt[0], ss->ctl + PT_CTL_SET * p, 32, hipMemcpyDeviceToHost, ss->stream));
@@ -1514,11 +1598,22 @@ int trace_wave(pt_session* ss, uint32_t spp) {
         if (ss->ctl_host[pt::C_FRESH] == 0u && ss->ctl_host[pt::C_CARRY] == 0u) break;
         if (guard > 100000u) return fail(PT_E_HIP, "wavefront rounds did not drain");
         chains = ss->ctl_host[pt::C_FRESH] + ss->ctl_host[pt::C_CARRY];
+        counted = true;
         // near the cooperative hand-over every round is counted (the tail's rounds take ms)
         batch = chains > 4096u && chains > 4u * ss->coop_max ? ss->round_batch : (chains > 4096u ? 1u : 2u);
         sparse = chains < ss->path_sparse;
     }
+    if (early_end) {
+        // the pass ends when the early cooperative launch has run its chains to the end too
+        HIP_TRY(hipStreamWaitEvent(ss->stream, early_end, 0));
+    }
     HIP_TRY(hipEventRecord(e1, ss->stream));
+    if (early_end) {
+        // (both streams past the events before they go)
+        HIP_TRY(hipStreamSynchronize(ss->side_stream));
+        (void)hipEventDestroy(early_end);
+        (void)hipEventDestroy(early_taken);
+    }
     ss->pending.emplace_back(e0, e1);
     ss->samples_done += spp;
     return PT_OK;
@@ -1702,10 +1797,12 @@ void pt_session_free(pt_session* ss) {
     (void)hipFree(ss->rad); (void)hipFree(ss->wg_prof);
     if (ss->ctl_host) (void)hipHostFree(ss->ctl_host);
     if (ss->prog_host) (void)hipHostFree(ss->prog_host);
-    if (ss->stream) {
+    if (ss->side_stream) (void)hipStreamSynchronize(ss->side_stream);
+    if (ss->stream || ss->side_stream) {
         // back to the device's pool for the next session (no destroy/create per render)
         std::lock_guard<std::mutex> lk(g_spare_mu);
-        g_spare_streams[ss->dev].push_back(ss->stream);
+        if (ss->stream) g_spare_streams[ss->dev].push_back(ss->stream);
+        if (ss->side_stream) g_spare_streams[ss->dev].push_back(ss->side_stream);
     }
     delete ss;
 }
@@ -1985,7 +2082,7 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
         // per-rank phase times (the CLI's PT_STATS=2): set-up = the device's scene upload (if
         // this session did it) + the session's buffers and init kernel
         for (int g = 0; g < ngpu; ++g)
-            fprintf(stderr, "pt_render rank %d/%d: setup_ms=%.1f scene_upload_ms=%.1f wait_ms=%.1f render_ms=%.1f "
+            fprintf(stderr, "pt_render rank %d/%d: setup_ms=%.1f scene_upload_ms=%.3f wait_ms=%.1f render_ms=%.1f "
                     "resolve_ms=%.1f\n", g, ngpu, ph[(size_t)g].setup, ph[(size_t)g].upload, ph[(size_t)g].wait,
                     ph[(size_t)g].render, ph[(size_t)g].resolve);
         fprintf(stderr, "pt_render gather_ms=%.1f path=%s\n", gather_ms, agg.gather_rccl ? "rccl" : "host");

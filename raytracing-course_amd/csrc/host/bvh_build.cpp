@@ -102,8 +102,35 @@ struct Builder {
         float k;
         uint32_t i;
     };
-    void sort_axis(uint32_t first, uint32_t last, int axis, std::vector<KI>& tmp) {
-        tmp.resize(last - first);
+    // When every key of the range is equal (a mesh given in absolute coordinates with
+    // POSITION 0 0 0: every dragon triangle), each comparison is false and introsort
+    // moves the elements by a permutation of the range that depends on its length
+    // alone.  A node sorts its range four times (three axes and the re-sort), so the
+    // permutation is computed once -- std::sort of the identity under the same
+    // all-false comparisons -- and applied four times.
+    struct EqPerm {
+        uint32_t n = 0;
+        std::vector<uint32_t> p;   // sorted position j takes the element at p[j]
+    };
+    void sort_axis(uint32_t first, uint32_t last, int axis, std::vector<KI>& tmp, EqPerm& eq) {
+        const uint32_t n = last - first;
+        const float k0 = key[3 * (size_t)perm[first] + axis];
+        bool equal = true;
+        for (uint32_t j = first + 1; j < last && equal; ++j) equal = !(key[3 * (size_t)perm[j] + axis] < k0) &&
+                                                                   !(k0 < key[3 * (size_t)perm[j] + axis]);
+        if (equal && n > 16u) {
+            if (eq.n != n) {
+                eq.n = n;
+                eq.p.resize(n);
+                for (uint32_t j = 0; j < n; ++j) eq.p[j] = j;
+                std::sort(eq.p.begin(), eq.p.end(), [](uint32_t, uint32_t) { return false; });
+            }
+            tmp.resize(n);
+            for (uint32_t j = 0; j < n; ++j) tmp[j].i = perm[first + eq.p[j]];
+            for (uint32_t j = 0; j < n; ++j) perm[first + j] = tmp[j].i;
+            return;
+        }
+        tmp.resize(n);
         for (uint32_t j = first; j < last; ++j) tmp[j - first] = KI{key[3 * (size_t)perm[j] + axis], perm[j]};
         std::sort(tmp.begin(), tmp.end(), [](const KI& u, const KI& v) { return u.k < v.k; });
         for (uint32_t j = first; j < last; ++j) perm[j] = tmp[j - first].i;
@@ -115,6 +142,7 @@ struct Builder {
     // front of the right one: the same preorder as the sequential recursion.
     uint32_t build(uint32_t first, uint32_t last, std::vector<HNode>& nodes, int spawn) {
         thread_local std::vector<KI> tmp;
+        thread_local EqPerm eq;
         BB bb;
         for (uint32_t i = first; i < last; ++i) extend_bb(bb, box[perm[i]]);
         HNode cur;
@@ -129,7 +157,7 @@ struct Builder {
         float opt[3] = {kInf, kInf, kInf};
         uint32_t cuts[3] = {0, 0, 0};
         for (int axis = 0; axis < 3; ++axis) {
-            sort_axis(first, last, axis, tmp);
+            sort_axis(first, last, axis, tmp, eq);
             BB pref = box[perm[first]];
             for (uint32_t cut = first + 1; cut < last; ++cut) {
                 cutq[cut] = calc_s(pref) * (float)(cut - first);
@@ -151,7 +179,7 @@ struct Builder {
         uint32_t cut = 0;
         for (int axis = 0; axis < 3; ++axis) {
             if (optimum == opt[axis]) {
-                sort_axis(first, last, axis, tmp);  // the reference re-sorts (and may permute again)
+                sort_axis(first, last, axis, tmp, eq);  // the reference re-sorts (and may permute again)
                 cut = cuts[axis];
                 break;
             }

@@ -363,7 +363,10 @@ TUNE_KEYS = ["wg_per_cu=2", "wg_per_cu=1", "runend=1000000", "sparse_steps=2", "
              "lowq=100000000,lowq_wg=1", "lowq=100000000,lowq_probe_every=1,lowq_probe_min=2,lowq_aux_extra=2",
              "cap=64", "batch=1", "batch=64", "roundlog=1", "roundlog=2", "prepstats=1",
              # the cooperative engine after the path rounds, intake in queue order / by samples left
-             "coop=300,coop_order=0", "coop=300,coop_order=1"]
+             "coop=300,coop_order=0", "coop=300,coop_order=1",
+             # the early cooperative launch on a second stream (the heaviest chains, from the first
+             # count on), beside the path rounds
+             "coop=300,early=1,early_at=100000000", "coop=300,early=64,early_at=100000000,early_wg=2"]
 
 
 @pytest.mark.parametrize("tune", TUNE_KEYS)
