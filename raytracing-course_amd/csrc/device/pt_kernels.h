@@ -82,7 +82,8 @@ enum : uint32_t { PE_LIVE = 0u, PE_MISS = 1u, PE_CUT = 2u, PE_TERM = 3u };
 
 // round counters: set p = ctl + PT_CTL_SET * p; the work-batch heads are one per
 // XCD, each on its own 128-B line (C_HEADS + 32 x)
-enum : uint32_t { C_FRESH = 0u, C_CARRY = 1u, C_DONE = 3u, C_EXACT = 4u, C_FRONT = 5u, C_BACK = 6u, C_HEADS = 32u };
+enum : uint32_t { C_FRESH = 0u, C_CARRY = 1u, C_DONE = 3u, C_EXACT = 4u, C_FRONT = 5u, C_BACK = 6u, C_WGDONE = 7u,
+                  C_HEADS = 32u };   // C_WGDONE: k_wpath workgroups that have finished the round
 #define PT_CTL_SET 288u          // words per counter set (C_HEADS + 8 x 32)
 // statistics counters: one copy per XCD (PT_CTR_COPIES x PT_CTR_STRIDE u64), summed by the host
 #define PT_CTR_COPIES 8u
@@ -137,6 +138,14 @@ struct WaveParams {
     // launch took the first entries of the intake order)
     const uint32_t* pin;
     uint32_t pin_n;
+    // a cooperative launch beside a path round (the early launch): it stops at a chain
+    // cycle's end once side_stop counts side_stop_n finished path workgroups, and yields its
+    // chains as suspended queries at their start (q_init_pre: the ray was counted when it was
+    // first taken) to yield_cq (counter yield_ctr: the path round's next carry queue)
+    const uint32_t* side_stop;
+    uint32_t side_stop_n;
+    uint32_t* yield_cq;
+    uint32_t* yield_ctr;
 };
 #define PT_ORDER_BUCKETS 256u
 
@@ -228,5 +237,5 @@ hipError_t pt_launch_side_take(pt::WaveParams p, uint32_t k, pt::RayQ side, uint
 // team = lanes per chain (8 -- the default --, 16, 32 or 64)
 // big: the scene exceeds the LDS tables (QC_FOLD / QC_NPL / QC_NEM; team 8 or 64 then)
 hipError_t pt_launch_coop(pt::WaveParams p, uint32_t grid, uint32_t team, bool big, hipStream_t s,
-                          hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
+                          hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, uint32_t waves = QC_WAVES);
 hipError_t pt_launch_resolve(const pt::ResolveParams& p, uint32_t n_tiles, hipStream_t s);

@@ -846,6 +846,12 @@ __global__ void __launch_bounds__(PT_PATH_WG) __attribute__((amdgpu_waves_per_eu
     const uint32_t wave = threadIdx.x >> 6;
     if (wave == PT_NQ) path_shade_wave(P, L);
     else path_query_wave<SPARSE>(P, L, wave);
+    // the round's finished workgroups (an early cooperative launch beside this round stops
+    // once all are done: WaveParams::side_stop)
+    __syncthreads();
+    if (threadIdx.x == 0u)
+        __hip_atomic_fetch_add(P.ctl + PT_CTL_SET * (1u - P.parity) + C_WGDONE, 1u, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---- cooperative engine (end of a pass) ---------------------------------------
@@ -1257,10 +1263,12 @@ __device__ __forceinline__ bool coop_shade(const WaveParams& P, const QcScene& Q
 // BIG: a scene beyond the LDS tables (RAY_DEPTH > QC_FOLD, more than QC_NPL planes
 // or QC_NEM emitters): the rest of them from HBM (a separate instantiation, so the
 // common case carries none of that code)
-template <uint32_t T, bool BIG>
-__global__ void __launch_bounds__(64u * QC_WAVES) __attribute__((amdgpu_waves_per_eu(QC_WAVES_PER_EU, QC_WAVES_PER_EU)))
+// W: waves per workgroup (QC_WAVES; the early launch beside the low-chain path rounds may
+// use 6: two path workgroups and one of 6 waves fill a CU's 12 wave slots and 158 KB of LDS)
+template <uint32_t T, bool BIG, uint32_t W = QC_WAVES>
+__global__ void __launch_bounds__(64u * W) __attribute__((amdgpu_waves_per_eu(QC_WAVES_PER_EU, QC_WAVES_PER_EU)))
 k_wcoop(WaveParams P) {
-    __shared__ QcTeamLds<T> Ls[QC_WAVES * (64u / T)];
+    __shared__ QcTeamLds<T> Ls[W * (64u / T)];
     __shared__ QcScene Q;
     const uint32_t lane = lane_id(), tl = lane % T, tbase = lane - tl;
     QcTeamLds<T>& L = Ls[(threadIdx.x >> 6) * (64u / T) + lane / T];
@@ -1303,6 +1311,36 @@ k_wcoop(WaveParams P) {
     px.R.saved_ok = 0u;
     px.nv = px.done = 0u;
     for (;;) {
+        if (P.side_stop) {
+            // beside a path round: once its workgroups have all finished, the chains leave at
+            // this chain cycle's end -- each team's next query, as a suspended query at its
+            // start, to the round's next carry queue (a resumed query is not counted again: its
+            // ray was counted when first taken), its pixel state and the current path's fold
+            // records to HBM (the path engine continues the path from there)
+            uint32_t fin = 0u;
+            if (lane == 0u) fin = __hip_atomic_load(P.side_stop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            fin = __builtin_amdgcn_readfirstlane(fin);
+            if (fin >= P.side_stop_n) {
+                const uint32_t k = wave_append(P.yield_ctr, have && tl == 0u);
+                if (have && tl == 0u) {
+                    Query q;
+                    q_init_pre(ray, Pt, pid, pre, q);
+                    uint32_t* w = P.yield_cq + (size_t)k * P.carry_words;
+                    *reinterpret_cast<Query*>(w) = q;
+                    w[sizeof(Query) / 4u] = slot;
+                    PixelHot hot;
+                    hot.R = px.R;
+                    hot.nv = px.nv;
+                    hot.done = px.done;
+                    store_hot(P.st, slot, hot);
+                    P.st.rec[2u * slot + 1u] = L.sum;
+                }
+                const uint32_t nv = __shfl(px.nv, (int)tbase, 64);
+                if (have && tl < nv && (!BIG || tl < QC_FOLD)) P.st.fold[(size_t)slot * P.st.depth + tl] = L.fold[tl];
+                have = false;
+                exhausted = true;
+            }
+        }
         // teams without a chain take the next one (queue order: carry, then fresh)
         const bool need = !have && !exhausted;
         if (__ballot(need) != 0ull) {
@@ -1620,12 +1658,16 @@ hipError_t pt_launch_side_take(pt::WaveParams p, uint32_t k, pt::RayQ side, uint
 }
 
 hipError_t pt_launch_coop(pt::WaveParams p, uint32_t grid, uint32_t team, bool big, hipStream_t s, hipEvent_t e0,
-                          hipEvent_t e1) {
+                          hipEvent_t e1, uint32_t waves) {
     hipError_t e = hipMemsetAsync(p.ctl + PT_CTL_SET * (1u - p.parity), 0, 4u * PT_CTL_SET, s);
     if (e != hipSuccess) return e;
     p.path = 1u;
     if (e0 && (e = hipEventRecord(e0, s)) != hipSuccess) return e;
-    if (big) {
+    if (waves == 6u && team == 8u) {
+        // (the early launch's 6-wave workgroups)
+        if (big) hipLaunchKernelGGL((pt::k_wcoop<8u, true, 6u>), dim3(grid), dim3(64u * 6u), 0, s, p);
+        else hipLaunchKernelGGL((pt::k_wcoop<8u, false, 6u>), dim3(grid), dim3(64u * 6u), 0, s, p);
+    } else if (big) {
         // (a scene beyond the LDS tables: teams of 8, or whole waves for deep trees)
         if (team == 64u) hipLaunchKernelGGL((pt::k_wcoop<64u, true>), dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
         else hipLaunchKernelGGL((pt::k_wcoop<8u, true>), dim3(grid), dim3(64u * QC_WAVES), 0, s, p);

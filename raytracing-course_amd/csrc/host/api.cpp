@@ -90,12 +90,13 @@ const Rccl& rccl() {
 //                     768 per CU; the mix of the other rounds)
 //   lowq_wg=N         ... and their path workgroups per CU (PT_CMAX chains each; default 2)
 //   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
-//   coop_order=0      the cooperative engine takes its chains in queue order (default: the pixels
-//                     with the most samples left first)
-//   early=K, early_at=N, early_wg=W
-//                     once a pass's chains fall below N (default 768 per CU), its K heaviest chains
-//                     (1: what W cooperative workgroups per CU hold) run in a cooperative launch on a
-//                     second stream beside the path rounds, to the end of the pass (default: off)
+//   coop_order=1      the pass's final cooperative launch takes the pixels with the most samples
+//                     left first (default: queue order)
+//   early=K, early_at=N, early_wg=W, early_waves=V
+//                     once a pass's chains fall below N (default 768 per CU), each path round runs
+//                     its K heaviest chains (1: what W cooperative workgroups of V waves per CU hold,
+//                     V = 4 or 6) in a cooperative launch on a second stream beside it; the launch
+//                     hands its chains back when the round's path workgroups finish (default: off)
 //   cap=N             chains a workgroup may hold
 //   batch=N           round-queue entries a query wave takes per pull (1..64, default 32)
 //   lstack=N          aux stack words a path-engine query may use (default and maximum PT_LSTACK;
@@ -252,11 +253,12 @@ struct pt_session {
     // early cooperative launch: once a pass's chains fall below early_at, the early_k chains
     // with the most samples left run in a cooperative launch on a second stream (early_wg
     // workgroups per CU, beside the path engine's low-chain rounds) to the end of the pass
-    uint32_t early_k = 0, early_at = 0, early_wg = 1;
+    uint32_t early_k = 0, early_at = 0, early_wg = 1, early_waves = 4;
     pt::RayQ side = {};           // its queue (early_k entries) ...
     uint32_t* side_carry = nullptr;   // ... its suspended queries' restart records (early_k x carry_words)
     uint32_t* side_ctl = nullptr;     // ... and its two round-counter sets
     hipStream_t side_stream = nullptr;
+    hipEvent_t side_taken = nullptr, side_end = nullptr;   // its queue is taken / it has stopped
     uint32_t coop_team = 8;       // lanes per chain in the cooperative engine (pure-coop rate, teams of
                                   // 64 / 32 / 16 / 8: 283 / 392 / 572 / 815 Mray/s)
     // every device buffer below lives in one allocation (pt_session_create)
@@ -1179,15 +1181,18 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // above the hand-over
         if (ss->coop_max && !tune_has("sparse")) ss->path_sparse = std::min(ss->path_sparse, ss->coop_max);
         ss->round_batch = (uint32_t)std::max(1, tune_int("round_batch", (int)ss->round_batch));
-        ss->coop_order = tune_int("coop_order", 1) != 0;
+        ss->coop_order = tune_int("coop_order", 0) != 0;
         // Early cooperative launch (teams of 8, QC_WAVES waves per workgroup: 32 chains each):
         // the low-chain rounds leave each CU room for one more workgroup, which the heaviest
         // chains use from then on instead of waiting for the final hand-over
         ss->early_wg = (uint32_t)std::max(1, tune_int("early_wg", 1));
+        ss->early_waves = tune_int("early_waves", 4) == 6 ? 6u : 4u;
         ss->early_at = (uint32_t)std::max(0, tune_int("early_at", (int)(cus * 768u)));
         ss->early_k = (uint32_t)std::max(0, tune_int("early", 0));
-        if (ss->early_k == 1u) ss->early_k = cus * ss->early_wg * QC_WAVES * 8u;   // early=1: what the launch holds
+        if (ss->early_k == 1u) ss->early_k = cus * ss->early_wg * ss->early_waves * 8u;   // early=1: what it holds
         if (!ss->coop_max || ss->coop_team != 8u) ss->early_k = 0;
+        // a round's carry output also takes the early launch's yielded chains
+        ss->carry_cap = (uint32_t)std::min<uint64_t>(n, (uint64_t)ss->lane_cap + ss->early_k);
         {
             static const char* keys[3] = {"probe_every", "probe_min", "aux_extra"};
             static const char* lkeys[3] = {"lowq_probe_every", "lowq_probe_min", "lowq_aux_extra"};
@@ -1405,8 +1410,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     bool sparse = ss->n_slots < ss->path_sparse;
     // the cooperative engine once the chains are few (before the first count: the pixels)
     uint32_t chains = ss->n_slots;
-    bool early_done = false, counted = false;
-    hipEvent_t early_end = nullptr, early_taken = nullptr;
+    bool counted = false;
     for (uint32_t guard = 0;; ++guard) {
         if (chains <= ss->coop_max) {
             // the cooperative engine runs every remaining chain to the end of the pass, one launch
@@ -1475,15 +1479,19 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             }
             break;
         }
-        // the early cooperative launch (once per pass): the heaviest chains leave the path
-        // engine for a cooperative launch on the second stream, which runs them to the end
-        // of the pass beside the path rounds (those take the rest through wp.pin)
+        // The early cooperative launch, beside every low-chain round: the round's heaviest
+        // chains (most samples left) run in a cooperative launch on the second stream while
+        // the path round runs the others (through wp.pin); the launch stops at a chain cycle's
+        // end once the round's path workgroups have all finished, its chains yielded to the
+        // next round's carry queue, and the next round starts when both are done.
         // (only after a count: before the first one `chains` is the slot count, not the
         // queue's, and every pixel has the same samples left)
-        if (ss->early_k && counted && !early_done && chains < ss->early_at && chains > ss->coop_max) {
-            early_done = true;
+        bool side = false;
+        if (ss->early_k && counted && chains < ss->early_at && chains > ss->coop_max) {
             const uint32_t k = std::min(ss->early_k, chains / 4u);
+            const uint32_t grid = chains < ss->lowq && ss->low_grid ? ss->low_grid : ss->path_grid;
             if (k) {
+                side = true;
                 if (!ss->side_stream && take_stream(ss->dev, &ss->side_stream) != hipSuccess)
                     return fail(PT_E_HIP, "stream creation failed");
                 wp.parity = p;
@@ -1492,11 +1500,14 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 HIP_TRY(pt_launch_coop_order(wp, chains, ss->stream));
                 HIP_TRY(hipMemsetAsync(ss->side_ctl, 0, 8 * PT_CTL_SET, ss->stream));
                 HIP_TRY(pt_launch_side_take(wp, k, ss->side, ss->side_carry, ss->side_ctl, ss->stream));
-                // (the event lives until the pass ends: the side stream's wait must not
-                // outlive it)
-                HIP_TRY(hipEventCreateWithFlags(&early_taken, hipEventDisableTiming));
-                HIP_TRY(hipEventRecord(early_taken, ss->stream));
-                HIP_TRY(hipStreamWaitEvent(ss->side_stream, early_taken, 0));
+                // the round's output counters (its finished-workgroup count among them) are zero
+                // before the side launch can look at them
+                uint32_t* out = ss->ctl + PT_CTL_SET * (1u - p);
+                HIP_TRY(hipMemsetAsync(out, 0, 4u * PT_CTL_SET, ss->stream));
+                if (!ss->side_taken) HIP_TRY(hipEventCreateWithFlags(&ss->side_taken, hipEventDisableTiming));
+                if (!ss->side_end) HIP_TRY(hipEventCreateWithFlags(&ss->side_end, hipEventDisableTiming));
+                HIP_TRY(hipEventRecord(ss->side_taken, ss->stream));
+                HIP_TRY(hipStreamWaitEvent(ss->side_stream, ss->side_taken, 0));
                 pt::WaveParams sp = wp;
                 sp.fq[0] = ss->side;
                 sp.cq[0] = ss->side_carry;
@@ -1504,6 +1515,10 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 sp.parity = 0u;
                 sp.order = sp.order_cur = nullptr;
                 sp.pin = nullptr;
+                sp.side_stop = out + pt::C_WGDONE;
+                sp.side_stop_n = grid;
+                sp.yield_cq = wp.cq[1u - p];
+                sp.yield_ctr = out + pt::C_CARRY;
                 hipEvent_t i0, i1;
                 HIP_TRY(hipEventCreate(&i0));
                 HIP_TRY(hipEventCreate(&i1));
@@ -1513,13 +1528,14 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 ss->isect_launches++;
                 ss->coop_launches++;
                 const bool big = ss->depth > QC_FOLD || s->planes.size() > QC_NPL || s->emitters.size() > QC_NEM;
-                HIP_TRY(pt_launch_coop(sp, ss->early_wg * (ss->coop_grid / 8u), 8u, big, ss->side_stream, i0, i1));
-                if (!early_end) HIP_TRY(hipEventCreateWithFlags(&early_end, hipEventDisableTiming));
-                HIP_TRY(hipEventRecord(early_end, ss->side_stream));
-                // the next path round takes the other chains: items k .. chains of the order
+                HIP_TRY(pt_launch_coop(sp, ss->early_wg * (ss->coop_grid / 8u), 8u, big, ss->side_stream, i0, i1,
+                                       ss->early_waves));
+                HIP_TRY(hipEventRecord(ss->side_end, ss->side_stream));
+                // the path round takes the other chains: items k .. chains of the order
                 wp.pin = wp.order + k;
                 wp.pin_n = chains - k;
                 wp.order = wp.order_cur = nullptr;
+                batch = 1u;   // (the next round reads what the side launch yields)
             }
         }
         for (uint32_t r = 0; r < batch; ++r) {
@@ -1551,7 +1567,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 }
             }
             HIP_TRY(pt_launch_path_round(wp, grid, 64u, ss->stream, sparse, i0, i1));
-            wp.pin = nullptr;   // (only the round right after the early launch skips its chains)
+            wp.pin = nullptr;   // (only the round beside the early launch skips its chains)
             if (wp.wg_prof) {
                 uint32_t cnt[2][8];
                 HIP_TRY(hipMemcpyAsync(cnt[0], ss->ctl + PT_CTL_SET * p, 32, hipMemcpyDeviceToHost, ss->stream));
@@ -1571,6 +1587,8 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             ss->rounds++;
             p ^= 1u;
         }
+        // (a side launch yields into this round's output: the count waits for it)
+        if (side) HIP_TRY(hipStreamWaitEvent(ss->stream, ss->side_end, 0));
         HIP_TRY(hipMemcpyAsync(ss->ctl_host, ss->ctl + PT_CTL_SET * p, 8, hipMemcpyDeviceToHost, ss->stream));
         if (wp.progress) {
             // report the finished samples while the rounds run
@@ -1603,17 +1621,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
         batch = chains > 4096u && chains > 4u * ss->coop_max ? ss->round_batch : (chains > 4096u ? 1u : 2u);
         sparse = chains < ss->path_sparse;
     }
-    if (early_end) {
-        // the pass ends when the early cooperative launch has run its chains to the end too
-        HIP_TRY(hipStreamWaitEvent(ss->stream, early_end, 0));
-    }
     HIP_TRY(hipEventRecord(e1, ss->stream));
-    if (early_end) {
-        // (both streams past the events before they go)
-        HIP_TRY(hipStreamSynchronize(ss->side_stream));
-        (void)hipEventDestroy(early_end);
-        (void)hipEventDestroy(early_taken);
-    }
     ss->pending.emplace_back(e0, e1);
     ss->samples_done += spp;
     return PT_OK;
@@ -1798,6 +1806,8 @@ void pt_session_free(pt_session* ss) {
     if (ss->ctl_host) (void)hipHostFree(ss->ctl_host);
     if (ss->prog_host) (void)hipHostFree(ss->prog_host);
     if (ss->side_stream) (void)hipStreamSynchronize(ss->side_stream);
+    if (ss->side_taken) (void)hipEventDestroy(ss->side_taken);
+    if (ss->side_end) (void)hipEventDestroy(ss->side_end);
     if (ss->stream || ss->side_stream) {
         // back to the device's pool for the next session (no destroy/create per render)
         std::lock_guard<std::mutex> lk(g_spare_mu);
