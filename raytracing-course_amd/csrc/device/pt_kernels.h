@@ -237,5 +237,5 @@ hipError_t pt_launch_side_take(pt::WaveParams p, uint32_t k, pt::RayQ side, uint
 // team = lanes per chain (8 -- the default --, 16, 32 or 64)
 // big: the scene exceeds the LDS tables (QC_FOLD / QC_NPL / QC_NEM; team 8 or 64 then)
 hipError_t pt_launch_coop(pt::WaveParams p, uint32_t grid, uint32_t team, bool big, hipStream_t s,
-                          hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, uint32_t waves = QC_WAVES);
+                          hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t pt_launch_resolve(const pt::ResolveParams& p, uint32_t n_tiles, hipStream_t s);

@@ -1263,12 +1263,10 @@ __device__ __forceinline__ bool coop_shade(const WaveParams& P, const QcScene& Q
 // BIG: a scene beyond the LDS tables (RAY_DEPTH > QC_FOLD, more than QC_NPL planes
 // or QC_NEM emitters): the rest of them from HBM (a separate instantiation, so the
 // common case carries none of that code)
-// W: waves per workgroup (QC_WAVES; the early launch beside the low-chain path rounds may
-// use 6: two path workgroups and one of 6 waves fill a CU's 12 wave slots and 158 KB of LDS)
-template <uint32_t T, bool BIG, uint32_t W = QC_WAVES>
-__global__ void __launch_bounds__(64u * W) __attribute__((amdgpu_waves_per_eu(QC_WAVES_PER_EU, QC_WAVES_PER_EU)))
+template <uint32_t T, bool BIG>
+__global__ void __launch_bounds__(64u * QC_WAVES) __attribute__((amdgpu_waves_per_eu(QC_WAVES_PER_EU, QC_WAVES_PER_EU)))
 k_wcoop(WaveParams P) {
-    __shared__ QcTeamLds<T> Ls[W * (64u / T)];
+    __shared__ QcTeamLds<T> Ls[QC_WAVES * (64u / T)];
     __shared__ QcScene Q;
     const uint32_t lane = lane_id(), tl = lane % T, tbase = lane - tl;
     QcTeamLds<T>& L = Ls[(threadIdx.x >> 6) * (64u / T) + lane / T];
@@ -1658,16 +1656,12 @@ hipError_t pt_launch_side_take(pt::WaveParams p, uint32_t k, pt::RayQ side, uint
 }
 
 hipError_t pt_launch_coop(pt::WaveParams p, uint32_t grid, uint32_t team, bool big, hipStream_t s, hipEvent_t e0,
-                          hipEvent_t e1, uint32_t waves) {
+                          hipEvent_t e1) {
     hipError_t e = hipMemsetAsync(p.ctl + PT_CTL_SET * (1u - p.parity), 0, 4u * PT_CTL_SET, s);
     if (e != hipSuccess) return e;
     p.path = 1u;
     if (e0 && (e = hipEventRecord(e0, s)) != hipSuccess) return e;
-    if (waves == 6u && team == 8u) {
-        // (the early launch's 6-wave workgroups)
-        if (big) hipLaunchKernelGGL((pt::k_wcoop<8u, true, 6u>), dim3(grid), dim3(64u * 6u), 0, s, p);
-        else hipLaunchKernelGGL((pt::k_wcoop<8u, false, 6u>), dim3(grid), dim3(64u * 6u), 0, s, p);
-    } else if (big) {
+    if (big) {
         // (a scene beyond the LDS tables: teams of 8, or whole waves for deep trees)
         if (team == 64u) hipLaunchKernelGGL((pt::k_wcoop<64u, true>), dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
         else hipLaunchKernelGGL((pt::k_wcoop<8u, true>), dim3(grid), dim3(64u * QC_WAVES), 0, s, p);

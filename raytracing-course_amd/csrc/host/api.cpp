@@ -92,11 +92,11 @@ const Rccl& rccl() {
 //   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
 //   coop_order=1      the pass's final cooperative launch takes the pixels with the most samples
 //                     left first (default: queue order)
-//   early=K, early_at=N, early_wg=W, early_waves=V
+//   early=K, early_at=N, early_wg=W
 //                     once a pass's chains fall below N (default 768 per CU), each path round runs
-//                     its K heaviest chains (1: what W cooperative workgroups of V waves per CU hold,
-//                     V = 4 or 6) in a cooperative launch on a second stream beside it; the launch
-//                     hands its chains back when the round's path workgroups finish (default: off)
+//                     its K heaviest chains (1: what W cooperative workgroups per CU hold) in a
+//                     cooperative launch on a second stream beside it; the launch hands its chains
+//                     back when the round's path workgroups finish (default: 1; 0 = off)
 //   cap=N             chains a workgroup may hold
 //   batch=N           round-queue entries a query wave takes per pull (1..64, default 32)
 //   lstack=N          aux stack words a path-engine query may use (default and maximum PT_LSTACK;
@@ -253,7 +253,7 @@ struct pt_session {
     // early cooperative launch: once a pass's chains fall below early_at, the early_k chains
     // with the most samples left run in a cooperative launch on a second stream (early_wg
     // workgroups per CU, beside the path engine's low-chain rounds) to the end of the pass
-    uint32_t early_k = 0, early_at = 0, early_wg = 1, early_waves = 4;
+    uint32_t early_k = 0, early_at = 0, early_wg = 1;
     pt::RayQ side = {};           // its queue (early_k entries) ...
     uint32_t* side_carry = nullptr;   // ... its suspended queries' restart records (early_k x carry_words)
     uint32_t* side_ctl = nullptr;     // ... and its two round-counter sets
@@ -273,6 +273,7 @@ struct pt_session {
     uint32_t carry_cap = 0, carry_words = 0;
     uint32_t* ctl = nullptr;      // 2 x PT_CTL_SET round counters
     uint32_t* ctl_host = nullptr; // pinned copy of one counter set
+    double roundlog_t = 0.0;      // (roundlog=2: the last round's end, host clock)
     uint32_t shade_grid = 0, rounds = 0;
     hipStream_t stream = nullptr;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, pending_isect;
@@ -1186,10 +1187,9 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // the low-chain rounds leave each CU room for one more workgroup, which the heaviest
         // chains use from then on instead of waiting for the final hand-over
         ss->early_wg = (uint32_t)std::max(1, tune_int("early_wg", 1));
-        ss->early_waves = tune_int("early_waves", 4) == 6 ? 6u : 4u;
         ss->early_at = (uint32_t)std::max(0, tune_int("early_at", (int)(cus * 768u)));
-        ss->early_k = (uint32_t)std::max(0, tune_int("early", 0));
-        if (ss->early_k == 1u) ss->early_k = cus * ss->early_wg * ss->early_waves * 8u;   // early=1: what it holds
+        ss->early_k = (uint32_t)std::max(0, tune_int("early", 1));
+        if (ss->early_k == 1u) ss->early_k = cus * ss->early_wg * QC_WAVES * 8u;   // early=1: what it holds
         if (!ss->coop_max || ss->coop_team != 8u) ss->early_k = 0;
         // a round's carry output also takes the early launch's yielded chains
         ss->carry_cap = (uint32_t)std::min<uint64_t>(n, (uint64_t)ss->lane_cap + ss->early_k);
@@ -1325,6 +1325,10 @@ int pt_session_layout(const pt_session* ss, uint32_t* n_tiles, uint64_t* packed_
 }
 
 namespace {
+double wall_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int trace_wave(pt_session* ss, uint32_t spp) {
     const DevScene& ds = *ss->ds;
     const pt_scene* s = ss->sc;
@@ -1400,6 +1404,10 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     HIP_TRY(hipEventCreate(&e1));
     HIP_TRY(hipEventRecord(e0, ss->stream));
     HIP_TRY(pt_launch_wave_start(wp, ss->stream));
+    if (tune_int("roundlog", 0) == 2) {
+        HIP_TRY(hipStreamSynchronize(ss->stream));
+        ss->roundlog_t = wall_ms();
+    }
     // rounds until no fresh ray and no suspended query is left; counts are
     // checked every few rounds (empty rounds are cheap, syncs are not free)
     // (the first round is counted alone: it ends once the pass's work is handed out, and
@@ -1528,8 +1536,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 ss->isect_launches++;
                 ss->coop_launches++;
                 const bool big = ss->depth > QC_FOLD || s->planes.size() > QC_NPL || s->emitters.size() > QC_NEM;
-                HIP_TRY(pt_launch_coop(sp, ss->early_wg * (ss->coop_grid / 8u), 8u, big, ss->side_stream, i0, i1,
-                                       ss->early_waves));
+                HIP_TRY(pt_launch_coop(sp, ss->early_wg * (ss->coop_grid / 8u), 8u, big, ss->side_stream, i0, i1));
                 HIP_TRY(hipEventRecord(ss->side_end, ss->side_stream));
                 // the path round takes the other chains: items k .. chains of the order
                 wp.pin = wp.order + k;
@@ -1609,9 +1616,12 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 if (rec[2 * i].w < wp.target) lag.push_back(wp.target - rec[2 * i].w);
             std::sort(lag.begin(), lag.end());
             const size_t m = lag.size();
-            fprintf(stderr, "round %u chains %u+%u unfinished %zu lag p50 %u p90 %u p99 %u max %u\n", ss->rounds,
-                    ss->ctl_host[pt::C_FRESH], ss->ctl_host[pt::C_CARRY], m, m ? lag[m / 2] : 0u,
-                    m ? lag[m * 9 / 10] : 0u, m ? lag[m * 99 / 100] : 0u, m ? lag[m - 1] : 0u);
+            const double now = wall_ms();
+            fprintf(stderr, "round %u chains %u -> %u+%u (%s%s) %.2f ms; unfinished %zu lag p50 %u p90 %u p99 %u max %u\n",
+                    ss->rounds, chains, ss->ctl_host[pt::C_FRESH], ss->ctl_host[pt::C_CARRY],
+                    chains < ss->lowq ? "low" : "full", side ? "+side" : "", now - ss->roundlog_t, m,
+                    m ? lag[m / 2] : 0u, m ? lag[m * 9 / 10] : 0u, m ? lag[m * 99 / 100] : 0u, m ? lag[m - 1] : 0u);
+            ss->roundlog_t = wall_ms();
         }
         if (ss->ctl_host[pt::C_FRESH] == 0u && ss->ctl_host[pt::C_CARRY] == 0u) break;
         if (guard > 100000u) return fail(PT_E_HIP, "wavefront rounds did not drain");
