@@ -101,7 +101,8 @@ const Rccl& rccl() {
 //   batch=N           round-queue entries a query wave takes per pull (1..64, default 32)
 //   lstack=N          aux stack words a path-engine query may use (default and maximum PT_LSTACK;
 //                     a query needing more takes the exact DFS)
-//   roundlog=1|2      per-round kernel times / pixels' remaining samples on stderr
+//   roundlog=1|2|3    per-round kernel times / each round's chains, wall time and rays / and the
+//                     pixels' remaining samples, on stderr
 //   wgprof=FILE       per-workgroup timelines (-DPT_WPROF builds)
 //   cprof=1           per-phase cycles of the cooperative engine on stderr (-DPT_CPROF builds)
 //   qstats=FILE       per-query work counters of the host self-test render
@@ -273,7 +274,8 @@ struct pt_session {
     uint32_t carry_cap = 0, carry_words = 0;
     uint32_t* ctl = nullptr;      // 2 x PT_CTL_SET round counters
     uint32_t* ctl_host = nullptr; // pinned copy of one counter set
-    double roundlog_t = 0.0;      // (roundlog=2: the last round's end, host clock)
+    double roundlog_t = 0.0;      // (roundlog>=2: the last round's end, host clock, and the rays by then)
+    unsigned long long roundlog_rays = 0;
     uint32_t shade_grid = 0, rounds = 0;
     hipStream_t stream = nullptr;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, pending_isect;
@@ -1404,9 +1406,13 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     HIP_TRY(hipEventCreate(&e1));
     HIP_TRY(hipEventRecord(e0, ss->stream));
     HIP_TRY(pt_launch_wave_start(wp, ss->stream));
-    if (tune_int("roundlog", 0) == 2) {
+    if (tune_int("roundlog", 0) >= 2) {
         HIP_TRY(hipStreamSynchronize(ss->stream));
         ss->roundlog_t = wall_ms();
+        unsigned long long cc[PT_CTR_COPIES * PT_CTR_STRIDE];
+        HIP_TRY(hipMemcpy(cc, ss->counters, sizeof(cc), hipMemcpyDeviceToHost));
+        ss->roundlog_rays = 0;
+        for (uint32_t x = 0; x < PT_CTR_COPIES; ++x) ss->roundlog_rays += cc[PT_CTR_STRIDE * x];
     }
     // rounds until no fresh ray and no suspended query is left; counts are
     // checked every few rounds (empty rounds are cheap, syncs are not free)
@@ -1607,20 +1613,30 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             HIP_TRY(e);
         }
         HIP_TRY(hipStreamSynchronize(ss->stream));
-        if (tune_int("roundlog", 0) == 2) {
-            // diagnostics: how far behind the pass target the unfinished pixels are
-            std::vector<uint4> rec(2ull * ss->n_slots);
-            HIP_TRY(hipMemcpy(rec.data(), ss->st.rec, rec.size() * sizeof(uint4), hipMemcpyDeviceToHost));
-            std::vector<uint32_t> lag;
-            for (uint32_t i = 0; i < ss->n_slots; ++i)
-                if (rec[2 * i].w < wp.target) lag.push_back(wp.target - rec[2 * i].w);
-            std::sort(lag.begin(), lag.end());
-            const size_t m = lag.size();
+        if (tune_int("roundlog", 0) >= 2) {
+            // diagnostics: each round's chains, kind, wall time and rays (roundlog=3: also how
+            // far behind the pass target the unfinished pixels are)
             const double now = wall_ms();
-            fprintf(stderr, "round %u chains %u -> %u+%u (%s%s) %.2f ms; unfinished %zu lag p50 %u p90 %u p99 %u max %u\n",
-                    ss->rounds, chains, ss->ctl_host[pt::C_FRESH], ss->ctl_host[pt::C_CARRY],
-                    chains < ss->lowq ? "low" : "full", side ? "+side" : "", now - ss->roundlog_t, m,
-                    m ? lag[m / 2] : 0u, m ? lag[m * 9 / 10] : 0u, m ? lag[m * 99 / 100] : 0u, m ? lag[m - 1] : 0u);
+            unsigned long long cc[PT_CTR_COPIES * PT_CTR_STRIDE], rays = 0;
+            HIP_TRY(hipMemcpy(cc, ss->counters, sizeof(cc), hipMemcpyDeviceToHost));
+            for (uint32_t x = 0; x < PT_CTR_COPIES; ++x) rays += cc[PT_CTR_STRIDE * x];
+            const double ms = now - ss->roundlog_t;
+            fprintf(stderr, "round %u chains %u -> %u+%u (%s%s) %.2f ms rays %llu %.0f Mray/s", ss->rounds, chains,
+                    ss->ctl_host[pt::C_FRESH], ss->ctl_host[pt::C_CARRY], chains < ss->lowq ? "low" : "full",
+                    side ? "+side" : "", ms, rays - ss->roundlog_rays, (rays - ss->roundlog_rays) / ms / 1e3);
+            ss->roundlog_rays = rays;
+            if (tune_int("roundlog", 0) == 3) {
+                std::vector<uint4> rec(2ull * ss->n_slots);
+                HIP_TRY(hipMemcpy(rec.data(), ss->st.rec, rec.size() * sizeof(uint4), hipMemcpyDeviceToHost));
+                std::vector<uint32_t> lag;
+                for (uint32_t i = 0; i < ss->n_slots; ++i)
+                    if (rec[2 * i].w < wp.target) lag.push_back(wp.target - rec[2 * i].w);
+                std::sort(lag.begin(), lag.end());
+                const size_t m = lag.size();
+                fprintf(stderr, "; unfinished %zu lag p50 %u p90 %u p99 %u max %u", m, m ? lag[m / 2] : 0u,
+                        m ? lag[m * 9 / 10] : 0u, m ? lag[m * 99 / 100] : 0u, m ? lag[m - 1] : 0u);
+            }
+            fprintf(stderr, "\n");
             ss->roundlog_t = wall_ms();
         }
         if (ss->ctl_host[pt::C_FRESH] == 0u && ss->ctl_host[pt::C_CARRY] == 0u) break;
