@@ -367,7 +367,10 @@ TUNE_KEYS = ["wg_per_cu=2", "wg_per_cu=1", "runend=1000000", "sparse_steps=2", "
              # the early cooperative launch on a second stream (the heaviest chains, from the first
              # count on), beside the path rounds
              "coop=300,early=1,early_at=100000000", "coop=300,early=64,early_at=100000000,early_wg=2",
-             "coop=300,early=0", "coop=300,early=1,early_at=100000000,coop_order=1"]
+             "coop=300,early=0", "coop=300,early=1,early_at=100000000,coop_order=1",
+             # diagnostics hooks (their counters are compiled in only with -DPT_CPROF / -DPT_WPROF;
+             # the host side runs in every build)
+             "coop=300,cprof=1", "wgprof=/tmp/pt_wgprof_test.bin"]
 
 
 @pytest.mark.parametrize("tune", TUNE_KEYS)

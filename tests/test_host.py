@@ -198,6 +198,27 @@ def test_coop_integrator_on_host_bit_exact(name, monkeypatch):
     assert got.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
 
 
+def test_query_log_on_host(tmp_path, monkeypatch):
+    """PT_TUNE qstats=FILE: the host render logs one 16-B record per query
+    (aux visits, node records, primitive tests | exact-DFS bit), and the image
+    stays the same."""
+    name = HOST_RENDER[0]
+    m, img, rad = U.golden_image(name)
+    log = tmp_path / "q.bin"
+    monkeypatch.setenv("PT_TUNE", "qstats=%s" % log)
+    with pt.Scene.load(U.golden_scene_path(name)) as s:
+        s.prepare()
+        if m["window"]:
+            x0, y0, w, h = m["window"]
+        else:
+            x0, y0, h, w = 0, 0, img.shape[0], img.shape[1]
+        got = s.selftest_render_host(x0, y0, w, h, traversal=0)
+    assert got.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
+    q = np.fromfile(log, dtype=np.uint32).reshape(-1, 4)
+    assert len(q) >= w * h   # at least one query per sample
+    assert q[:, 0].sum() > 0
+
+
 def _gamma_table():
     with pt.Scene.load(U.scene_path("practice5_1.txt")) as s:
         s.prepare()
