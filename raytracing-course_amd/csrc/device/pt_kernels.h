@@ -83,7 +83,9 @@ enum : uint32_t { PE_LIVE = 0u, PE_MISS = 1u, PE_CUT = 2u, PE_TERM = 3u };
 // round counters: set p = ctl + PT_CTL_SET * p; the work-batch heads are one per
 // XCD, each on its own 128-B line (C_HEADS + 32 x)
 enum : uint32_t { C_FRESH = 0u, C_CARRY = 1u, C_DONE = 3u, C_EXACT = 4u, C_FRONT = 5u, C_BACK = 6u, C_WGDONE = 7u,
-                  C_HEADS = 32u };   // C_WGDONE: k_wpath workgroups that have finished the round
+                  C_DEADLINE = 8u, C_HEADS = 32u };
+// C_WGDONE: k_wpath workgroups that have finished the round; C_DEADLINE: the round's end
+// (low 32 bits of the 100-MHz realtime clock, 0 = not set yet; WaveParams::path_ticks)
 #define PT_CTL_SET 288u          // words per counter set (C_HEADS + 8 x 32)
 // statistics counters: one copy per XCD (PT_CTR_COPIES x PT_CTR_STRIDE u64), summed by the host
 #define PT_CTR_COPIES 8u
@@ -117,6 +119,8 @@ struct WaveParams {
     // path engine (k_wpath): chains continue inside the kernel
     uint32_t path;                // 1 (k_wshade shades the exact-DFS results only)
     uint32_t path_budget;         // loop trips a query wave keeps its chains going after the round's work ran out
+    uint32_t path_ticks;          // ... or, if nonzero, 100-MHz clock ticks after the first wave found it out:
+                                  // every wave of the round stops at that one time
     uint32_t path_runend;         // a round with at most this many chains runs them to the end of the pass
     unsigned long long* progress; // optional host-mapped count of finished samples (progress bar), or null
     uint32_t path_cap;            // chains a workgroup may hold (<= PT_CMAX)

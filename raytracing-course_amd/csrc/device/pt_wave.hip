@@ -196,8 +196,10 @@ __global__ void __launch_bounds__(256) k_wcamera_merge(WaveParams P) {
 // (suspended queries, then fresh rays) second, so a chain keeps going inside the
 // kernel instead of advancing one query per round -- with fewer pixels than
 // lanes (a rank of a multi-GPU render, the end of a pass) the lanes stay busy.
-// Once the round's work is used up a query wave keeps its chains going for
-// `path_budget` more trips, then suspends its queries to the carry queue; the
+// Once the round's work is used up a query wave keeps its chains going until the
+// round's deadline (`path_ticks` after the first wave found the work used up: all
+// waves stop together; or `path_budget` more trips of its own), then suspends its
+// queries to the carry queue; the
 // shade wave, last out, hands the remaining chains' next rays to the fresh queue
 // of the next round.  Rounds then only rebalance chains between workgroups.
 //
@@ -382,6 +384,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     uint32_t bbase = 0u, bleft = 0u;  // this wave's batch of the round's work not yet handed out
     bool exhausted = false;
     uint32_t wpost = 0u;              // trips since the round's work ran out
+    uint32_t deadline = 0u;           // the round's end (path_ticks mode; 0 = not read yet)
     uint32_t trip = 0u;
     uint32_t ptrip = 0u;              // trips since the last probe turn
     const uint32_t wq = qw;                 // this query wave's done ring
@@ -411,7 +414,28 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
             exhausted = __ballot(!used) == 0ull;
         }
         if (exhausted && bleft == 0u) {
-            if (wpost >= budget) {
+            bool over;
+            if (budget == 0xffffffffu) {
+                over = false;
+            } else if (P.path_ticks) {
+                // One deadline for the whole round: the trip counts of workgroups with heavy
+                // and light chains differ, so a per-wave trip budget ends them at different
+                // times and the first ones out wait for the last (a round of a rank of 8:
+                // query waves tripping ~75 % of the round's span)
+                if (deadline == 0u) {
+                    uint32_t d = 0u;
+                    if (lane_id() == 0u) {
+                        const uint32_t want = ((uint32_t)__builtin_amdgcn_s_memrealtime() + P.path_ticks) | 1u;
+                        const uint32_t old = atomicCAS(out + C_DEADLINE, 0u, want);
+                        d = old ? old : want;
+                    }
+                    deadline = __builtin_amdgcn_readfirstlane(d);
+                }
+                over = (int32_t)((uint32_t)__builtin_amdgcn_s_memrealtime() - deadline) >= 0;
+            } else {
+                over = wpost >= budget;
+            }
+            if (over) {
                 // the round is over for this wave: suspend its running queries
                 if (active) {
                     const uint32_t k = wave_append(out + C_CARRY, true);

@@ -73,7 +73,10 @@ const Rccl& rccl() {
 // for a correct or a fast render; the keys exist for A/B runs and diagnostics
 // (INTEGRATION.md "Tuning and diagnostics"):
 //   engine=mega       megakernel instead of the wavefront path engine (replay traversal)
-//   budget=N          path engine: trips a query wave keeps its chains after the round's work ran out
+//   budget_us=N       path engine: a round ends N us after its work ran out, for every wave at once
+//                     (default 5000; 0: each wave after `budget` trips of its own)
+//   budget=N          ... trips a query wave keeps its chains after the round's work ran out, when
+//                     budget_us is 0 or budget alone is given (default 1024)
 //   wg_per_cu=N       path engine: workgroups per CU (grid)
 //   runend=N          a round with at most N chains runs them to the end of the pass
 //   sparse=N          rounds with fewer than N chains run the end-of-pass kernel
@@ -241,7 +244,7 @@ struct pt_session {
     unsigned long long* wg_prof = nullptr;
     // wavefront engine buffers (replay traversal)
     bool wave = false;
-    uint32_t path_grid = 0, path_budget = 1024, path_runend = 0, path_sparse = 0, sparse_steps = 8;
+    uint32_t path_grid = 0, path_budget = 1024, path_ticks = 0, path_runend = 0, path_sparse = 0, sparse_steps = 8;
     uint32_t coop_max = 0, coop_grid = 0, coop_reserve = 0;   // cooperative engine (k_wcoop) at the end of a pass
     uint32_t round_batch = 1;     // rounds launched per count while the chains are far above the hand-over
     // k_wpath's per-trip step mix: {probe_every, probe_min, aux_extra}, and the one of
@@ -1138,6 +1141,9 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // path engine: PT_NQ query waves + 1 shade wave per workgroup, as many workgroups
         // per CU as its waves-per-SIMD occupancy holds (4 SIMDs per CU)
         ss->path_budget = (uint32_t)std::max(1, tune_int("budget", (int)ss->path_budget));
+        // rounds end at one time for every wave (budget_us after the work ran out; 0: each
+        // wave after `budget` trips of its own, also the mode of an explicit budget=N alone)
+        ss->path_ticks = (uint32_t)std::max(0, tune_int("budget_us", tune_has("budget") ? 0 : 5000)) * 100u;
         const int wg_cu = std::max(1, (int)(PT_PATH_WAVES_PER_EU * 4u / (PT_NQ + 1u)));
         ss->path_grid = cus * (uint32_t)std::max(1, tune_int("wg_per_cu", wg_cu));
         // suspended-query records: Query | slot | aux stack, rounded to 16 B.  Only a
@@ -1373,6 +1379,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.aux_stack = std::max<uint32_t>(s->auxw_stack, 1u);
     wp.path = 1u;
     wp.path_budget = ss->path_budget;
+    wp.path_ticks = ss->path_ticks;
     wp.path_runend = ss->path_runend;
     // Chains a workgroup may hold: 5/8 of the pixels' fair share, within
     // [256, PT_CMAX].  Below the share, about a third of the chains wait in the
