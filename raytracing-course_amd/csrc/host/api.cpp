@@ -1143,7 +1143,8 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         ss->path_budget = (uint32_t)std::max(1, tune_int("budget", (int)ss->path_budget));
         // rounds end at one time for every wave (budget_us after the work ran out; 0: each
         // wave after `budget` trips of its own, also the mode of an explicit budget=N alone)
-        ss->path_ticks = (uint32_t)std::max(0, tune_int("budget_us", tune_has("budget") ? 0 : 5000)) * 100u;
+        // (at most 10 s: the device compares 32-bit clock differences as signed)
+        ss->path_ticks = (uint32_t)std::min(10000000, std::max(0, tune_int("budget_us", tune_has("budget") ? 0 : 5000))) * 100u;
         const int wg_cu = std::max(1, (int)(PT_PATH_WAVES_PER_EU * 4u / (PT_NQ + 1u)));
         ss->path_grid = cus * (uint32_t)std::max(1, tune_int("wg_per_cu", wg_cu));
         // suspended-query records: Query | slot | aux stack, rounded to 16 B.  Only a
