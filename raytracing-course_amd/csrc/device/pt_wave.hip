@@ -1320,7 +1320,7 @@ k_wcoop(WaveParams P) {
     uint64_t cp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t cp_start = __builtin_amdgcn_s_memtime();
 #endif
-    bool have = false, exhausted = false;
+    bool have = false, exhausted = false, stopped = false;
     uint32_t slot = 0u;
     Ray ray;
     ray.o = ray.d = mk3(0.f, 0.f, 0.f);
@@ -1361,6 +1361,7 @@ k_wcoop(WaveParams P) {
                 if (have && tl < nv && (!BIG || tl < QC_FOLD)) P.st.fold[(size_t)slot * P.st.depth + tl] = L.fold[tl];
                 have = false;
                 exhausted = true;
+                stopped = true;
             }
         }
         // teams without a chain take the next one (queue order: carry, then fresh)
@@ -1473,6 +1474,49 @@ k_wcoop(WaveParams P) {
         if (P.progress && tl == 0u && prog >= 256u) {
             __hip_atomic_fetch_add(P.progress, (unsigned long long)prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             prog = 0u;
+        }
+    }
+    if (stopped) {
+        // A launch beside a path round that stopped: the work items no team took (a
+        // workgroup that started only after the round's end -- the launch shares the
+        // device with the path round and anything else on it) go to the next round as
+        // they are, their pixels' records untouched in HBM (a fresh ray is counted
+        // here, as the intake would have)
+        for (;;) {
+            const uint32_t gi = wave_append(out + C_HEADS, true);
+            const bool on = gi < n_total;
+            if (__ballot(on) == 0ull) break;
+            Ray r;
+            float rp = PT_INF;
+            int rid = -1;
+            F4 rpre = F4{0.f, 0.f, 0.f, 0.f};
+            uint32_t rslot = 0u;
+            if (on && gi < n_carry) {
+                const uint32_t* w = P.cq[P.parity] + (size_t)gi * P.carry_words;
+                r = reinterpret_cast<const Query*>(w)->ray;
+                rslot = w[sizeof(Query) / 4u];
+                q_planes_e(P.S, PlanesLds<BIG>{Q, P.S}, r, rp, rid);
+                rpre = q_prep(P.S, r);
+            } else if (on) {
+                const uint32_t fi = gi - n_carry;
+                const F4 o = FQ.ro[fi], d = FQ.rd[fi];
+                r.o = mk3(o.x, o.y, o.z);
+                r.d = mk3(d.x, d.y, d.z);
+                rslot = f2u(o.w);
+                rp = d.w;
+                rid = FQ.pid[fi];
+                rpre = FQ.ri[fi];
+                rays++;
+                C.planes += P.S.n_planes;
+            }
+            const uint32_t k2 = wave_append(P.yield_ctr, on);
+            if (on) {
+                Query q;
+                q_init_pre(r, rp, rid, rpre, q);
+                uint32_t* w = P.yield_cq + (size_t)k2 * P.carry_words;
+                *reinterpret_cast<Query*>(w) = q;
+                w[sizeof(Query) / 4u] = rslot;
+            }
         }
     }
     if (P.progress && tl == 0u && prog)

@@ -368,6 +368,9 @@ TUNE_KEYS = ["wg_per_cu=2", "wg_per_cu=1", "runend=1000000", "sparse_steps=2", "
              # count on), beside the path rounds
              "coop=300,early=1,early_at=100000000", "coop=300,early=64,early_at=100000000,early_wg=2",
              "coop=300,early=0", "coop=300,early=1,early_at=100000000,coop_order=1",
+             # more early workgroups than fit beside the round (the late ones find it over and
+             # hand their untaken items on)
+             "coop=300,early=1,early_at=100000000,early_wg=8",
              # diagnostics hooks (their counters are compiled in only with -DPT_CPROF / -DPT_WPROF;
              # the host side runs in every build)
              "coop=300,cprof=1", "wgprof=/tmp/pt_wgprof_test.bin"]
