@@ -74,7 +74,7 @@ const Rccl& rccl() {
 // (INTEGRATION.md "Tuning and diagnostics"):
 //   engine=mega       megakernel instead of the wavefront path engine (replay traversal)
 //   budget_us=N       path engine: a round ends N us after its work ran out, for every wave at once
-//                     (default 5000; 0: each wave after `budget` trips of its own)
+//                     (default 2500; 0: each wave after `budget` trips of its own)
 //   budget=N          ... trips a query wave keeps its chains after the round's work ran out, when
 //                     budget_us is 0 or budget alone is given (default 1024)
 //   wg_per_cu=N       path engine: workgroups per CU (grid)
@@ -1144,7 +1144,7 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // rounds end at one time for every wave (budget_us after the work ran out; 0: each
         // wave after `budget` trips of its own, also the mode of an explicit budget=N alone)
         // (at most 10 s: the device compares 32-bit clock differences as signed)
-        ss->path_ticks = (uint32_t)std::min(10000000, std::max(0, tune_int("budget_us", tune_has("budget") ? 0 : 5000))) * 100u;
+        ss->path_ticks = (uint32_t)std::min(10000000, std::max(0, tune_int("budget_us", tune_has("budget") ? 0 : 2500))) * 100u;
         const int wg_cu = std::max(1, (int)(PT_PATH_WAVES_PER_EU * 4u / (PT_NQ + 1u)));
         ss->path_grid = cus * (uint32_t)std::max(1, tune_int("wg_per_cu", wg_cu));
         // suspended-query records: Query | slot | aux stack, rounded to 16 B.  Only a
