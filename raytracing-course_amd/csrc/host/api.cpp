@@ -93,8 +93,8 @@ const Rccl& rccl() {
 //                     768 per CU; the mix of the other rounds)
 //   lowq_wg=N         ... and their path workgroups per CU (PT_CMAX chains each; default 2)
 //   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
-//   coop_order=1      the pass's final cooperative launch takes the pixels with the most samples
-//                     left first (default: queue order)
+//   coop_order=0      the pass's final cooperative launch takes its chains in queue order (default:
+//                     the pixels with the most samples left first)
 //   early=K, early_at=N, early_wg=W
 //                     once a pass's chains fall below N (default 768 per CU), each path round runs
 //                     its K heaviest chains (1: what W cooperative workgroups per CU hold) in a
@@ -1191,7 +1191,7 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // above the hand-over
         if (ss->coop_max && !tune_has("sparse")) ss->path_sparse = std::min(ss->path_sparse, ss->coop_max);
         ss->round_batch = (uint32_t)std::max(1, tune_int("round_batch", (int)ss->round_batch));
-        ss->coop_order = tune_int("coop_order", 0) != 0;
+        ss->coop_order = tune_int("coop_order", 1) != 0;
         // Early cooperative launch (teams of 8, QC_WAVES waves per workgroup: 32 chains each):
         // the low-chain rounds leave each CU room for one more workgroup, which the heaviest
         // chains use from then on instead of waiting for the final hand-over
