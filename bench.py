@@ -13,11 +13,16 @@ the timed region.
 Multi-GPU: one process per GPU.  `python bench.py --gpus N` (no WORLD_SIZE in
 the environment) starts the N ranks itself under torch.distributed.run before
 anything touches a GPU; under torchrun it runs as the rank it is given and
-exits non-zero if WORLD_SIZE != --gpus.  The frame's 16x16 tiles are dealt
-round-robin to ranks (no data-path collective) and every rank advances its
-pixels by spp-per-step x N samples per step, so the per-GPU work is fixed as N
-grows ("weak" scaling); the timed region ends with the framebuffer resolve
-(tonemap on device) and an RCCL gather of the packed 8-bit tiles to rank 0.
+exits non-zero if WORLD_SIZE != --gpus.  The frame's 16x16 tiles are dealt to
+ranks in diagonal stripes (no data-path collective).  `--scaling strong` (the
+default, the metric's own job: "1080p/256spp, 1/2/4/8 GPU"): a step is
+spp-per-step samples of EVERY pixel of the frame at any N, each rank rendering
+its 1/N of the pixels, so the job is fixed and N GPUs should finish it N times
+faster (`--steps 16` = the whole 256-spp frame).  `--scaling weak`: every rank
+advances its pixels by spp-per-step x N samples per step (per-GPU work fixed as
+N grows; one long pass per rank, which hides the end-of-pass tail).  The timed
+region ends with the framebuffer resolve (tonemap on device) and an RCCL gather
+of the packed 8-bit tiles to rank 0.
 
 Also reported: the roofline of the dominant kernel (k_wpath, the persistent
 path engine: closest-hit queries + shading) from in-kernel counters and
@@ -95,6 +100,13 @@ def spawn_ranks(args, argv):
     return subprocess.call(cmd, env=env)
 
 
+def rank_spp(spp_per_step, world, scaling):
+    """samples per pixel a rank's pixels advance per step: strong scaling, the frame's
+    spp-per-step at any N (each rank owns 1/N of the pixels: the job is fixed); weak, N
+    times that (the rank's work per step is the one-GPU step's)"""
+    return spp_per_step * (world if scaling == "weak" else 1)
+
+
 def probe_ranks(args, rank, world):
     """CPU check of the launch path (tests/test_dist.py): every rank joins a gloo
     group and rank 0 prints the ranks it sees.  No GPU is touched."""
@@ -104,7 +116,9 @@ def probe_ranks(args, rank, world):
     got = [None] * world
     dist.all_gather_object(got, {"rank": rank, "pid": os.getpid(), "local_rank": int(os.environ.get("LOCAL_RANK", 0))})
     if rank == 0:
-        print(json.dumps({"probe": True, "n_gpus": world, "gpus_arg": args.gpus, "ranks": got}))
+        print(json.dumps({"probe": True, "n_gpus": world, "gpus_arg": args.gpus, "ranks": got,
+                          "scaling": args.scaling, "rank_spp_per_step": rank_spp(args.spp_per_step, world, args.scaling),
+                          "pass_spp": rank_spp(args.spp_per_step, world, args.scaling) * args.steps}))
     dist.destroy_process_group()
     del torch
 
@@ -270,20 +284,29 @@ def cpu_baseline(pt, args):
 def wall_to_ppm(config, ngpu):
     """The drop-in CLI (run.sh <scene.txt> <out.ppm>) on the whole config: process
     start -> PPM closed (parse, reference BVH, aux BVH, upload, full render,
-    tonemap, gather, P6 write), as the reference's `run.sh` is timed.  ngpu > 1:
-    one process drives ngpu GPUs (PT_NGPU) and gathers with RCCL."""
+    tonemap, gather, P6 write), as the reference's `run.sh` is timed (SURVEY §8d:
+    the metric stops at "PPM closed"; the process's exit after it -- the HIP
+    runtime's teardown -- is reported apart as `teardown_s`).  ngpu > 1: one
+    process drives ngpu GPUs (PT_NGPU) and gathers with RCCL."""
     src = scene_file(config)
     out = os.path.join("/tmp", "pt_bench_%s_%d.ppm" % (config, os.getpid()))
     env = dict(os.environ, PT_STATS="2", PT_QUIET="1", PT_NGPU=str(ngpu))
     if ngpu > 1:
         env["PT_GATHER"] = "rccl"
+    u0 = time.time()
     t0 = time.perf_counter()
     # bounded (120 s; c3 takes ~1 s): a hung CLI (e.g. RCCL initialisation) must not hold back the bench line
     r = subprocess.run([os.path.join(REPO, "run.sh"), src, out], env=env, capture_output=True, text=True,
                        timeout=120)
-    dt = time.perf_counter() - t0
+    dt_exit = time.perf_counter() - t0
+    u1 = time.time()
     if r.returncode != 0:
         raise RuntimeError(r.stderr.strip()[-300:])
+    # the CLI prints the wall-clock time at which the PPM was closed (PT_STATS=2)
+    um = re.search(r"unix_main=([\d.]+) unix_written=([\d.]+)", r.stderr)
+    written = float(um.group(2)) if um else None
+    dt = (written - u0) if written else dt_exit
+    teardown = (u1 - written) if written else None
     md5 = hashlib.md5(open(out, "rb").read()).hexdigest()
     os.unlink(out)
     stats = [ln for ln in r.stderr.splitlines() if ln.startswith("rays=")]
@@ -298,13 +321,20 @@ def wall_to_ppm(config, ngpu):
             phases.setdefault("ranks", []).append({k: float(v) for k, v in re.findall(r"(\w+)=([\d.]+)", ln)})
         elif ln.startswith("pt_render gather_ms"):
             phases["gather_ms"] = float(re.search(r"gather_ms=([\d.]+)", ln).group(1))
-    return {"config": config, "ngpu": ngpu, "seconds": dt, "rays": rays, "mray_s": rays / dt / 1e6,
-            "render_ms": float(m["wall_ms"]), "kernel_ms": float(m["kernel_ms"]),
-            "render_mray_s": rays / float(m["kernel_ms"]) / 1e3 if float(m["kernel_ms"]) > 0 else None,
+    render_ms = float(m["wall_ms"])
+    kernel_ms = float(m["kernel_ms"])
+    return {"config": config, "ngpu": ngpu, "seconds": dt, "seconds_to_exit": dt_exit, "teardown_s": teardown,
+            "rays": rays, "mray_s": rays / dt / 1e6,
+            "render_ms": render_ms, "kernel_ms": kernel_ms,
+            # the same pass over two clocks: the pass's kernels (HIP events) and pt_render's own wall
+            # (session set-up + the pass + tonemap + gather)
+            "render_mray_s": rays / kernel_ms / 1e3 if kernel_ms > 0 else None,
+            "render_wall_mray_s": rays / render_ms / 1e3 if render_ms > 0 else None,
             "gather_rccl": int(m.get("gather_rccl", 0)), "ppm_md5": md5, "phases": phases,
-            "what": "PT_NGPU=%d run.sh <scene> <out.ppm>: one process, process start to PPM closed "
-                    "(all spp of the config); render_ms = pt_render's wall (session set-up, the pass, "
-                    "tonemap, gather), kernel_ms = the pass's kernels (HIP events, slowest GPU)" % ngpu}
+            "what": "PT_NGPU=%d run.sh <scene> <out.ppm>: one process; seconds = process start to PPM closed "
+                    "(all spp of the config), teardown_s = the process exit after it; render_ms = pt_render's "
+                    "wall (session set-up, the pass, tonemap, gather), kernel_ms = the pass's kernels (HIP "
+                    "events, slowest GPU)" % ngpu}
 
 
 # -------------------------------------------------------------- roofline --
@@ -374,10 +404,16 @@ def roofline(st0, st1, traffic_json, key):
 
 
 def kernel_resources():
+    """the compiler's resource report of the path engine's two instantiations and the
+    cooperative engine's default one (teams of 8; tools/kernel_resources.py)"""
     try:
         import kernel_resources as KR
         ks = KR.kernel("k_wpath")
-        return {("end_of_pass" if "ILb1" in k else "main"): v for k, v in ks.items()}
+        out = {("end_of_pass" if "ILb1" in k else "main"): v for k, v in ks.items()}
+        for k, v in KR.kernel("k_wcoop").items():
+            if "ILj8ELb0" in k:
+                out["coop_team8"] = v
+        return out
     except Exception:
         return None
 
@@ -389,7 +425,10 @@ def main():
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3")
-    ap.add_argument("--spp-per-step", type=int, default=16, help="samples per pixel per step, per GPU")
+    ap.add_argument("--spp-per-step", type=int, default=16,
+                    help="samples per pixel per step (strong: of every pixel of the frame; weak: x N per rank)")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong (default): the frame's job split over N GPUs; weak: per-GPU work fixed")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-wallclock", action="store_true", help="skip the full-config CLI run (wall_to_ppm)")
     ap.add_argument("--cpu-configs", nargs="+", default=list(CPU_SAMPLES), choices=list(CPU_SAMPLES))
@@ -452,7 +491,9 @@ def main():
     ss = pt.Session(scene, device=local, rank=rank, world=world, traversal=trav)
     ss.sync()
     t_ready = time.perf_counter()
-    spp = args.spp_per_step * world   # weak scaling: a rank owns 1/world of the pixels
+    # strong: every pixel of the frame advances spp-per-step per step at any N (a rank owns 1/N of
+    # them); weak: a rank's pixels advance N times as far, so its work per step is the one-GPU work
+    spp = rank_spp(args.spp_per_step, world, args.scaling)
     packed = torch.empty(max(ss.packed_bytes, 1), dtype=torch.uint8, device=device)
     for _ in range(args.warmup):
         ss.trace(spp)
@@ -511,20 +552,23 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": T * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: md5-pinned 89,928-triangle dragon stand-in (SURVEY §8d), per-pixel reference seeds",
-            "config": {"workload": "config 3: %s %dx%d, %d spp per step per rank (of 256), RAY_DEPTH %d; %s "
-                                   "traversal of the reference tree (bit-exact)" % (args.config, W, H, spp,
-                                                                                     info["ray_depth"], args.traversal),
+            "config": {"workload": "config 3: %s %dx%d, %d spp of every pixel per step (%s scaling; the metric's "
+                                   "job is 256 spp = 16 steps of 16), RAY_DEPTH %d; %s traversal of the reference "
+                                   "tree (bit-exact)" % (args.config, W, H, spp, args.scaling, info["ray_depth"],
+                                                         args.traversal),
                        "pixels": W * H, "samples_per_step": W * H * spp,
+                       "spp_per_step_per_pixel": spp, "scaling": args.scaling,
                        "parallelism": "pixel tiles x%d" % world},
             "roofline": roof,
             "wavefront_rounds": int(st1["rounds"] - st0["rounds"]),
             "kernel_ms_per_step": kms / args.steps,
             "rays": total_rays,
             "msamples_per_s": W * H * spp * args.steps / T / 1e6,
+            "pass_spp": spp * args.steps,
             "node_visits_per_ray": float(tsum[2]) / max(total_rays, 1),
             "aux_visits_per_ray": float(tsum[6]) / max(total_rays, 1),
             "fallback_rate": float(tsum[7]) / max(total_rays, 1),
@@ -560,8 +604,13 @@ def main():
             try:
                 res["wall_to_ppm"] = wall_to_ppm(args.config, ngpu)
                 # the metric's own pass: the whole config (256 spp for c3) as ONE pass, rays over its
-                # kernel time -- beside `value`, whose 16-spp steps coalesce into a pass of steps x 16
+                # kernel time (HIP events) and over pt_render's wall -- beside `value`, whose 16-spp
+                # steps coalesce into a pass of steps x 16
                 res["render_256spp_mray_s"] = res["wall_to_ppm"]["render_mray_s"]
+                res["render_256spp_wall_mray_s"] = res["wall_to_ppm"]["render_wall_mray_s"]
+                res["render_256spp_clocks"] = ("render_256spp_mray_s: rays / the pass's kernel time (HIP "
+                                               "events); render_256spp_wall_mray_s: rays / pt_render's wall "
+                                               "(session set-up + pass + tonemap + gather)")
             except Exception as e:
                 log("wall-clock run failed:", e)
                 res["wall_to_ppm"] = None

@@ -25,12 +25,14 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 4   /* 2: pt_render_opts.gather; 3: pt_stats per-engine (coop_*) fields;
+#define PT_ABI_VERSION 5   /* 2: pt_render_opts.gather; 3: pt_stats per-engine (coop_*) fields;
                               4: pt_gather_init, and the session tile deal changed from tile
                               t -> rank t % world to tile (tx, ty) -> rank (tx + ty) % world
                               (local tiles still in ascending tile order): a driver that
                               un-interleaves packed tiles itself must use pt_unpack_tiles
-                              (or ptrace.rank_tiles), not its own formula */
+                              (or ptrace.rank_tiles), not its own formula;
+                              5: pt_stats.short_pixels / handed_on, and pt_session_resolve fails
+                              when an owned pixel's sample count differs from the samples traced */
 
 enum {
     PT_OK = 0,
@@ -146,6 +148,11 @@ typedef struct pt_stats {
     uint64_t coop_rays, coop_node_visits, coop_prim_tests, coop_aux_visits;
     double coop_ms;
     uint64_t coop_launches;
+    /* ABI 5: pixels found at a resolve with a sample count other than the samples traced
+       (a lost chain: pt_session_resolve then fails; must be 0), and work items an early
+       cooperative launch's late workgroups handed on to the next round untaken */
+    uint64_t short_pixels;
+    uint64_t handed_on;
 } pt_stats;
 
 /* Scene::Render minus the stream write: renders W*H*3 u8 (row-major, top row

@@ -150,7 +150,13 @@ struct WaveParams {
     uint32_t side_stop_n;
     uint32_t* yield_cq;
     uint32_t* yield_ctr;
+    uint32_t side_flags;          // PT_SIDE_* test hooks of that launch (0 in every render)
 };
+// k_wcoop beside a path round, test hooks (PT_TUNE side_late / handon): every workgroup
+// behaves as one that started after the round's end (takes nothing, hands every item on);
+// the untaken items are dropped instead of handed on (a lost chain: the resolve's check)
+#define PT_SIDE_LATE 1u
+#define PT_SIDE_NO_HANDON 2u
 #define PT_ORDER_BUCKETS 256u
 
 // path engine geometry: PT_NQ query waves + 1 shade wave per workgroup; at most
@@ -208,11 +214,17 @@ struct WaveParams {
 
 struct ResolveParams {
     PixelState st;
+    TileMap tm;                   // which slots are pixels (the rest of a partial edge tile are not)
     const float* thr;             // 256 gamma thresholds
     uint8_t* out;                 // 3 * n_slots
     float* rad;                   // optional 3 * n_slots
     uint32_t samples;             // samples accumulated so far
+    unsigned long long* counters; // statistics counters: C_SHORT counts the owned pixels whose
+                                  // samples done differ from `samples` (a lost chain; must be 0)
 };
+// statistics counter slots (per copy, PT_CTR_STRIDE u64) besides rays .. fallbacks_ray (0-7)
+// and the cooperative engine's share (8-10, 13)
+enum : uint32_t { CTR_SHORT = 11u, CTR_HANDON = 12u };
 
 }  // namespace pt
 

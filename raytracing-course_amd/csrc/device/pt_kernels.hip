@@ -95,6 +95,12 @@ __global__ void __launch_bounds__(256) k_resolve(ResolveParams P) {
     thr[threadIdx.x] = P.thr[threadIdx.x];
     __syncthreads();
     const uint32_t slot = blockIdx.x * 256u + threadIdx.x;
+    // every owned pixel must have taken exactly `samples` samples (src/scene.cpp:192-199,
+    // the reference's loop): a chain lost by the engines would leave its pixel short, and
+    // an image wrong without any other error -- counted here, an error of the resolve
+    uint32_t px, py;
+    const bool pix = slot_pixel(P.tm, blockIdx.x, threadIdx.x, px, py);
+    wave_add_u64(ctr_copy(P.counters) + CTR_SHORT, pix && load_hot(P.st, slot).done != P.samples ? 1ull : 0ull);
     const float inv = 1.f / (float)P.samples;    // src/scene.cpp:201: (1.f / SAMPLES) * sum
     const f3 s = load_sum(P.st, slot);
     const float m[3] = {inv * s.x, inv * s.y, inv * s.z};

@@ -1335,33 +1335,13 @@ k_wcoop(WaveParams P) {
     for (;;) {
         if (P.side_stop) {
             // beside a path round: once its workgroups have all finished, the chains leave at
-            // this chain cycle's end -- each team's next query, as a suspended query at its
-            // start, to the round's next carry queue (a resumed query is not counted again: its
-            // ray was counted when first taken), its pixel state and the current path's fold
-            // records to HBM (the path engine continues the path from there)
+            // this chain cycle's end (after the loop: the yield's registers stay out of it)
             uint32_t fin = 0u;
             if (lane == 0u) fin = __hip_atomic_load(P.side_stop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
             fin = __builtin_amdgcn_readfirstlane(fin);
-            if (fin >= P.side_stop_n) {
-                const uint32_t k = wave_append(P.yield_ctr, have && tl == 0u);
-                if (have && tl == 0u) {
-                    Query q;
-                    q_init_pre(ray, Pt, pid, pre, q);
-                    uint32_t* w = P.yield_cq + (size_t)k * P.carry_words;
-                    *reinterpret_cast<Query*>(w) = q;
-                    w[sizeof(Query) / 4u] = slot;
-                    PixelHot hot;
-                    hot.R = px.R;
-                    hot.nv = px.nv;
-                    hot.done = px.done;
-                    store_hot(P.st, slot, hot);
-                    P.st.rec[2u * slot + 1u] = L.sum;
-                }
-                const uint32_t nv = __shfl(px.nv, (int)tbase, 64);
-                if (have && tl < nv && (!BIG || tl < QC_FOLD)) P.st.fold[(size_t)slot * P.st.depth + tl] = L.fold[tl];
-                have = false;
-                exhausted = true;
+            if (fin >= P.side_stop_n || (P.side_flags & PT_SIDE_LATE)) {
                 stopped = true;
+                break;
             }
         }
         // teams without a chain take the next one (queue order: carry, then fresh)
@@ -1476,8 +1456,32 @@ k_wcoop(WaveParams P) {
             prog = 0u;
         }
     }
+    uint32_t handed = 0u;
     if (stopped) {
-        // A launch beside a path round that stopped: the work items no team took (a
+        // A launch beside a path round that stopped: each team's next query, as a
+        // suspended query at its start, to the round's next carry queue (a resumed query is
+        // not counted again: its ray was counted when first taken), its pixel state and the
+        // current path's fold records to HBM (the path engine continues the path from there)
+        const uint32_t k = wave_append(P.yield_ctr, have && tl == 0u);
+        if (have && tl == 0u) {
+            Query q;
+            q_init_pre(ray, Pt, pid, pre, q);
+            uint32_t* w = P.yield_cq + (size_t)k * P.carry_words;
+            *reinterpret_cast<Query*>(w) = q;
+            w[sizeof(Query) / 4u] = slot;
+            PixelHot hot;
+            hot.R = px.R;
+            hot.nv = px.nv;
+            hot.done = px.done;
+            store_hot(P.st, slot, hot);
+            P.st.rec[2u * slot + 1u] = L.sum;
+        }
+        const uint32_t nv = __shfl(px.nv, (int)tbase, 64);
+        if (have && tl < nv && (!BIG || tl < QC_FOLD)) P.st.fold[(size_t)slot * P.st.depth + tl] = L.fold[tl];
+        have = false;
+    }
+    if (stopped && !(P.side_flags & PT_SIDE_NO_HANDON)) {
+        // ... then the work items no team took (a
         // workgroup that started only after the round's end -- the launch shares the
         // device with the path round and anything else on it) go to the next round as
         // they are, their pixels' records untouched in HBM (a fresh ray is counted
@@ -1510,6 +1514,7 @@ k_wcoop(WaveParams P) {
                 C.planes += P.S.n_planes;
             }
             const uint32_t k2 = wave_append(P.yield_ctr, on);
+            handed += on ? 1u : 0u;
             if (on) {
                 Query q;
                 q_init_pre(r, rp, rid, rpre, q);
@@ -1533,6 +1538,7 @@ k_wcoop(WaveParams P) {
     wave_add_u64(ctr + 9, C.nodes);
     wave_add_u64(ctr + 10, C.ptests);
     wave_add_u64(ctr + 13, C.aux);
+    wave_add_u64(ctr + CTR_HANDON, handed);
 #ifdef PT_CPROF
     // (per team first lanes: chain counts; cycle sums are per wave, counted by lane 0)
     cp[7] = __builtin_amdgcn_s_memtime() - cp_start;

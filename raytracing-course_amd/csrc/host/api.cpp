@@ -100,7 +100,14 @@ const Rccl& rccl() {
 //                     its K heaviest chains (1: what W cooperative workgroups per CU hold) in a
 //                     cooperative launch on a second stream beside it; the launch hands its chains
 //                     back when the round's path workgroups finish (default: 1; 0 = off)
-//   cap=N             chains a workgroup may hold
+//   side_prio=0|1|2   that launch's stream: 0 normal priority (may share a main stream's
+//                     hardware queue), 1 the greatest priority (a queue pool of its own; default),
+//                     2 a CU-masked stream over every CU (always a queue of its own); take_stream
+//   inject_fail=G     pt_render: rank G fails after its set-up (tests of the error paths)
+//   side_late=1       test hook: the early launch's workgroups all act as late ones (take no
+//                     chain, hand every work item on to the next round)
+//   handon=0          test hook: ... and drop those items instead (lost chains: the resolve fails)
+//   cap=N            chains a workgroup may hold
 //   batch=N           round-queue entries a query wave takes per pull (1..64, default 32)
 //   lstack=N          aux stack words a path-engine query may use (default and maximum PT_LSTACK;
 //                     a query needing more takes the exact DFS)
@@ -150,18 +157,36 @@ int tune_int(const char* key, int def) {
 // streams made ahead of time by pt_device_init (stream creation costs ~8 ms of
 // the runtime's first use), adopted by the next session on that device
 std::mutex g_spare_mu;
-std::map<int, std::vector<hipStream_t>> g_spare_streams;
-hipError_t take_stream(int dev, hipStream_t* s) {
+std::map<int, std::vector<hipStream_t>> g_spare_streams, g_spare_side;
+// side: the early cooperative launch's stream.  It must run BESIDE the session's path
+// round, so it must never share a hardware queue with a main stream: the runtime maps
+// streams onto at most GPU_MAX_HW_QUEUES (4) queues per priority level and, past that,
+// hands a new stream an existing queue of the same priority, where its kernels run in
+// submission order after the other stream's.  A side launch queued behind (or ahead of)
+// its own path round then runs alone: it holds the pass's heaviest chains to the end of
+// the pass at the cooperative engine's rate (round 4: with 4 and 8 sessions on one
+// device, the ranks past the third rendered 1.3-1.7x slower).  Side streams are made at
+// the greatest priority, a queue pool of their own.
+hipError_t take_stream(int dev, hipStream_t* s, bool side = false) {
     {
         std::lock_guard<std::mutex> lk(g_spare_mu);
-        auto& v = g_spare_streams[dev];
+        auto& v = side ? g_spare_side[dev] : g_spare_streams[dev];
         if (!v.empty()) {
             *s = v.back();
             v.pop_back();
             return hipSuccess;
         }
     }
-    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    const int mode = side ? tune_int("side_prio", 1) : 0;
+    if (mode == 2) {
+        // a CU-masked stream (every CU) always gets a hardware queue of its own
+        std::vector<uint32_t> m(64, 0xffffffffu);
+        return hipExtStreamCreateWithCUMask(s, (uint32_t)m.size(), m.data());
+    }
+    if (mode == 0) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    int least = 0, greatest = 0;
+    if (const hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest)) return e;
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
 }
 
 #define HIP_TRY(expr)                                                                                 \
@@ -269,11 +294,12 @@ struct pt_session {
     unsigned char* arena = nullptr;
     size_t arena_bytes = 0;
     pt::RayQ fq[2] = {};          // fresh rays (n_slots each)
-    pt::DoneQ done = {};          // exact-DFS results (lane_cap)
-    pt::RayQ ex = {};             // rays handed to the exact DFS (lane_cap)
+    pt::DoneQ done = {};          // exact-DFS results (n_slots)
+    pt::RayQ ex = {};             // rays handed to the exact DFS (n_slots)
     uint32_t* carry = nullptr;    // 2 * carry_cap * carry_words
     uint2* endq = nullptr;        // path_grid * PT_CMAX: the shade waves' ended paths
-    uint32_t lane_cap = 0;        // min(pixels, query lanes): what one round can suspend or hand over
+    unsigned long long short_seen = 0;   // CTR_SHORT at the last resolve
+    uint32_t lane_cap = 0;        // min(pixels, query lanes): what one round can suspend
     uint32_t carry_cap = 0, carry_words = 0;
     uint32_t* ctl = nullptr;      // 2 x PT_CTL_SET round counters
     uint32_t* ctl_host = nullptr; // pinned copy of one counter set
@@ -1150,8 +1176,11 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // suspended-query records: Query | slot | aux stack, rounded to 16 B.  Only a
         // query lane suspends (one query at round end), and a pixel has at most one ray
         // in flight, so a round appends at most min(pixels, query lanes) of them: the
-        // carry queue can never overflow.  The exact-DFS hand-over queues (ex, done)
-        // have the same bound.
+        // carry queue can never overflow.  The exact-DFS hand-over queues (ex, done, hid)
+        // do NOT have that bound: a lane that hands its ray over goes on with another
+        // chain of the round's supply, so a round can hand over a ray of every chain --
+        // at most one per pixel (a chain that leaves for k_wexact leaves the round).
+        // They hold n entries.
         ss->carry_words = ((uint32_t)(sizeof(pt::Query) / 4) + 1u + std::max<uint32_t>(s->auxw_stack, 1u) + 3u) & ~3u;
         ss->lane_cap = (uint32_t)std::min<uint64_t>(n, (uint64_t)ss->path_grid * PT_NQ * 64u);
         ss->carry_cap = ss->lane_cap;
@@ -1251,13 +1280,12 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         const size_t a_ctr = sec(8 * PT_CTR_COPIES * PT_CTR_STRIDE), a_out = sec(3 * n);
         size_t a_fq[2][3] = {{0, 0, 0}, {0, 0, 0}}, a_pid = 0, a_dq[2] = {0, 0}, a_ex[2] = {0, 0}, a_hid = 0;
         size_t a_carry = 0, a_ctl = 0, a_endq = 0, a_order = 0, a_side[6] = {0, 0, 0, 0, 0, 0};
-        const size_t lanes = ss->lane_cap;
         if (ss->wave) {
             for (int q = 0; q < 2; ++q)
                 for (int k = 0; k < 3; ++k) a_fq[q][k] = sec(n * 16);
             a_pid = sec(2 * n * 4);
-            for (int k = 0; k < 2; ++k) { a_dq[k] = sec(lanes * 16); a_ex[k] = sec(lanes * 16); }
-            a_hid = sec(lanes * 4);
+            for (int k = 0; k < 2; ++k) { a_dq[k] = sec(n * 16); a_ex[k] = sec(n * 16); }
+            a_hid = sec(n * 4);
             a_carry = sec(2ull * ss->carry_cap * ss->carry_words * 4);
             a_ctl = sec(8 * PT_CTL_SET);
             a_endq = sec((size_t)ss->path_grid * PT_CMAX * sizeof(uint2));
@@ -1509,12 +1537,17 @@ int trace_wave(pt_session* ss, uint32_t spp) {
         // (only after a count: before the first one `chains` is the slot count, not the
         // queue's, and every pixel has the same samples left)
         bool side = false;
+        // (test hook side_late: the side launch runs after the path round, on its stream --
+        // every workgroup one that started after the round's end)
+        pt::WaveParams late_sp;
+        bool late = false;
+        uint32_t late_grid = 0;
         if (ss->early_k && counted && chains < ss->early_at && chains > ss->coop_max) {
             const uint32_t k = std::min(ss->early_k, chains / 4u);
             const uint32_t grid = chains < ss->lowq && ss->low_grid ? ss->low_grid : ss->path_grid;
             if (k) {
                 side = true;
-                if (!ss->side_stream && take_stream(ss->dev, &ss->side_stream) != hipSuccess)
+                if (!ss->side_stream && take_stream(ss->dev, &ss->side_stream, true) != hipSuccess)
                     return fail(PT_E_HIP, "stream creation failed");
                 wp.parity = p;
                 wp.order_cur = ss->order;
@@ -1541,6 +1574,8 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 sp.side_stop_n = grid;
                 sp.yield_cq = wp.cq[1u - p];
                 sp.yield_ctr = out + pt::C_CARRY;
+                sp.side_flags = (tune_int("side_late", 0) ? PT_SIDE_LATE : 0u) |
+                                (tune_int("handon", 1) ? 0u : PT_SIDE_NO_HANDON);
                 hipEvent_t i0, i1;
                 HIP_TRY(hipEventCreate(&i0));
                 HIP_TRY(hipEventCreate(&i1));
@@ -1550,8 +1585,16 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 ss->isect_launches++;
                 ss->coop_launches++;
                 const bool big = ss->depth > QC_FOLD || s->planes.size() > QC_NPL || s->emitters.size() > QC_NEM;
-                HIP_TRY(pt_launch_coop(sp, ss->early_wg * (ss->coop_grid / 8u), 8u, big, ss->side_stream, i0, i1));
-                HIP_TRY(hipEventRecord(ss->side_end, ss->side_stream));
+                if (sp.side_flags & PT_SIDE_LATE) {
+                    late = true;
+                    late_sp = sp;
+                    late_grid = ss->early_wg * (ss->coop_grid / 8u);
+                    HIP_TRY(hipEventRecord(i0, ss->stream));   // (timed with the round)
+                    HIP_TRY(hipEventRecord(i1, ss->stream));
+                } else {
+                    HIP_TRY(pt_launch_coop(sp, ss->early_wg * (ss->coop_grid / 8u), 8u, big, ss->side_stream, i0, i1));
+                    HIP_TRY(hipEventRecord(ss->side_end, ss->side_stream));
+                }
                 // the path round takes the other chains: items k .. chains of the order
                 wp.pin = wp.order + k;
                 wp.pin_n = chains - k;
@@ -1589,6 +1632,14 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             }
             HIP_TRY(pt_launch_path_round(wp, grid, 64u, ss->stream, sparse, i0, i1));
             wp.pin = nullptr;   // (only the round beside the early launch skips its chains)
+            if (late) {
+                // (it yields into the round's output counters, which the round's own launch
+                // zeroed: a side launch that could yield before that zeroing would lose items)
+                const bool big = ss->depth > QC_FOLD || s->planes.size() > QC_NPL || s->emitters.size() > QC_NEM;
+                HIP_TRY(pt_launch_coop(late_sp, late_grid, 8u, big, ss->stream));
+                HIP_TRY(hipEventRecord(ss->side_end, ss->stream));
+                late = false;
+            }
             if (wp.wg_prof) {
                 uint32_t cnt[2][8];
                 HIP_TRY(hipMemcpyAsync(cnt[0], ss->ctl + PT_CTL_SET * p, 32, hipMemcpyDeviceToHost, ss->stream));
@@ -1661,6 +1712,19 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     return PT_OK;
 }
 }  // namespace
+
+// the statistics counters, summed over their per-XCD copies (after the stream's work)
+static hipError_t read_counters(pt_session* ss, unsigned long long c[PT_CTR_STRIDE]) {
+    unsigned long long cc[PT_CTR_COPIES * PT_CTR_STRIDE];
+    // (on the session's stream: the null stream would also wait for other sessions' work)
+    hipError_t e = hipMemcpyAsync(cc, ss->counters, sizeof(cc), hipMemcpyDeviceToHost, ss->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ss->stream);
+    for (uint32_t k = 0; k < PT_CTR_STRIDE; ++k) c[k] = 0ull;
+    if (e != hipSuccess) return e;
+    for (uint32_t x = 0; x < PT_CTR_COPIES; ++x)
+        for (uint32_t k = 0; k < PT_CTR_STRIDE; ++k) c[k] += cc[PT_CTR_STRIDE * x + k];
+    return hipSuccess;
+}
 
 // run the coalesced trace() calls of the wavefront engine as one pass
 static int flush_trace(pt_session* ss) {
@@ -1749,6 +1813,8 @@ int pt_session_resolve(pt_session* ss, uint8_t* dev_out, float* dev_radiance) {
     HIP_TRY(hipSetDevice(ss->dev));
     pt::ResolveParams rp;
     rp.st = ss->st;
+    rp.tm = ss->tm;
+    rp.counters = ss->counters;
     rp.thr = ss->ds->thr;
     rp.out = dev_out ? dev_out : ss->out;
     rp.rad = dev_radiance;
@@ -1764,6 +1830,15 @@ int pt_session_resolve(pt_session* ss, uint8_t* dev_out, float* dev_radiance) {
     if (hipEventElapsedTime(&ms, e0, e1) == hipSuccess) ss->resolve_ms += ms;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+    // pixels short of (or past) the samples so far: a chain was lost -- an error, not an image
+    unsigned long long c[PT_CTR_STRIDE];
+    HIP_TRY(read_counters(ss, c));
+    if (c[pt::CTR_SHORT] != ss->short_seen) {
+        const unsigned long long k = c[pt::CTR_SHORT] - ss->short_seen;
+        ss->short_seen = c[pt::CTR_SHORT];
+        return fail(PT_E_HIP, std::to_string(k) + " pixel(s) did not take exactly " + std::to_string(rp.samples) +
+                                  " samples (a chain was lost)");
+    }
     return PT_OK;
 }
 
@@ -1789,10 +1864,8 @@ int pt_session_stats(pt_session* ss, pt_stats* st) {
     if (!ss || !st) return fail(PT_E_INVALID, "null argument");
     int rc = pt_session_sync(ss);
     if (rc) return rc;
-    unsigned long long cc[PT_CTR_COPIES * PT_CTR_STRIDE], c[PT_CTR_STRIDE] = {0};
-    HIP_TRY(hipMemcpy(cc, ss->counters, sizeof(cc), hipMemcpyDeviceToHost));
-    for (uint32_t x = 0; x < PT_CTR_COPIES; ++x)
-        for (uint32_t k = 0; k < PT_CTR_STRIDE; ++k) c[k] += cc[PT_CTR_STRIDE * x + k];
+    unsigned long long c[PT_CTR_STRIDE];
+    HIP_TRY(read_counters(ss, c));
     memset(st, 0, sizeof(*st));
     st->rays = c[0];
     st->node_visits = c[1];
@@ -1821,6 +1894,8 @@ int pt_session_stats(pt_session* ss, pt_stats* st) {
     st->coop_aux_visits = c[13];
     st->coop_ms = ss->coop_ms;
     st->coop_launches = ss->coop_launches;
+    st->short_pixels = c[pt::CTR_SHORT];
+    st->handed_on = c[pt::CTR_HANDON];
     return PT_OK;
 }
 
@@ -1833,20 +1908,22 @@ void* pt_session_stream(pt_session* ss) {
 void pt_session_free(pt_session* ss) {
     if (!ss) return;
     (void)hipSetDevice(ss->dev);
+    // both streams drained before any buffer goes (a side launch may still run after a
+    // failed pass)
     if (ss->stream) (void)hipStreamSynchronize(ss->stream);
+    if (ss->side_stream) (void)hipStreamSynchronize(ss->side_stream);
     finish_pending(ss);
     (void)hipFree(ss->arena);
     (void)hipFree(ss->rad); (void)hipFree(ss->wg_prof);
     if (ss->ctl_host) (void)hipHostFree(ss->ctl_host);
     if (ss->prog_host) (void)hipHostFree(ss->prog_host);
-    if (ss->side_stream) (void)hipStreamSynchronize(ss->side_stream);
     if (ss->side_taken) (void)hipEventDestroy(ss->side_taken);
     if (ss->side_end) (void)hipEventDestroy(ss->side_end);
     if (ss->stream || ss->side_stream) {
-        // back to the device's pool for the next session (no destroy/create per render)
+        // back to the device's pools for the next session (no destroy/create per render)
         std::lock_guard<std::mutex> lk(g_spare_mu);
         if (ss->stream) g_spare_streams[ss->dev].push_back(ss->stream);
-        if (ss->side_stream) g_spare_streams[ss->dev].push_back(ss->side_stream);
+        if (ss->side_stream) g_spare_side[ss->dev].push_back(ss->side_stream);
     }
     delete ss;
 }
@@ -2039,6 +2116,7 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
         int r = pt_session_create(s, &so, &sess[(size_t)g]);
         pt_session* x = sess[(size_t)g];
         if (!r) r = pt_session_sync(x);   // (the session's init kernel)
+        if (!r && tune_int("inject_fail", -1) == g) r = fail(PT_E_INVALID, "injected failure (PT_TUNE inject_fail)");
         f.setup = ms_since(t_g);
         if (x) f.upload = x->upload_ms;
         if (same == 2) {
@@ -2047,7 +2125,8 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
             ++created;
             turn_cv.notify_all();
             const auto tw = std::chrono::steady_clock::now();
-            turn_cv.wait(lk, [&] { return created == ngpu && turn == g; });
+            // (>=: every rank advances `turn` once, failed or not, so no rank can be skipped)
+            turn_cv.wait(lk, [&] { return created == ngpu && turn >= g; });
             f.wait = ms_since(tw);
         }
         const auto t_r = std::chrono::steady_clock::now();
@@ -2080,13 +2159,6 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
         if (r) {
             trc[(size_t)g] = r;
             terr[(size_t)g] = pt_last_error();
-            if (same == 2) {
-                // (a failed rank must not leave the others waiting for their turn)
-                std::lock_guard<std::mutex> lk(turn_mu);
-                created = ngpu;
-                turn = ngpu;
-                turn_cv.notify_all();
-            }
         }
     };
     if (ngpu == 1) {
@@ -2125,10 +2197,16 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
     if (const char* e = getenv("PT_STATS"); e && atoi(e) >= 2) {
         // per-rank phase times (the CLI's PT_STATS=2): set-up = the device's scene upload (if
         // this session did it) + the session's buffers and init kernel
-        for (int g = 0; g < ngpu; ++g)
+        for (int g = 0; g < ngpu; ++g) {
+            pt_stats rs;
+            if ((rc = pt_session_stats(sess[(size_t)g], &rs))) return cleanup(rc);
             fprintf(stderr, "pt_render rank %d/%d: setup_ms=%.1f scene_upload_ms=%.3f wait_ms=%.1f render_ms=%.1f "
-                    "resolve_ms=%.1f\n", g, ngpu, ph[(size_t)g].setup, ph[(size_t)g].upload, ph[(size_t)g].wait,
-                    ph[(size_t)g].render, ph[(size_t)g].resolve);
+                    "resolve_ms=%.1f isect_ms=%.1f coop_ms=%.1f coop_launches=%llu rounds=%llu rays=%llu "
+                    "handed_on=%llu\n", g, ngpu, ph[(size_t)g].setup, ph[(size_t)g].upload, ph[(size_t)g].wait,
+                    ph[(size_t)g].render, ph[(size_t)g].resolve, rs.isect_ms, rs.coop_ms,
+                    (unsigned long long)rs.coop_launches, (unsigned long long)rs.rounds,
+                    (unsigned long long)rs.rays, (unsigned long long)rs.handed_on);
+        }
         fprintf(stderr, "pt_render gather_ms=%.1f path=%s\n", gather_ms, agg.gather_rccl ? "rccl" : "host");
     }
     for (int g = 0; g < ngpu; ++g) {
@@ -2146,6 +2224,7 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
         agg.plane_tests += st.plane_tests; agg.samples += st.samples; agg.errors += st.errors;
         agg.aux_visits += st.aux_visits; agg.fallbacks += st.fallbacks;
         agg.fallbacks_ray += st.fallbacks_ray;
+        agg.short_pixels += st.short_pixels; agg.handed_on += st.handed_on;
         agg.isect_ms = std::max(agg.isect_ms, st.isect_ms);
         agg.isect_launches += st.isect_launches;
         agg.coop_rays += st.coop_rays; agg.coop_node_visits += st.coop_node_visits;

@@ -26,7 +26,7 @@ TRAVERSAL_REPLAY = 0
 TRAVERSAL_EXACT = 1
 TRAVERSAL_REPLAY_DIV = 2
 GATHER_AUTO, GATHER_RCCL, GATHER_HOST = 0, 1, 2
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # One HIP runtime per process: PyTorch bundles its own libamdhip64 (soname
 # libamdhip64.so.7, but its users link the unversioned name), so loading
@@ -66,7 +66,8 @@ class Stats(C.Structure):
                 ("fallbacks_ray", C.c_uint64), ("isect_ms", C.c_double), ("isect_launches", C.c_uint64),
                 ("rounds", C.c_uint64), ("gather_rccl", C.c_uint64),
                 ("coop_rays", C.c_uint64), ("coop_node_visits", C.c_uint64), ("coop_prim_tests", C.c_uint64),
-                ("coop_aux_visits", C.c_uint64), ("coop_ms", C.c_double), ("coop_launches", C.c_uint64)]
+                ("coop_aux_visits", C.c_uint64), ("coop_ms", C.c_double), ("coop_launches", C.c_uint64),
+                ("short_pixels", C.c_uint64), ("handed_on", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

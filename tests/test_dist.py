@@ -122,6 +122,19 @@ def test_bench_gpus_n_starts_n_ranks(n):
     assert sorted(r["local_rank"] for r in out["ranks"]) == list(range(n))
 
 
+@pytest.mark.parametrize("scaling,spp", [("strong", 16), ("weak", 32), (None, 16)])
+def test_bench_scaling_modes(scaling, spp):
+    """`--scaling strong` (default): a step advances every pixel of the frame by
+    spp-per-step at any N -- the metric's fixed job, 16 steps = 256 spp; `--scaling
+    weak`: a rank's pixels advance N x spp-per-step per step (per-GPU work fixed)."""
+    args = ["--gpus", "2", "--probe-ranks", "--steps", "16"] + (["--scaling", scaling] if scaling else [])
+    rc, out, err = _bench(args)
+    assert rc == 0, err[-2000:]
+    assert out["scaling"] == (scaling or "strong")
+    assert out["rank_spp_per_step"] == spp and out["pass_spp"] == 16 * spp
+    assert sorted(r["rank"] for r in out["ranks"]) == [0, 1]
+
+
 def test_bench_refuses_mismatched_world():
     """under torchrun, a WORLD_SIZE that differs from --gpus is an error, not a
     silently relabelled run"""

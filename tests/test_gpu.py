@@ -371,6 +371,9 @@ TUNE_KEYS = ["wg_per_cu=2", "wg_per_cu=1", "runend=1000000", "sparse_steps=2", "
              # more early workgroups than fit beside the round (the late ones find it over and
              # hand their untaken items on)
              "coop=300,early=1,early_at=100000000,early_wg=8",
+             # every early workgroup a late one (side_late), the side stream at each priority
+             "coop=300,early=1,early_at=100000000,side_late=1",
+             "coop=300,early=1,early_at=100000000,side_prio=0", "coop=300,early=1,early_at=100000000,side_prio=2",
              # diagnostics hooks (their counters are compiled in only with -DPT_CPROF / -DPT_WPROF;
              # the host side runs in every build)
              "coop=300,cprof=1", "wgprof=/tmp/pt_wgprof_test.bin"]
@@ -388,6 +391,49 @@ def test_tuning_keys_bit_exact(pt, name, tune, monkeypatch):
     assert st["errors"] == 0
     assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
     assert np.array_equal(rgb, img)
+
+
+SIDE = "coop=300,budget=2,early=1,early_at=100000000,early_wg=8,side_late=1"
+
+
+@pytest.mark.parametrize("name", ["dragon_64x64x16", "c2_win_240_200_24x24"])
+def test_side_launch_hand_on_runs_and_is_counted(pt, name, monkeypatch):
+    """The early cooperative launch's workgroups that find their round over take nothing
+    and hand the round's untaken work items on (k_wcoop, after its main loop).  PT_TUNE
+    side_late=1 makes every workgroup such a late one, so the hand-on path certainly runs:
+    pt_stats.handed_on counts its items, and the bytes stay the reference's."""
+    monkeypatch.setenv("PT_TUNE", SIDE)
+    m, img, rad = U.golden_image(name)
+    with pt.Scene.load(U.golden_scene_path(name)) as s:
+        win = tuple(m["window"]) if m["window"] else None
+        rgb, r, st = s.render(radiance=True, window=win)
+    assert st["handed_on"] > 0 and st["short_pixels"] == 0 and st["errors"] == 0
+    assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
+    assert np.array_equal(rgb, img)
+
+
+def test_lost_chains_fail_the_resolve(pt, monkeypatch):
+    """A chain the engines lose leaves its pixel short of the pass target.  The resolve
+    counts the owned pixels whose sample count differs from the samples traced and fails
+    (src/scene.cpp:192-199: every pixel takes exactly SAMPLES samples): with the hand-on
+    loop disabled (PT_TUNE handon=0) the untaken items are dropped, and pt_render must
+    return that error, not an image."""
+    monkeypatch.setenv("PT_TUNE", SIDE + ",handon=0")
+    with pt.Scene.load(U.golden_scene_path("dragon_64x64x16")) as s:
+        with pytest.raises(pt.PTError, match="did not take exactly"):
+            s.render()
+
+
+@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("bad", [0, 1, 2])
+def test_render_ngpu_failed_rank_returns(pt, mode, bad, monkeypatch):
+    """pt_render(ngpu = 3) with one rank failing after its set-up (PT_TUNE inject_fail):
+    the call returns that rank's error -- with same_device=2 (ranks rendering in turn) a
+    failed rank must not leave a later one waiting for its turn."""
+    monkeypatch.setenv("PT_TUNE", "same_device=%s,inject_fail=%d" % (mode, bad))
+    with pt.Scene.load(U.scene_path("c1")) as s:
+        with pytest.raises(pt.PTError, match="injected failure"):
+            s.render(ngpu=3)
 
 
 def test_gather_init_one_rank(pt):

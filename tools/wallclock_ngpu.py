@@ -64,7 +64,9 @@ def run(src, n, tune):
             "cli_phases_ms": cli, "gather_ms": float(g.group(1)) if g else None,
             "setup_ms_max": max(x["setup_ms"] for x in ranks), "setup_ms": [x["setup_ms"] for x in ranks],
             "scene_upload_ms": [x["scene_upload_ms"] for x in ranks], "render_ms": renders,
-            "render_ms_max": max(renders), "resolve_ms": [x["resolve_ms"] for x in ranks]}
+            "render_ms_max": max(renders), "resolve_ms": [x["resolve_ms"] for x in ranks],
+            "coop_ms": [x.get("coop_ms") for x in ranks], "isect_ms": [x.get("isect_ms") for x in ranks],
+            "rounds": [x.get("rounds") for x in ranks], "rank_rays": [x.get("rays") for x in ranks]}
 
 
 def main():
