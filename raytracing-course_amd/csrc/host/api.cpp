@@ -922,11 +922,20 @@ int pt_device_init(int device) {
     HIP_TRY(pt_preload_kernels_wave());
     {
         // the runtime's copy path starts on its first transfer (tens of ms): do one
-        // now, and make the first session's stream
+        // now, and make the first session's stream (a lock per device: the CLI's
+        // per-device threads warm their devices at the same time)
+        struct Warm { std::mutex mu; bool done = false; };
         static std::mutex mu;
-        static std::map<int, bool> warmed;
-        std::lock_guard<std::mutex> lk(mu);
-        if (!warmed[device]) {
+        static std::map<int, std::unique_ptr<Warm>> warmed;
+        Warm* w;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            auto& e = warmed[device];
+            if (!e) e.reset(new Warm());
+            w = e.get();
+        }
+        std::lock_guard<std::mutex> lk(w->mu);
+        if (!w->done) {
             void* d = nullptr;
             uint32_t h = 0;
             hipStream_t s = nullptr;
@@ -937,7 +946,7 @@ int pt_device_init(int device) {
             HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
             std::lock_guard<std::mutex> lk2(g_spare_mu);
             g_spare_streams[device].push_back(s);
-            warmed[device] = true;
+            w->done = true;
         }
     }
     return PT_OK;

@@ -15,6 +15,7 @@
 //    partition move elements as a function of the comparison results only, so
 //    the permutation is identical to sorting the 100-B Primitive objects.
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <stdexcept>
 #include <thread>
@@ -114,10 +115,15 @@ struct Builder {
     };
     void sort_axis(uint32_t first, uint32_t last, int axis, std::vector<KI>& tmp, EqPerm& eq) {
         const uint32_t n = last - first;
-        const float k0 = key[3 * (size_t)perm[first] + axis];
+        // every comparison false <=> each key is NaN or equal to the range's non-NaN keys
+        // (the reference is the first non-NaN key: a NaN reference compares false with
+        // keys that are ordered among themselves)
+        uint32_t j0 = first;
+        while (j0 < last && std::isnan(key[3 * (size_t)perm[j0] + axis])) ++j0;
+        const float k0 = j0 < last ? key[3 * (size_t)perm[j0] + axis] : 0.f;
         bool equal = true;
-        for (uint32_t j = first + 1; j < last && equal; ++j) equal = !(key[3 * (size_t)perm[j] + axis] < k0) &&
-                                                                   !(k0 < key[3 * (size_t)perm[j] + axis]);
+        for (uint32_t j = j0 + 1; j < last && equal; ++j) equal = !(key[3 * (size_t)perm[j] + axis] < k0) &&
+                                                                !(k0 < key[3 * (size_t)perm[j] + axis]);
         if (equal && n > 16u) {
             if (eq.n != n) {
                 eq.n = n;
