@@ -944,8 +944,15 @@ int pt_device_init(int device) {
             HIP_TRY(hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost));
             HIP_TRY(hipFree(d));
             HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+            {
+                std::lock_guard<std::mutex> lk2(g_spare_mu);
+                g_spare_streams[device].push_back(s);
+            }
+            // ... and its early cooperative launch's stream
+            hipStream_t side = nullptr;
+            HIP_TRY(take_stream(device, &side, true));
             std::lock_guard<std::mutex> lk2(g_spare_mu);
-            g_spare_streams[device].push_back(s);
+            g_spare_side[device].push_back(side);
             w->done = true;
         }
     }
@@ -1307,6 +1314,14 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
             }
         }
         if (take_stream(ss->dev, &ss->stream) != hipSuccess) return cleanup(fail(PT_E_HIP, "stream creation failed"));
+        // the early launch's stream and events at set-up (a stream's creation costs ms: not in the pass)
+        if (ss->early_k) {
+            if (take_stream(ss->dev, &ss->side_stream, true) != hipSuccess)
+                return cleanup(fail(PT_E_HIP, "stream creation failed"));
+            if (hipEventCreateWithFlags(&ss->side_taken, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&ss->side_end, hipEventDisableTiming) != hipSuccess)
+                return cleanup(fail(PT_E_HIP, "event creation failed"));
+        }
         void* p = nullptr;
         if (hipMalloc(&p, at) != hipSuccess) return cleanup(fail(PT_E_OOM, "device allocation failed (session buffers)"));
         ss->arena = static_cast<unsigned char*>(p);
