@@ -83,7 +83,9 @@ enum : uint32_t { PE_LIVE = 0u, PE_MISS = 1u, PE_CUT = 2u, PE_TERM = 3u };
 // round counters: set p = ctl + PT_CTL_SET * p; the work-batch heads are one per
 // XCD, each on its own 128-B line (C_HEADS + 32 x)
 enum : uint32_t { C_FRESH = 0u, C_CARRY = 1u, C_DONE = 3u, C_EXACT = 4u, C_FRONT = 5u, C_BACK = 6u, C_WGDONE = 7u,
-                  C_DEADLINE = 8u, C_HEADS = 32u };
+                  C_DEADLINE = 8u, C_ENDED = 9u, C_HEADS = 32u };
+// C_ENDED: k_wcoop chains whose pixel reached the pass target (the final launch stops at
+// side_stop_n of them to hand its last chains to whole-wave teams)
 // C_WGDONE: k_wpath workgroups that have finished the round; C_DEADLINE: the round's end
 // (low 32 bits of the 100-MHz realtime clock, 0 = not set yet; WaveParams::path_ticks)
 #define PT_CTL_SET 288u          // words per counter set (C_HEADS + 8 x 32)
@@ -145,7 +147,9 @@ struct WaveParams {
     // a cooperative launch beside a path round (the early launch): it stops at a chain
     // cycle's end once side_stop counts side_stop_n finished path workgroups, and yields its
     // chains as suspended queries at their start (q_init_pre: the ray was counted when it was
-    // first taken) to yield_cq (counter yield_ctr: the path round's next carry queue)
+    // first taken) to yield_cq (counter yield_ctr: the path round's next carry queue).  The
+    // pass's final launch uses the same stop with side_stop = its own C_ENDED: once all but
+    // its last chains have ended, those go to a launch of whole-wave teams
     const uint32_t* side_stop;
     uint32_t side_stop_n;
     uint32_t* yield_cq;

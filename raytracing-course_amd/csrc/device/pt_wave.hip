@@ -964,6 +964,15 @@ __device__ __forceinline__ bool qc_prim_hit(const SceneView& S, uint32_t i, cons
                            blob_piece(S, o + 48u), ray, h);
 }
 
+// k_wcoop's work counters: per wave in LDS, one LDS add per wave and counting site (a
+// lane-private counter costs a VGPR for the kernel's life; the engine sits at the
+// 3-waves-per-SIMD limit)
+enum : uint32_t { LC_RAYS = 0u, LC_NODES, LC_PTESTS, LC_PLANES, LC_AUX, LC_FALLB, LC_HANDED, LC_N = 8u };
+__device__ __forceinline__ void lc_add(uint32_t* lc, uint32_t k, bool c, uint32_t w = 1u) {
+    const unsigned long long m = __ballot(c);
+    if (m && lane_id() == (uint32_t)__ffsll((long long)m) - 1u) atomicAdd(lc + k, (uint32_t)__popcll(m) * w);
+}
+
 #ifdef PT_CPROF
 // diagnostics build: per-phase shader cycles of the cooperative engine (summed per wave)
 #define QC_T0() uint64_t qc_t = __builtin_amdgcn_s_memtime()
@@ -985,7 +994,7 @@ __device__ __forceinline__ bool qc_prim_hit(const SceneView& S, uint32_t i, cons
 // tells which.  `exact` set = hand the ray to the exact DFS.
 template <uint32_t T>
 __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bool on, const Ray& ray, float P,
-                       int pid, F4 pre, uint32_t reserve, QCounts& C, bool& exact, Hit& hit, bool& bvh QC_CP_ARG) {
+                       int pid, F4 pre, uint32_t reserve, uint32_t* lc, bool& exact, Hit& hit, bool& bvh QC_CP_ARG) {
     QC_T0();
     constexpr uint32_t SCAP = QcTeamLds<T>::SCAP, HCAP = QcTeamLds<T>::HCAP;
     const uint32_t lane = lane_id(), tl = lane % T, tbase = lane - tl;
@@ -1023,7 +1032,7 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
             Node nd;
             nd.a = b4;                             // the leaf's node record: {c.xyz, s.x}, {s.y, s.z, first, count}
             nd.b = F4{b5.x, b5.y, b3.y, b3.z};
-            C.nodes += act ? 1u : 0u;
+            lc_add(lc, LC_NODES, act);
             const bool hb = act && qc_slab_hit(nd, ray, inv, par);
             const uint32_t ref = f2u(b3.y), cnt = hb ? f2u(b3.z) : 0u;
             Hit best;
@@ -1031,15 +1040,15 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
             best.n = mk3(0.f, 0.f, 0.f);
             best.interior = 0u;
             int lid = -1;
+            lc_add(lc, LC_PTESTS, cnt != 0u);
             if (cnt) {
                 Hit hh;
-                C.ptests++;
                 if (qc_prim_hit_rec(S, ref, b0, b1, b2, F4{b3.w, 0.f, 0.f, 0.f}, ray, hh)) { best = hh; lid = (int)ref; }
             }
             for (uint32_t i = 1; __ballot(i < cnt) != 0ull; ++i) {
+                lc_add(lc, LC_PTESTS, i < cnt);
                 if (i < cnt) {
                     Hit hh;
-                    C.ptests++;
                     if (qc_prim_hit(S, ref + i, ray, hh) && hh.t < best.t) { best = hh; lid = (int)(ref + i); }
                 }
             }
@@ -1085,7 +1094,7 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
                 const uint32_t ni = tl / PT_AUXW + j * (T / PT_AUXW);
                 act[j] = ni < k;
                 const uint32_t node = act[j] ? L.stk[ns + ni] : 0u;
-                C.aux += act[j] && e == 0u ? 1u : 0u;
+                lc_add(lc, LC_AUX, act[j] && e == 0u);
                 if (node < QC_TOPN) {
                     ea[j] = Q.top[node * PT_AUXW + e].a;
                     eb[j] = Q.top[node * PT_AUXW + e].b;
@@ -1158,7 +1167,7 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
                 const bool hs = pon && node_slab(nd, ray, t, in);
                 tq[b] = t;
                 hf[b] = (hs ? 1u : 0u) | (in << 1);
-                C.nodes += pon ? 1u : 0u;
+                lc_add(lc, LC_NODES, pon);
             }
 #pragma unroll
             for (uint32_t b = 0; b < NG; ++b) {
@@ -1294,6 +1303,9 @@ k_wcoop(WaveParams P) {
     __shared__ QcScene Q;
     const uint32_t lane = lane_id(), tl = lane % T, tbase = lane - tl;
     QcTeamLds<T>& L = Ls[(threadIdx.x >> 6) * (64u / T) + lane / T];
+    __shared__ uint32_t Lc[QC_WAVES][LC_N];
+    uint32_t* lc = Lc[threadIdx.x >> 6];
+    if (lane < LC_N) lc[lane] = 0u;
     {
         // this launch's copies: the first planes and emitters, the aux BVH's top nodes
         F4* q = reinterpret_cast<F4*>(&Q);
@@ -1313,8 +1325,7 @@ k_wcoop(WaveParams P) {
     uint32_t* out = P.ctl + PT_CTL_SET * (1u - P.parity);
     const uint32_t n_carry = in[C_CARRY], n_total = in[C_FRESH] + n_carry;
     const RayQ FQ = P.fq[P.parity];
-    QCounts C{0u, 0u, 0u, 0u};
-    uint32_t rays = 0u, fallbacks = 0u, prog = 0u;
+    uint32_t prog = 0u;   // finished samples not yet reported (wave-uniform)
 #ifdef PT_CPROF
     // expansion, candidates, decisions, shading, next ray, chain cycles, chains, wave lifetime
     uint64_t cp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1375,7 +1386,8 @@ k_wcoop(WaveParams P) {
                         Pt = d.w;
                         pid = FQ.pid[fi];
                         pre = FQ.ri[fi];
-                        if (tl == 0u) { rays++; C.planes += P.S.n_planes; }
+                        lc_add(lc, LC_RAYS, tl == 0u);
+                        lc_add(lc, LC_PLANES, tl == 0u, P.S.n_planes);
                     }
                     // the pixel's state for the chain's life: RNG / vertices / samples and the
                     // sum in the first lane's registers, the current path's fold records in LDS
@@ -1397,15 +1409,18 @@ k_wcoop(WaveParams P) {
         if (__ballot(have) == 0ull) break;
         bool ex, bvh;
         Hit h;
-        int id = qc_team<T>(P.S, Q, L, have, ray, Pt, pid, pre, P.coop_reserve, C, ex, h, bvh QC_CP_PASS);
+        int id = qc_team<T>(P.S, Q, L, have, ray, Pt, pid, pre, P.coop_reserve, lc, ex, h, bvh QC_CP_PASS);
         bool emit = false, sdone = false;
         QC_T0();
         if (tl == 0u && have) {
             if (ex) {
                 // the exact stack DFS (non-finite rays, too many hitting leaves)
                 LdsMemN<1u> stk{L.stk};
-                id = q_exact(P.S, ray, stk, h, C);
-                fallbacks++;
+                QCounts Cx{0u, 0u, 0u, 0u};
+                id = q_exact(P.S, ray, stk, h, Cx);
+                atomicAdd(lc + LC_NODES, Cx.nodes);
+                atomicAdd(lc + LC_PTESTS, Cx.ptests);
+                atomicAdd(lc + LC_FALLB, 1u);
             } else if (id >= 0 && !bvh) {
                 // the plane hit (its record from the LDS copy)
                 Prim pr = P.S.prims[id];
@@ -1414,11 +1429,19 @@ k_wcoop(WaveParams P) {
                 (void)prim_intersect(pr, ray, h);
             }
             emit = coop_shade<BIG>(P, Q, L, px, slot, ray, id, h, sdone);
-            prog += sdone ? 1u : 0u;
-            if (emit) { rays++; C.planes += P.S.n_planes; }
         }
+        prog += (uint32_t)__popcll(__ballot(sdone));
+        lc_add(lc, LC_RAYS, emit);
+        lc_add(lc, LC_PLANES, emit, P.S.n_planes);
         emit = __shfl(emit ? 1 : 0, (int)tbase, 64) != 0;
         QC_TICK(3);
+        {
+            // chains that end here (their pixel reached the target): counted for the final
+            // launch's stop (one atomic per wave)
+            const unsigned long long me = __ballot(have && !emit && tl == 0u);
+            if (P.side_stop && me && lane == (uint32_t)__ffsll((long long)me) - 1u)
+                atomicAdd(out + C_ENDED, (uint32_t)__popcll(me));
+        }
         if (have && !emit) {
 #ifdef PT_CPROF
             // when the chains end: a histogram over 2^20-cycle buckets of the wave's lifetime
@@ -1451,12 +1474,12 @@ k_wcoop(WaveParams P) {
 #endif
         }
         QC_TICK(4);
-        if (P.progress && tl == 0u && prog >= 256u) {
-            __hip_atomic_fetch_add(P.progress, (unsigned long long)prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (P.progress && prog >= 256u) {
+            if (lane == 0u)
+                __hip_atomic_fetch_add(P.progress, (unsigned long long)prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             prog = 0u;
         }
     }
-    uint32_t handed = 0u;
     if (stopped) {
         // A launch beside a path round that stopped: each team's next query, as a
         // suspended query at its start, to the round's next carry queue (a resumed query is
@@ -1510,11 +1533,11 @@ k_wcoop(WaveParams P) {
                 rp = d.w;
                 rid = FQ.pid[fi];
                 rpre = FQ.ri[fi];
-                rays++;
-                C.planes += P.S.n_planes;
             }
+            lc_add(lc, LC_RAYS, on && gi >= n_carry);
+            lc_add(lc, LC_PLANES, on && gi >= n_carry, P.S.n_planes);
+            lc_add(lc, LC_HANDED, on);
             const uint32_t k2 = wave_append(P.yield_ctr, on);
-            handed += on ? 1u : 0u;
             if (on) {
                 Query q;
                 q_init_pre(r, rp, rid, rpre, q);
@@ -1524,21 +1547,22 @@ k_wcoop(WaveParams P) {
             }
         }
     }
-    if (P.progress && tl == 0u && prog)
+    if (P.progress && lane == 0u && prog)
         __hip_atomic_fetch_add(P.progress, (unsigned long long)prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    unsigned long long* ctr = ctr_copy(P.counters);
-    wave_add_u64(ctr + 0, rays);
-    wave_add_u64(ctr + 1, C.nodes);
-    wave_add_u64(ctr + 2, C.ptests);
-    wave_add_u64(ctr + 3, C.planes);
-    wave_add_u64(ctr + 5, C.aux);
-    wave_add_u64(ctr + 6, fallbacks);
-    // this engine's share (pt_stats coop_*)
-    wave_add_u64(ctr + 8, rays);
-    wave_add_u64(ctr + 9, C.nodes);
-    wave_add_u64(ctr + 10, C.ptests);
-    wave_add_u64(ctr + 13, C.aux);
-    wave_add_u64(ctr + CTR_HANDON, handed);
+    // the wave's counters (LDS) to this XCD's statistics copy: the totals, and this engine's
+    // share (pt_stats coop_*)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0u) {
+        unsigned long long* ctr = ctr_copy(P.counters);
+        const uint32_t v[LC_N] = {lc[0], lc[1], lc[2], lc[3], lc[4], lc[5], lc[6], lc[7]};
+        const uint32_t to[LC_N] = {0u, 1u, 2u, 3u, 5u, 6u, CTR_HANDON, 0u};
+        for (uint32_t k = 0; k < LC_HANDED + 1u; ++k)
+            if (v[k]) atomicAdd(ctr + to[k], (unsigned long long)v[k]);
+        if (v[LC_RAYS]) atomicAdd(ctr + 8, (unsigned long long)v[LC_RAYS]);
+        if (v[LC_NODES]) atomicAdd(ctr + 9, (unsigned long long)v[LC_NODES]);
+        if (v[LC_PTESTS]) atomicAdd(ctr + 10, (unsigned long long)v[LC_PTESTS]);
+        if (v[LC_AUX]) atomicAdd(ctr + 13, (unsigned long long)v[LC_AUX]);
+    }
 #ifdef PT_CPROF
     // (per team first lanes: chain counts; cycle sums are per wave, counted by lane 0)
     cp[7] = __builtin_amdgcn_s_memtime() - cp_start;

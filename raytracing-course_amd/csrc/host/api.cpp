@@ -93,6 +93,8 @@ const Rccl& rccl() {
 //                     768 per CU; the mix of the other rounds)
 //   lowq_wg=N         ... and their path workgroups per CU (PT_CMAX chains each; default 2)
 //   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
+//   coop_grow=N       the final cooperative launch (teams of 8) hands its last N chains to a launch
+//                     of whole-wave teams (default: 4 per CU; 0 = never)
 //   coop_order=0      the pass's final cooperative launch takes its chains in queue order (default:
 //                     the pixels with the most samples left first)
 //   early=K, early_at=N, early_wg=W
@@ -288,6 +290,7 @@ struct pt_session {
     uint32_t* side_ctl = nullptr;     // ... and its two round-counter sets
     hipStream_t side_stream = nullptr;
     hipEvent_t side_taken = nullptr, side_end = nullptr;   // its queue is taken / it has stopped
+    uint32_t coop_grow = 0;       // the final launch's last chains handed to whole-wave teams (0: never)
     uint32_t coop_team = 8;       // lanes per chain in the cooperative engine (pure-coop rate, teams of
                                   // 64 / 32 / 16 / 8: 283 / 392 / 572 / 815 Mray/s)
     // every device buffer below lives in one allocation (pt_session_create)
@@ -1237,6 +1240,8 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         if (ss->coop_max && !tune_has("sparse")) ss->path_sparse = std::min(ss->path_sparse, ss->coop_max);
         ss->round_batch = (uint32_t)std::max(1, tune_int("round_batch", (int)ss->round_batch));
         ss->coop_order = tune_int("coop_order", 1) != 0;
+        // the final launch's last chains to whole-wave teams: what one whole-wave wave per SIMD holds
+        ss->coop_grow = (uint32_t)std::max(0, tune_int("coop_grow", (int)(cus * 4u)));
         // Early cooperative launch (teams of 8, QC_WAVES waves per workgroup: 32 chains each):
         // the low-chain rounds leave each CU room for one more workgroup, which the heaviest
         // chains use from then on instead of waiting for the final hand-over
@@ -1487,11 +1492,15 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     bool counted = false;
     for (uint32_t guard = 0;; ++guard) {
         if (chains <= ss->coop_max) {
-            // the cooperative engine runs every remaining chain to the end of the pass, one launch
-            {
-                // (a scene beyond the engine's LDS tables runs the BIG instantiation: teams of 8 or 64)
-                const bool big = ss->depth > QC_FOLD || s->planes.size() > QC_NPL || s->emitters.size() > QC_NEM;
-                const uint32_t team = big && ss->coop_team != 64u ? 8u : ss->coop_team;
+            // The cooperative engine runs every remaining chain to the end of the pass.  A
+            // launch of teams of 8 (the default) stops once all but ss->coop_grow of its chains
+            // have ended and hands those -- the pass's slowest, whose chain cycle sets the
+            // launch's end -- to a launch of whole-wave teams (the shortest cycle).
+            // (a scene beyond the engine's LDS tables runs the BIG instantiation: teams of 8 or 64)
+            const bool big = ss->depth > QC_FOLD || s->planes.size() > QC_NPL || s->emitters.size() > QC_NEM;
+            uint32_t team = big && ss->coop_team != 64u ? 8u : ss->coop_team;
+            for (uint32_t launch = 0;; ++launch) {
+                const bool grow = launch == 0 && team != 64u && ss->coop_grow && chains > ss->coop_grow;
                 wp.parity = p;
                 hipEvent_t i0, i1;
                 HIP_TRY(hipEventCreate(&i0));
@@ -1517,7 +1526,17 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                     wp.order = ss->order + 2 * PT_ORDER_BUCKETS;
                     HIP_TRY(pt_launch_coop_order(wp, chains, ss->stream));
                 }
-                HIP_TRY(pt_launch_coop(wp, grid, team, big, ss->stream, i0, i1));
+                pt::WaveParams cp_ = wp;
+                if (grow) {
+                    // stop at the chain cycle after all but coop_grow chains have ended (its own
+                    // C_ENDED); the rest go to the next launch's input as suspended queries
+                    uint32_t* out = ss->ctl + PT_CTL_SET * (1u - p);
+                    cp_.side_stop = out + pt::C_ENDED;
+                    cp_.side_stop_n = chains - ss->coop_grow;
+                    cp_.yield_cq = wp.cq[1u - p];
+                    cp_.yield_ctr = out + pt::C_CARRY;
+                }
+                HIP_TRY(pt_launch_coop(cp_, grid, team, big, ss->stream, i0, i1));
                 wp.order = wp.order_cur = nullptr;
                 if (cprof) {
                     unsigned long long cp[64];
@@ -1548,8 +1567,13 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                     HIP_TRY(e);
                 }
                 HIP_TRY(hipStreamSynchronize(ss->stream));
-                if (ss->ctl_host[pt::C_CARRY] != 0u || ss->ctl_host[pt::C_FRESH] != 0u)
-                    return fail(PT_E_HIP, "cooperative engine left chains behind");
+                const uint32_t left = ss->ctl_host[pt::C_CARRY] + ss->ctl_host[pt::C_FRESH];
+                if (left == 0u) break;
+                if (!grow) return fail(PT_E_HIP, "cooperative engine left chains behind");
+                // the last chains: whole-wave teams
+                chains = left;
+                team = 64u;
+                if (tune_int("roundlog", 0) >= 2) fprintf(stderr, "coop grow: %u chains to teams of 64\n", left);
             }
             break;
         }
