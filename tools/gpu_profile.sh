@@ -10,8 +10,8 @@ export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/prof
 rm -rf $OUT
 mkdir -p $OUT
-STEPS=${STEPS:-4}
-B="python3 bench.py --no-cpu-baseline --no-wallclock --steps $STEPS --warmup 1"
+STEPS=${STEPS:-20}
+B="python3 bench.py --no-cpu-baseline --no-wallclock --steps $STEPS --warmup 5"
 timeout -s KILL 60 rocprofv3 -L > $OUT/avail.txt 2>&1 || true
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- \
   $B > $OUT/bench_kt.json 2> $OUT/bench_kt.err && echo KT_OK &&
@@ -24,7 +24,7 @@ timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU \
   SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_sq -o run -- \
   $B > $OUT/bench_sq.json 2> $OUT/bench_sq.err && echo SQ_OK &&
-timeout -k 10 900 python3 bench.py ${BENCH_ARGS:-} > $OUT/bench_default.json 2> $OUT/bench_default.err && echo BENCH_OK &&
+timeout -k 10 900 python3 bench.py --steps 20 --warmup 5 ${BENCH_ARGS:-} > $OUT/bench_default.json 2> $OUT/bench_default.err && echo BENCH_OK &&
 cat $OUT/bench_default.json || exit 1
 # instruction-mix pass: only the counters this rocprofv3 lists
 SQ2=""
