@@ -102,6 +102,7 @@ const Rccl& rccl() {
 //                     its K heaviest chains (1: what W cooperative workgroups per CU hold) in a
 //                     cooperative launch on a second stream beside it; the launch hands its chains
 //                     back when the round's path workgroups finish (default: 1; 0 = off)
+//   side_team=16      that launch's teams of 16 lanes (default 8)
 //   side_prio=0|1|2   that launch's stream: 0 normal priority (may share a main stream's
 //                     hardware queue), 1 the greatest priority (a queue pool of its own; default),
 //                     2 a CU-masked stream over every CU (always a queue of its own); take_stream
@@ -284,7 +285,7 @@ struct pt_session {
     // early cooperative launch: once a pass's chains fall below early_at, the early_k chains
     // with the most samples left run in a cooperative launch on a second stream (early_wg
     // workgroups per CU, beside the path engine's low-chain rounds) to the end of the pass
-    uint32_t early_k = 0, early_at = 0, early_wg = 1;
+    uint32_t early_k = 0, early_at = 0, early_wg = 1, side_team = 8;
     pt::RayQ side = {};           // its queue (early_k entries) ...
     uint32_t* side_carry = nullptr;   // ... its suspended queries' restart records (early_k x carry_words)
     uint32_t* side_ctl = nullptr;     // ... and its two round-counter sets
@@ -1248,7 +1249,11 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         ss->early_wg = (uint32_t)std::max(1, tune_int("early_wg", 1));
         ss->early_at = (uint32_t)std::max(0, tune_int("early_at", (int)(cus * 768u)));
         ss->early_k = (uint32_t)std::max(0, tune_int("early", 1));
-        if (ss->early_k == 1u) ss->early_k = cus * ss->early_wg * QC_WAVES * 8u;   // early=1: what it holds
+        // lanes per chain of that launch: 8 (default) or 16 (half the chains, a shorter chain cycle)
+        // (a scene beyond the LDS tables has only the teams-of-8 BIG instantiation)
+        const bool big = ss->depth > QC_FOLD || s->planes.size() > QC_NPL || s->emitters.size() > QC_NEM;
+        ss->side_team = tune_int("side_team", 8) == 16 && !big ? 16u : 8u;
+        if (ss->early_k == 1u) ss->early_k = cus * ss->early_wg * QC_WAVES * (64u / ss->side_team);   // early=1: what it holds
         if (!ss->coop_max || ss->coop_team != 8u) ss->early_k = 0;
         // a round's carry output also takes the early launch's yielded chains
         ss->carry_cap = (uint32_t)std::min<uint64_t>(n, (uint64_t)ss->lane_cap + ss->early_k);
@@ -1640,7 +1645,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                     HIP_TRY(hipEventRecord(i0, ss->stream));   // (timed with the round)
                     HIP_TRY(hipEventRecord(i1, ss->stream));
                 } else {
-                    HIP_TRY(pt_launch_coop(sp, ss->early_wg * (ss->coop_grid / 8u), 8u, big, ss->side_stream, i0, i1));
+                    HIP_TRY(pt_launch_coop(sp, ss->early_wg * (ss->coop_grid / 8u), ss->side_team, big, ss->side_stream, i0, i1));
                     HIP_TRY(hipEventRecord(ss->side_end, ss->side_stream));
                 }
                 // the path round takes the other chains: items k .. chains of the order
@@ -1684,7 +1689,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 // (it yields into the round's output counters, which the round's own launch
                 // zeroed: a side launch that could yield before that zeroing would lose items)
                 const bool big = ss->depth > QC_FOLD || s->planes.size() > QC_NPL || s->emitters.size() > QC_NEM;
-                HIP_TRY(pt_launch_coop(late_sp, late_grid, 8u, big, ss->stream));
+                HIP_TRY(pt_launch_coop(late_sp, late_grid, ss->side_team, big, ss->stream));
                 HIP_TRY(hipEventRecord(ss->side_end, ss->stream));
                 late = false;
             }

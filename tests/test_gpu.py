@@ -376,6 +376,7 @@ TUNE_KEYS = ["wg_per_cu=2", "wg_per_cu=1", "runend=1000000", "sparse_steps=2", "
              # every early workgroup a late one (side_late), the side stream at each priority
              "coop=300,early=1,early_at=100000000,side_late=1",
              "coop=300,early=1,early_at=100000000,side_prio=0", "coop=300,early=1,early_at=100000000,side_prio=2",
+             "coop=300,early=1,early_at=100000000,side_team=16",
              # diagnostics hooks (their counters are compiled in only with -DPT_CPROF / -DPT_WPROF;
              # the host side runs in every build)
              "coop=300,cprof=1", "wgprof=/tmp/pt_wgprof_test.bin"]
