@@ -75,6 +75,7 @@ const Rccl& rccl() {
 //   engine=mega       megakernel instead of the wavefront path engine (replay traversal)
 //   budget_us=N       path engine: a round ends N us after its work ran out, for every wave at once
 //                     (default 2500; 0: each wave after `budget` trips of its own)
+//   lowq_budget_us=N  ... the same for the low-chain rounds (default: budget_us)
 //   budget=N          ... trips a query wave keeps its chains after the round's work ran out, when
 //                     budget_us is 0 or budget alone is given (default 1024)
 //   wg_per_cu=N       path engine: workgroups per CU (grid)
@@ -272,7 +273,7 @@ struct pt_session {
     unsigned long long* wg_prof = nullptr;
     // wavefront engine buffers (replay traversal)
     bool wave = false;
-    uint32_t path_grid = 0, path_budget = 1024, path_ticks = 0, path_runend = 0, path_sparse = 0, sparse_steps = 8;
+    uint32_t path_grid = 0, path_budget = 1024, path_ticks = 0, low_ticks = 0, path_runend = 0, path_sparse = 0, sparse_steps = 8;
     uint32_t coop_max = 0, coop_grid = 0, coop_reserve = 0;   // cooperative engine (k_wcoop) at the end of a pass
     uint32_t round_batch = 1;     // rounds launched per count while the chains are far above the hand-over
     // k_wpath's per-trip step mix: {probe_every, probe_min, aux_extra}, and the one of
@@ -1191,6 +1192,10 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // wave after `budget` trips of its own, also the mode of an explicit budget=N alone)
         // (at most 10 s: the device compares 32-bit clock differences as signed)
         ss->path_ticks = (uint32_t)std::min(10000000, std::max(0, tune_int("budget_us", tune_has("budget") ? 0 : 2500))) * 100u;
+        // ... and the low-chain rounds' deadline (default: the same)
+        ss->low_ticks = tune_has("lowq_budget_us")
+                            ? (uint32_t)std::min(10000000, std::max(1, tune_int("lowq_budget_us", 2500))) * 100u
+                            : ss->path_ticks;
         const int wg_cu = std::max(1, (int)(PT_PATH_WAVES_PER_EU * 4u / (PT_NQ + 1u)));
         ss->path_grid = cus * (uint32_t)std::max(1, tune_int("wg_per_cu", wg_cu));
         // suspended-query records: Query | slot | aux stack, rounded to 16 B.  Only a
@@ -1674,6 +1679,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             uint32_t grid = ss->path_grid;
             {
                 const bool low = chains < ss->lowq;
+                wp.path_ticks = low ? ss->low_ticks : ss->path_ticks;
                 const uint32_t* m = low ? ss->mix_low : ss->mix;
                 wp.probe_every = m[0];
                 wp.probe_min = m[1];

@@ -360,7 +360,7 @@ def test_cli_ngpu_sessions_on_one_device(pt, tmp_path, mode):
 # coop, coop_team, lstack, same_device: the tests above.)
 TUNE_KEYS = ["wg_per_cu=2", "wg_per_cu=1", "runend=1000000", "sparse_steps=2", "sparse_steps=16", "round_batch=4",
              "probe_every=1", "probe_min=1", "aux_extra=0", "aux_extra=3", "lowq=0", "lowq=100000000",
-             "lowq=100000000,lowq_wg=1", "lowq=100000000,lowq_probe_every=1,lowq_probe_min=2,lowq_aux_extra=2",
+             "lowq=100000000,lowq_wg=1", "lowq=100000000,lowq_budget_us=20", "lowq=100000000,lowq_probe_every=1,lowq_probe_min=2,lowq_aux_extra=2",
              "cap=64", "batch=1", "batch=64", "budget_us=20", "budget_us=0", "roundlog=1", "roundlog=2", "roundlog=3", "prepstats=1",
              # the cooperative engine after the path rounds, intake in queue order / by samples left
              "coop=300,coop_order=0", "coop=300,coop_order=1",
