@@ -153,17 +153,20 @@ def test_device_init(pt):
     assert pt._lib.pt_device_init(4096) == pt.PT_E_NO_GPU
 
 
-@pytest.mark.parametrize("engine", ["coop64", "coop32", "coop16", "coop8", "path"])
+@pytest.mark.parametrize("engine", ["coop64", "coop32", "coop16", "coop8", "coop8grow", "path"])
 @pytest.mark.parametrize("name", sorted(M["images"]))
 def test_golden_images_each_engine(pt, name, engine, monkeypatch):
     """The replay traversal with one engine for the whole pass: the cooperative
     engine (a team of 64, 32 or 16 lanes per chain: breadth-first aux expansion,
     all candidate leaves at once, root paths a block of nodes per round;
     pt_coop.h) or the path engine alone (coop=0).  All must reproduce the
-    reference's bytes and ray count."""
+    reference's bytes and ray count.  coop8grow: teams of 8 that hand their last 64
+    chains to whole-wave teams (a second launch, coop_grow)."""
     coop = engine.startswith("coop")
-    team = engine[4:] if coop else "64"
-    monkeypatch.setenv("PT_TUNE", "coop=%s,coop_team=%s" % ("100000000" if coop else "0", team))
+    grow = engine.endswith("grow")
+    team = engine[4:].replace("grow", "") if coop else "64"
+    monkeypatch.setenv("PT_TUNE", "coop=%s,coop_team=%s,coop_grow=%d" % ("100000000" if coop else "0", team,
+                                                                       64 if grow else 0))
     m, img, rad = U.golden_image(name)
     with pt.Scene.load(U.golden_scene_path(name)) as s:
         s.prepare()
@@ -173,21 +176,26 @@ def test_golden_images_each_engine(pt, name, engine, monkeypatch):
     assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
     assert np.array_equal(rgb, img)
     if coop:
-        assert st["rounds"] == 1
+        # (every golden image has more than 64 pixels)
+        assert st["rounds"] == (2 if grow else 1)
 
 
-@pytest.mark.parametrize("team", ["64", "16", "8"])
+@pytest.mark.parametrize("team", ["64", "16", "8", "8grow"])
 @pytest.mark.parametrize("cfg", ["c1", "c2"])
 def test_coop_engine_full_config_md5(pt, cfg, team, monkeypatch):
-    """Configs 1 and 2 entirely on the cooperative engine: reference md5 and ray count."""
-    monkeypatch.setenv("PT_TUNE", "coop=100000000,coop_team=%s" % team)
+    """Configs 1 and 2 entirely on the cooperative engine: reference md5 and ray count
+    (8grow: teams of 8, the last 1,024 chains to whole-wave teams -- the default
+    hand-over of the pass's final launch)."""
+    grow = team.endswith("grow")
+    monkeypatch.setenv("PT_TUNE", "coop=100000000,coop_team=%s,coop_grow=%d" % (team.replace("grow", ""),
+                                                                             1024 if grow else 0))
     full = M["full"][cfg]
     with pt.Scene.load(U.scene_path(cfg)) as s:
         rgb, _, st = s.render()
         w, h = s.info["width"], s.info["height"]
     ppm = b"P6\n%d %d\n255\n" % (w, h) + rgb.tobytes()
     assert U.md5(ppm) == full["md5"]
-    assert st["rays"] == full["rays"] and st["rounds"] == 1
+    assert st["rays"] == full["rays"] and st["rounds"] == (2 if grow else 1)
 
 
 @pytest.mark.parametrize("engine", ["path", "path_dense", "path_coop"])
