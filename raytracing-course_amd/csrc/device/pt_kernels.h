@@ -161,6 +161,8 @@ struct WaveParams {
 // the untaken items are dropped instead of handed on (a lost chain: the resolve's check)
 #define PT_SIDE_LATE 1u
 #define PT_SIDE_NO_HANDON 2u
+// the final launch's stop: side_stop (its C_ENDED) against n_total - side_stop_n
+#define PT_STOP_GROW 4u
 #define PT_ORDER_BUCKETS 256u
 
 // path engine geometry: PT_NQ query waves + 1 shade wave per workgroup; at most

@@ -1326,6 +1326,10 @@ k_wcoop(WaveParams P) {
     const uint32_t n_carry = in[C_CARRY], n_total = in[C_FRESH] + n_carry;
     const RayQ FQ = P.fq[P.parity];
     uint32_t prog = 0u;   // finished samples not yet reported (wave-uniform)
+    // the stop count: side_stop_n finished path workgroups, or (the final launch's hand-over
+    // to whole-wave teams) all but side_stop_n of this launch's work items ended
+    const uint32_t stop_n = !(P.side_flags & PT_STOP_GROW) ? P.side_stop_n
+                            : n_total > P.side_stop_n ? n_total - P.side_stop_n : 0xffffffffu;
 #ifdef PT_CPROF
     // expansion, candidates, decisions, shading, next ray, chain cycles, chains, wave lifetime
     uint64_t cp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1350,7 +1354,7 @@ k_wcoop(WaveParams P) {
             uint32_t fin = 0u;
             if (lane == 0u) fin = __hip_atomic_load(P.side_stop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
             fin = __builtin_amdgcn_readfirstlane(fin);
-            if (fin >= P.side_stop_n || (P.side_flags & PT_SIDE_LATE)) {
+            if (fin >= stop_n || (P.side_flags & PT_SIDE_LATE)) {
                 stopped = true;
                 break;
             }

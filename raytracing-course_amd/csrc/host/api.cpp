@@ -1542,7 +1542,8 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                     // C_ENDED); the rest go to the next launch's input as suspended queries
                     uint32_t* out = ss->ctl + PT_CTL_SET * (1u - p);
                     cp_.side_stop = out + pt::C_ENDED;
-                    cp_.side_stop_n = chains - ss->coop_grow;
+                    cp_.side_stop_n = ss->coop_grow;   // (against the launch's own item count: before
+                    cp_.side_flags = PT_STOP_GROW;      //  the first count, `chains` is the slot count)
                     cp_.yield_cq = wp.cq[1u - p];
                     cp_.yield_ctr = out + pt::C_CARRY;
                 }
