@@ -176,8 +176,9 @@ def test_golden_images_each_engine(pt, name, engine, monkeypatch):
     assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
     assert np.array_equal(rgb, img)
     if coop:
-        # (every golden image has more than 64 pixels)
-        assert st["rounds"] == (2 if grow else 1)
+        # (the hand-over happens only if a chain is still running at a chain cycle after
+        # all but 64 have ended: at a few spp the last ones can all end in that cycle)
+        assert st["rounds"] in ((1, 2) if grow else (1,))
 
 
 @pytest.mark.parametrize("team", ["64", "16", "8", "8grow"])
