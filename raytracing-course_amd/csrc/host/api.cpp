@@ -75,7 +75,7 @@ const Rccl& rccl() {
 //   engine=mega       megakernel instead of the wavefront path engine (replay traversal)
 //   budget_us=N       path engine: a round ends N us after its work ran out, for every wave at once
 //                     (default 2500; 0: each wave after `budget` trips of its own)
-//   lowq_budget_us=N  ... the same for the low-chain rounds (default: budget_us)
+//   lowq_budget_us=N  ... the same for the low-chain rounds (default 5000)
 //   budget=N          ... trips a query wave keeps its chains after the round's work ran out, when
 //                     budget_us is 0 or budget alone is given (default 1024)
 //   wg_per_cu=N       path engine: workgroups per CU (grid)
@@ -95,7 +95,7 @@ const Rccl& rccl() {
 //   lowq_wg=N         ... and their path workgroups per CU (PT_CMAX chains each; default 2)
 //   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
 //   coop_grow=N       the final cooperative launch (teams of 8) hands its last N chains to a launch
-//                     of whole-wave teams (default: 4 per CU; 0 = never)
+//                     of whole-wave teams (default: 16 per CU; 0 = never)
 //   coop_order=0      the pass's final cooperative launch takes its chains in queue order (default:
 //                     the pixels with the most samples left first)
 //   early=K, early_at=N, early_wg=W
@@ -1192,10 +1192,13 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // wave after `budget` trips of its own, also the mode of an explicit budget=N alone)
         // (at most 10 s: the device compares 32-bit clock differences as signed)
         ss->path_ticks = (uint32_t)std::min(10000000, std::max(0, tune_int("budget_us", tune_has("budget") ? 0 : 2500))) * 100u;
-        // ... and the low-chain rounds' deadline (default: the same)
-        ss->low_ticks = tune_has("lowq_budget_us")
-                            ? (uint32_t)std::min(10000000, std::max(1, tune_int("lowq_budget_us", 2500))) * 100u
-                            : ss->path_ticks;
+        // ... and the low-chain rounds' deadline: 5 ms (fewer rounds, each of which re-sorts and
+        // re-takes the early launch's heaviest chains; with coop_grow 16 per CU, one GPU call,
+        // 3 repeats of every rank (tools/gpu_r5_ab.sh, profiles/r05_ab): rank of 8 mean 83.5 ->
+        // 80.2 ms per 256-spp pass, rank of 4 139.9 -> 137.6, of 2 259.2 -> 255.6, one GPU
+        // 488.8 -> 486.3); with budget_us=0 (trip budgets) the path rounds' mode
+        ss->low_ticks = ss->path_ticks == 0 ? 0u
+                        : (uint32_t)std::min(10000000, std::max(1, tune_int("lowq_budget_us", 5000))) * 100u;
         const int wg_cu = std::max(1, (int)(PT_PATH_WAVES_PER_EU * 4u / (PT_NQ + 1u)));
         ss->path_grid = cus * (uint32_t)std::max(1, tune_int("wg_per_cu", wg_cu));
         // suspended-query records: Query | slot | aux stack, rounded to 16 B.  Only a
@@ -1246,8 +1249,9 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         if (ss->coop_max && !tune_has("sparse")) ss->path_sparse = std::min(ss->path_sparse, ss->coop_max);
         ss->round_batch = (uint32_t)std::max(1, tune_int("round_batch", (int)ss->round_batch));
         ss->coop_order = tune_int("coop_order", 1) != 0;
-        // the final launch's last chains to whole-wave teams: what one whole-wave wave per SIMD holds
-        ss->coop_grow = (uint32_t)std::max(0, tune_int("coop_grow", (int)(cus * 4u)));
+        // the final launch's last chains to whole-wave teams: 16 per CU (4 per CU measured within
+        // the spread of 0; 16 with the 5-ms low-round deadline above: see low_ticks)
+        ss->coop_grow = (uint32_t)std::max(0, tune_int("coop_grow", (int)(cus * 16u)));
         // Early cooperative launch (teams of 8, QC_WAVES waves per workgroup: 32 chains each):
         // the low-chain rounds leave each CU room for one more workgroup, which the heaviest
         // chains use from then on instead of waiting for the final hand-over
