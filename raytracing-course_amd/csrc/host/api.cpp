@@ -1197,8 +1197,9 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // 3 repeats of every rank (tools/gpu_r5_ab.sh, profiles/r05_ab): rank of 8 mean 83.5 ->
         // 80.2 ms per 256-spp pass, rank of 4 139.9 -> 137.6, of 2 259.2 -> 255.6, one GPU
         // 488.8 -> 486.3); with budget_us=0 (trip budgets) the path rounds' mode
-        ss->low_ticks = ss->path_ticks == 0 ? 0u
-                        : (uint32_t)std::min(10000000, std::max(1, tune_int("lowq_budget_us", 5000))) * 100u;
+        ss->low_ticks = tune_has("lowq_budget_us")
+                            ? (uint32_t)std::min(10000000, std::max(1, tune_int("lowq_budget_us", 5000))) * 100u
+                            : ss->path_ticks == 0 ? 0u : 500000u;
         const int wg_cu = std::max(1, (int)(PT_PATH_WAVES_PER_EU * 4u / (PT_NQ + 1u)));
         ss->path_grid = cus * (uint32_t)std::max(1, tune_int("wg_per_cu", wg_cu));
         // suspended-query records: Query | slot | aux stack, rounded to 16 B.  Only a
