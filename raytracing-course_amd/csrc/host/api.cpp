@@ -96,6 +96,7 @@ const Rccl& rccl() {
 //   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
 //   coop_grow=N       the final cooperative launch (teams of 8) hands its last N chains to a launch
 //                     of whole-wave teams (default: 16 per CU; 0 = never)
+//   coop_grow_mid=N   ... and, before that, its last N chains to teams of 32 (default 0: no such stage)
 //   coop_order=0      the pass's final cooperative launch takes its chains in queue order (default:
 //                     the pixels with the most samples left first)
 //   early=K, early_at=N, early_wg=W
@@ -293,6 +294,7 @@ struct pt_session {
     hipStream_t side_stream = nullptr;
     hipEvent_t side_taken = nullptr, side_end = nullptr;   // its queue is taken / it has stopped
     uint32_t coop_grow = 0;       // the final launch's last chains handed to whole-wave teams (0: never)
+    uint32_t coop_grow_mid = 0;   // ... and an earlier stage of teams of 32 (0: none)
     uint32_t coop_team = 8;       // lanes per chain in the cooperative engine (pure-coop rate, teams of
                                   // 64 / 32 / 16 / 8: 283 / 392 / 572 / 815 Mray/s)
     // every device buffer below lives in one allocation (pt_session_create)
@@ -1253,6 +1255,10 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // the final launch's last chains to whole-wave teams: 16 per CU (4 per CU measured within
         // the spread of 0; 16 with the 5-ms low-round deadline above: see low_ticks)
         ss->coop_grow = (uint32_t)std::max(0, tune_int("coop_grow", (int)(cus * 16u)));
+        // ... and, before that, its last coop_grow_mid chains to teams of 32 (0: no such stage; a
+        // tree too deep for the teams-of-32 stack skips it)
+        ss->coop_grow_mid = (uint32_t)std::max(0, tune_int("coop_grow_mid", 0));
+        if (192u < reserve + 64u || s->max_stack > 192u) ss->coop_grow_mid = 0u;
         // Early cooperative launch (teams of 8, QC_WAVES waves per workgroup: 32 chains each):
         // the low-chain rounds leave each CU room for one more workgroup, which the heaviest
         // chains use from then on instead of waiting for the final hand-over
@@ -1514,8 +1520,16 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             // (a scene beyond the engine's LDS tables runs the BIG instantiation: teams of 8 or 64)
             const bool big = ss->depth > QC_FOLD || s->planes.size() > QC_NPL || s->emitters.size() > QC_NEM;
             uint32_t team = big && ss->coop_team != 64u ? 8u : ss->coop_team;
-            for (uint32_t launch = 0;; ++launch) {
-                const bool grow = launch == 0 && team != 64u && ss->coop_grow && chains > ss->coop_grow;
+            for (;;) {
+                // the next stage: teams of 8 -> (coop_grow_mid) teams of 32 -> (coop_grow) whole waves
+                uint32_t keep = 0u, next_team = 64u;
+                if (team == 8u && !big && ss->coop_grow_mid > ss->coop_grow && chains > ss->coop_grow_mid) {
+                    keep = ss->coop_grow_mid;
+                    next_team = 32u;
+                } else if (team != 64u && ss->coop_grow && chains > ss->coop_grow) {
+                    keep = ss->coop_grow;
+                }
+                const bool grow = keep != 0u;
                 wp.parity = p;
                 hipEvent_t i0, i1;
                 HIP_TRY(hipEventCreate(&i0));
@@ -1547,7 +1561,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                     // C_ENDED); the rest go to the next launch's input as suspended queries
                     uint32_t* out = ss->ctl + PT_CTL_SET * (1u - p);
                     cp_.side_stop = out + pt::C_ENDED;
-                    cp_.side_stop_n = ss->coop_grow;   // (against the launch's own item count: before
+                    cp_.side_stop_n = keep;            // (against the launch's own item count: before
                     cp_.side_flags = PT_STOP_GROW;      //  the first count, `chains` is the slot count)
                     cp_.yield_cq = wp.cq[1u - p];
                     cp_.yield_ctr = out + pt::C_CARRY;
@@ -1586,10 +1600,10 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 const uint32_t left = ss->ctl_host[pt::C_CARRY] + ss->ctl_host[pt::C_FRESH];
                 if (left == 0u) break;
                 if (!grow) return fail(PT_E_HIP, "cooperative engine left chains behind");
-                // the last chains: whole-wave teams
+                // the last chains: bigger teams
                 chains = left;
-                team = 64u;
-                if (tune_int("roundlog", 0) >= 2) fprintf(stderr, "coop grow: %u chains to teams of 64\n", left);
+                team = next_team;
+                if (tune_int("roundlog", 0) >= 2) fprintf(stderr, "coop grow: %u chains to teams of %u\n", left, team);
             }
             break;
         }

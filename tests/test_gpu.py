@@ -375,6 +375,7 @@ TUNE_KEYS = ["wg_per_cu=2", "wg_per_cu=1", "runend=1000000", "sparse_steps=2", "
              "coop=300,coop_order=0", "coop=300,coop_order=1",
              # its last chains handed to whole-wave teams (a second launch), or never
              "coop=300,coop_grow=100", "coop=300,coop_grow=1", "coop=300,coop_grow=0",
+             "coop=300,coop_grow=50,coop_grow_mid=200", "coop=300,coop_grow=0,coop_grow_mid=200",
              # the early cooperative launch on a second stream (the heaviest chains, from the first
              # count on), beside the path rounds
              "coop=300,early=1,early_at=100000000", "coop=300,early=64,early_at=100000000,early_wg=2",
