@@ -261,3 +261,7 @@ hipError_t pt_launch_side_take(pt::WaveParams p, uint32_t k, pt::RayQ side, uint
 hipError_t pt_launch_coop(pt::WaveParams p, uint32_t grid, uint32_t team, bool big, hipStream_t s,
                           hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t pt_launch_resolve(const pt::ResolveParams& p, uint32_t n_tiles, hipStream_t s);
+// the row-major ww x wh x 3 framebuffer from packed tiles: window tile t at byte src[t] of `in`
+// (src null: t * 768, the packed buffer of a session that owns every tile)
+hipError_t pt_launch_untile(const uint8_t* in, const uint32_t* src, uint32_t tiles_x, uint32_t ww, uint32_t wh,
+                            uint8_t* fb, hipStream_t s);

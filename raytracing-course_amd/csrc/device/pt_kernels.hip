@@ -113,6 +113,22 @@ __global__ void __launch_bounds__(256) k_resolve(ResolveParams P) {
     }
 }
 
+// The framebuffer from packed 8-bit tiles (src/scene.cpp:243-251's row-major P6
+// payload): window tile t (16x16 pixels, row-major inside the tile) is read at byte
+// src[t] of `in` (null: t * 768, a one-rank session's own packed buffer), the rest
+// of the rows are the window's (ww x wh).  One workgroup per tile, a pixel per lane.
+__global__ void __launch_bounds__(256) k_untile(const uint8_t* in, const uint32_t* src, uint32_t tiles_x, uint32_t ww,
+                                                uint32_t wh, uint8_t* fb) {
+    const uint32_t t = blockIdx.x;
+    const uint32_t x = (t % tiles_x) * 16u + (threadIdx.x & 15u), y = (t / tiles_x) * 16u + (threadIdx.x >> 4);
+    if (x >= ww || y >= wh) return;
+    const uint8_t* p = in + (src ? (size_t)src[t] : (size_t)t * 768u) + 3u * threadIdx.x;
+    uint8_t* q = fb + ((size_t)y * ww + x) * 3u;
+    q[0] = p[0];
+    q[1] = p[1];
+    q[2] = p[2];
+}
+
 }  // namespace pt
 
 // ---------------------------------------------------------------- launchers
@@ -133,6 +149,12 @@ hipError_t pt_launch_trace(const pt::TraceParams& p, int variant, uint32_t lds_b
         case 2: hipLaunchKernelGGL(pt::k_trace<2>, dim3(nx), dim3(256), lds_bytes, s, p); break;
         default: hipLaunchKernelGGL(pt::k_trace<3>, dim3(nx), dim3(256), lds_bytes, s, p); break;
     }
+    return hipGetLastError();
+}
+hipError_t pt_launch_untile(const uint8_t* in, const uint32_t* src, uint32_t tiles_x, uint32_t ww, uint32_t wh,
+                            uint8_t* fb, hipStream_t s) {
+    const uint32_t n = tiles_x * ((wh + 15u) / 16u);
+    if (n) hipLaunchKernelGGL(pt::k_untile, dim3(n), dim3(256), 0, s, in, src, tiles_x, ww, wh, fb);
     return hipGetLastError();
 }
 hipError_t pt_launch_resolve(const pt::ResolveParams& p, uint32_t n_tiles, hipStream_t s) {

@@ -270,6 +270,7 @@ struct pt_session {
     pt::PixelState st{};          // per-slot records + fold records (device)
     unsigned long long* counters = nullptr;
     uint8_t* out = nullptr;
+    uint8_t* fb = nullptr;            // rank 0: the window's row-major framebuffer (device)
     float* rad = nullptr;
     unsigned long long* wg_prof = nullptr;
     // wavefront engine buffers (replay traversal)
@@ -1320,6 +1321,8 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         const size_t tables = sec((ss->gtiles.size() + ord.size()) * 4);
         const size_t a_rec = sec(2 * n * sizeof(uint4)), a_fold = sec((size_t)ss->st.depth * n * sizeof(uint4));
         const size_t a_ctr = sec(8 * PT_CTR_COPIES * PT_CTR_STRIDE), a_out = sec(3 * n);
+        // the window's framebuffer (pt_render's device-side gather; rank 0's session)
+        const size_t a_fb = o->rank == 0 ? sec(3ull * ss->tm.ww * ss->tm.wh) : 0;
         size_t a_fq[2][3] = {{0, 0, 0}, {0, 0, 0}}, a_pid = 0, a_dq[2] = {0, 0}, a_ex[2] = {0, 0}, a_hid = 0;
         size_t a_carry = 0, a_ctl = 0, a_endq = 0, a_order = 0, a_side[6] = {0, 0, 0, 0, 0, 0};
         if (ss->wave) {
@@ -1364,6 +1367,7 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         ss->st.fold = reinterpret_cast<uint4*>(A + a_fold);
         ss->counters = reinterpret_cast<unsigned long long*>(A + a_ctr);
         ss->out = A + a_out;
+        if (o->rank == 0) ss->fb = A + a_fb;
         if (ss->wave) {
             for (int q = 0; q < 2; ++q) {
                 ss->fq[q].ro = reinterpret_cast<pt::F4*>(A + a_fq[q][0]);
@@ -2109,14 +2113,26 @@ int gather_rccl(const std::vector<pt_session*>& sess, int dev0, uint32_t W, uint
         r = R.Gather(buf.send[(size_t)g], g == 0 ? buf.recv : nullptr, cap, ncclUint8, 0, c[g], sess[g]->stream);
     if (r == ncclSuccess) r = R.GroupEnd();
     if (r != ncclSuccess) return fail(PT_E_RCCL, std::string("ncclGather: ") + R.GetErrorString(r));
-    std::vector<uint8_t> host(cap * n);
+    // the framebuffer on the first device: every window tile's source in the gathered blocks
+    // (owner * cap + its rank among the owner's tiles * 768), un-tiled by one kernel, one copy out
+    const uint32_t tiles_x = (W + 15u) / 16u, n_tiles = tiles_x * ((H + 15u) / 16u);
+    std::vector<uint32_t> src(n_tiles), seen((size_t)n, 0u);
+    for (uint32_t t = 0; t < n_tiles; ++t) {
+        const uint32_t g = pt::tile_owner(t, tiles_x, (uint32_t)n);
+        src[t] = (uint32_t)(g * cap + seen[g]++ * 768u);
+    }
+    if ((uint64_t)cap * n > 0xffffffffull) return fail(PT_E_INVALID, "gather buffer beyond 4 GB");
     HIP_TRY(hipSetDevice(dev0));
-    HIP_TRY(hipMemcpyAsync(host.data(), buf.recv, cap * n, hipMemcpyDeviceToHost, sess[0]->stream));
+    uint32_t* dsrc = nullptr;
+    HIP_TRY(hipMalloc(&dsrc, std::max<size_t>(n_tiles, 1) * 4));
+    struct Free { uint32_t* p; ~Free() { (void)hipFree(p); } } free_src{dsrc};
+    HIP_TRY(hipMemcpyAsync(dsrc, src.data(), n_tiles * 4ull, hipMemcpyHostToDevice, sess[0]->stream));
+    HIP_TRY(pt_launch_untile(buf.recv, dsrc, tiles_x, W, H, sess[0]->fb, sess[0]->stream));
+    HIP_TRY(hipMemcpyAsync(rgb, sess[0]->fb, 3ull * W * H, hipMemcpyDeviceToHost, sess[0]->stream));
     for (int g = 0; g < n; ++g) {
         HIP_TRY(hipSetDevice(dev0 + g));
         HIP_TRY(hipStreamSynchronize(sess[g]->stream));
     }
-    for (int g = 0; g < n; ++g) pt_unpack_tiles(W, H, (uint32_t)g, (uint32_t)n, host.data() + cap * g, rgb);
     return PT_OK;
 }
 }  // namespace
@@ -2263,7 +2279,17 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
             if (o.gather == PT_GATHER_RCCL) return cleanup(rc);
             if (try_rccl) fprintf(stderr, "pt_render: RCCL gather unavailable (%s); gathering through the host\n",
                                   pt_last_error());
-            for (int g = 0; g < ngpu; ++g) {
+            if (ngpu == 1 && sess[0]->n_slots) {
+                // one session owns every tile: un-tiled on its device, one copy out
+                pt_session* x = sess[0];
+                const uint32_t tiles_x = (W + 15u) / 16u;
+                if (hipSetDevice(x->dev) != hipSuccess ||
+                    pt_launch_untile(x->out, nullptr, tiles_x, W, H, x->fb, x->stream) != hipSuccess ||
+                    hipMemcpyAsync(rgb, x->fb, 3ull * W * H, hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
+                    hipStreamSynchronize(x->stream) != hipSuccess)
+                    return cleanup(fail(PT_E_HIP, "framebuffer copy failed"));
+            }
+            for (int g = 0; g < ngpu && ngpu > 1; ++g) {
                 pt_session* x = sess[(size_t)g];
                 if (!x->n_slots) continue;
                 std::vector<uint8_t> packed(3ull * x->n_slots);
