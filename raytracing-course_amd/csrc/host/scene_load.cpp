@@ -19,7 +19,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "pt_scene.h"
 
@@ -28,6 +31,49 @@ namespace {
 
 inline bool is_ws(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\v' || c == '\f' || c == '\r'; }
 inline bool is_dig(char c) { return c >= '0' && c <= '9'; }
+
+// Decimal -> float for the common token (Clinger's fast path): with the decimal
+// significand w <= 2^24 and the power of ten 10^|q| <= 10^10 both exact floats, ONE
+// IEEE multiply or divide gives the correctly rounded value -- strtof's result (glibc
+// strtof rounds correctly).  Tokens outside it go to strtof.  [b, e) is a scanned
+// token: sign, digits, optional '.', digits, optional exponent, with at least one digit.
+inline bool fast_float(const char* b, const char* e, float& out) {
+    static const float p10[11] = {1e0f, 1e1f, 1e2f, 1e3f, 1e4f, 1e5f, 1e6f, 1e7f, 1e8f, 1e9f, 1e10f};
+    const char* c = b;
+    bool neg = false;
+    if (*c == '+' || *c == '-') neg = *c++ == '-';
+    uint64_t w = 0;
+    int nd = 0, q = 0;
+    for (; c < e && is_dig(*c); ++c) {
+        if (w || *c != '0') { if (++nd > 9) return false; w = w * 10u + (uint64_t)(*c - '0'); }
+    }
+    if (c < e && *c == '.') {
+        for (++c; c < e && is_dig(*c); ++c) {
+            --q;
+            if (w || *c != '0') { if (++nd > 9) return false; w = w * 10u + (uint64_t)(*c - '0'); }
+        }
+    }
+    if (c < e) {   // exponent
+        ++c;
+        bool eneg = false;
+        if (c < e && (*c == '+' || *c == '-')) eneg = *c++ == '-';
+        if (c == e) return false;   // "1e" / "1e+": strtof decides (the token then fails)
+        int x = 0;
+        for (; c < e; ++c) {
+            if (x > 1000) return false;
+            x = x * 10 + (*c - '0');
+        }
+        q += eneg ? -x : x;
+    }
+    if (w > (1u << 24)) return false;
+    float f;
+    if (w == 0) f = 0.f;
+    else if (q >= 0 && q <= 10) f = (float)w * p10[q];
+    else if (q < 0 && q >= -10) f = (float)w / p10[-q];
+    else return false;
+    out = neg ? -f : f;
+    return true;
+}
 
 // the remainder of one line, read like a std::stringstream
 struct Cursor {
@@ -64,8 +110,9 @@ struct Cursor {
             q = r;
         }
         p = q;
-        char buf[128];
         const size_t n = (size_t)(q - b);
+        if (dig && fast_float(b, q, v)) return;
+        char buf[128];
         if (n == 0 || n >= sizeof(buf)) { v = 0.f; fail = true; return; }
         memcpy(buf, b, n);
         buf[n] = '\0';
@@ -167,10 +214,42 @@ std::string load_primitive(Lines& L, HPrim& pr) {
     return std::string();
 }
 
-}  // namespace
+// a top-level command (src/sceneload.cpp:114-172) on its line's stream `ss` (for a
+// command that ended a primitive block: the stale NEW_PRIMITIVE line's stream)
+void top_level(HScene& S, Cmd cmd, const std::string& name, Cursor& ss) {
+    switch (cmd) {
+        case C_DIMENSIONS: ss.get(S.W); ss.get(S.H); break;
+        case C_BG_COLOR: ss.get3(S.bg); break;
+        case C_CAMERA_POSITION: ss.get3(S.cam_pos); break;
+        case C_CAMERA_RIGHT: ss.get3(S.cam_right); break;
+        case C_CAMERA_UP: ss.get3(S.cam_up); break;
+        case C_CAMERA_FORWARD: ss.get3(S.cam_fwd); break;
+        case C_CAMERA_FOV_X: ss.get(S.fov_x); break;
+        case C_RAY_DEPTH: ss.get(S.depth); break;
+        case C_SAMPLES: ss.get(S.samples); break;
+        default: {
+            fprintf(stderr, "unexpected command(%s)\n", name.c_str());
+            S.warnings.push_back("unexpected command(" + name + ")");
+            break;
+        }
+    }
+}
 
-// src/sceneload.cpp:112-176
-void parse_scene(const char* text, size_t len, HScene& S) {
+// One stretch of the file: its primitives, and its top-level commands with their
+// streams, in order (replayed on the scene after every stretch is parsed, since
+// a command's effect can depend on the values before it: a failed extraction keeps them)
+struct Event {
+    Cmd cmd;
+    std::string name;
+    Cursor ss;
+};
+struct Stretch {
+    std::vector<HPrim> prims;
+    std::vector<Event> events;
+};
+
+// src/sceneload.cpp:112-176 over [text, text + len)
+void parse_stretch(const char* text, size_t len, Stretch& out) {
     Lines L{text, text + len};
     const char *lb, *le;
     std::string name;
@@ -183,29 +262,69 @@ void parse_scene(const char* text, size_t len, HScene& S) {
     again:
         const Cmd cmd = command_of(name.data(), name.size());
         if (cmd == C_EMPTY) continue;
-        switch (cmd) {
-            case C_DIMENSIONS: ss.get(S.W); ss.get(S.H); break;
-            case C_BG_COLOR: ss.get3(S.bg); break;
-            case C_CAMERA_POSITION: ss.get3(S.cam_pos); break;
-            case C_CAMERA_RIGHT: ss.get3(S.cam_right); break;
-            case C_CAMERA_UP: ss.get3(S.cam_up); break;
-            case C_CAMERA_FORWARD: ss.get3(S.cam_fwd); break;
-            case C_CAMERA_FOV_X: ss.get(S.fov_x); break;
-            case C_NEW_PRIMITIVE: {
-                HPrim pr;
-                name = load_primitive(L, pr);
-                S.prims.push_back(pr);
-                if (!name.empty()) goto again;   // the stale `ss` is reused, as in the reference
-                break;
-            }
-            case C_RAY_DEPTH: ss.get(S.depth); break;
-            case C_SAMPLES: ss.get(S.samples); break;
-            default: {
-                fprintf(stderr, "unexpected command(%s)\n", name.c_str());
-                S.warnings.push_back("unexpected command(" + name + ")");
-                break;
-            }
+        if (cmd == C_NEW_PRIMITIVE) {
+            HPrim pr;
+            name = load_primitive(L, pr);
+            out.prims.push_back(pr);
+            if (!name.empty()) goto again;   // the stale `ss` is reused, as in the reference
+            continue;
         }
+        out.events.push_back(Event{cmd, name, ss});
+    }
+}
+
+// does the line at p (up to e) start with the token NEW_PRIMITIVE (stringstream >> skips
+// leading whitespace)?
+bool starts_new_primitive(const char* p, const char* e) {
+    while (p < e && *p != '\n' && is_ws(*p)) ++p;
+    static const char k[] = "NEW_PRIMITIVE";
+    const size_t n = sizeof(k) - 1;
+    return (size_t)(e - p) >= n && memcmp(p, k, n) == 0 && (p + n == e || is_ws(p[n]));
+}
+
+}  // namespace
+
+// src/sceneload.cpp:112-176.  A large file is parsed in stretches on several threads.
+// A line whose first token is NEW_PRIMITIVE always starts a new primitive after pushing
+// the one being read -- at the top level, and inside a block too (load_primitive returns
+// it, and the top level dispatches it; NEW_PRIMITIVE reads nothing from the stale
+// stream) -- so stretches that begin at such lines parse independently.  Their
+// primitives are concatenated in order, and their top-level commands replayed in order.
+void parse_scene(const char* text, size_t len, HScene& S) {
+    unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (len < (1u << 20)) T = 1;
+    std::vector<size_t> cut{0};
+    for (unsigned k = 1; k < T; ++k) {
+        size_t at = std::max(cut.back(), len * k / T);
+        // the next line start at or after `at` whose line begins a primitive
+        if (at > 0) {
+            const void* nl = memchr(text + at - 1, '\n', len - (at - 1));
+            at = nl ? (size_t)(static_cast<const char*>(nl) - text) + 1 : len;
+        }
+        while (at < len && !starts_new_primitive(text + at, text + len)) {
+            const void* nl = memchr(text + at, '\n', len - at);
+            at = nl ? (size_t)(static_cast<const char*>(nl) - text) + 1 : len;
+        }
+        if (at >= len) break;
+        if (at > cut.back()) cut.push_back(at);
+    }
+    cut.push_back(len);
+    const size_t n = cut.size() - 1;
+    std::vector<Stretch> parts(n);
+    if (n == 1) {
+        parse_stretch(text, len, parts[0]);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < n; ++i)
+            th.emplace_back([&, i] { parse_stretch(text + cut[i], cut[i + 1] - cut[i], parts[i]); });
+        for (auto& t : th) t.join();
+    }
+    size_t np = 0;
+    for (const auto& p : parts) np += p.prims.size();
+    S.prims.reserve(S.prims.size() + np);
+    for (auto& p : parts) {
+        S.prims.insert(S.prims.end(), p.prims.begin(), p.prims.end());
+        for (auto& ev : p.events) top_level(S, ev.cmd, ev.name, ev.ss);
     }
 }
 

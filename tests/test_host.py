@@ -94,6 +94,63 @@ def test_loader_quirks_match_oracle(tmp_path, name):
     assert np.array_equal(rad.view(np.uint32), orad.view(np.uint32))
 
 
+def _big_quirky_scene(n_blocks=24000, seed=3):
+    """> 1 MB of scene text (the loader parses it in stretches on several threads) with
+    the grammar's quirks spread through it: top-level commands right after a block (the
+    stale-stream re-dispatch), partial top-level lines, unknown commands, blocks without
+    a blank line between them, leading whitespace, a POSITION before the type line, and
+    numbers in every form the fast decimal path takes or leaves to strtof."""
+    rng = np.random.default_rng(seed)
+    forms = ["%.6g", "%.9g", "%.3e", "%.1f", "%.12f", "%g"]
+    L = ["DIMENSIONS 16 12", "RAY_DEPTH 3", "SAMPLES 2", "CAMERA_POSITION 0 0 6", "CAMERA_RIGHT 1 0 0",
+         "CAMERA_UP 0 1 0", "CAMERA_FORWARD 0 0 -1", "CAMERA_FOV_X 1.1", ""]
+    unknown = 0
+    for i in range(n_blocks):
+        v = rng.normal(0, 1.5, 9)
+        f = forms[i % len(forms)]
+        lead = "   " if i % 97 == 5 else ""
+        L.append(lead + "NEW_PRIMITIVE")
+        if i % 211 == 7:
+            L.append("POSITION 3 3 3")             # lost: the type line resets the primitive
+        L.append("TRIANGLE " + " ".join(f % x for x in v))
+        L.append("COLOR %s %s 1" % (f % abs(v[0] / 3), "-0" if i % 13 == 0 else "1e-3"))
+        if i % 5 == 0:
+            L.append("EMISSION 0 0 0")
+        if i % 1009 == 11:
+            L.append("BG_COLOR 0.25 0.5 0.75")     # ends the block: re-dispatched on the stale stream
+        elif i % 1013 == 17:
+            L += ["", "SAMPLES 3", "DIMENSIONS 20"]  # a partial top-level line: H keeps its value
+        elif i % 1021 == 19:
+            L += ["FOO 1 2"]                       # unknown (warning), after the block
+            unknown += 1
+        elif i % 3 == 0:
+            continue                               # no blank line before the next NEW_PRIMITIVE
+        L.append("")
+    return "\n".join(L) + "\n", unknown
+
+
+def test_parallel_parse_matches_oracle(tmp_path):
+    """The loader's multi-threaded stretch parse gives the reference parse: same header
+    values, same primitives in the same order (BVH fingerprints against the oracle's own
+    loader), the same warnings; and the same image at 2 spp."""
+    text, unknown = _big_quirky_scene()
+    assert len(text) > (1 << 20)
+    p = tmp_path / "big.txt"
+    p.write_text(text)
+    o = U.OracleScene(str(p))
+    with pt.Scene.load(str(p)) as s:
+        s.prepare()
+        inf = s.info
+        assert (inf["width"], inf["height"], inf["samples"], inf["ray_depth"]) == (o.W, o.H, o.samples, o.depth)
+        assert inf["n_prims"] == o.n_prims and inf["n_warnings"] == unknown
+        nodes, prims = s.dump_bvh()
+        onodes, oprims = o.dump_bvh()
+        assert prims == oprims and nodes == onodes
+        rad = s.selftest_render_host(0, 0, 8, 6, spp=2)
+    _, orad, _ = o.render(0, 0, 8, 6, spp=2)
+    assert np.array_equal(rad.view(np.uint32), orad.view(np.uint32))
+
+
 def test_scene_errors():
     with pytest.raises(pt.PTError) as e:
         pt.Scene.load("/nonexistent/scene.txt")
