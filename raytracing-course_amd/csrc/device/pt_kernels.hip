@@ -116,17 +116,30 @@ __global__ void __launch_bounds__(256) k_resolve(ResolveParams P) {
 // The framebuffer from packed 8-bit tiles (src/scene.cpp:243-251's row-major P6
 // payload): window tile t (16x16 pixels, row-major inside the tile) is read at byte
 // src[t] of `in` (null: t * 768, a one-rank session's own packed buffer), the rest
-// of the rows are the window's (ww x wh).  One workgroup per tile, a pixel per lane.
-__global__ void __launch_bounds__(256) k_untile(const uint8_t* in, const uint32_t* src, uint32_t tiles_x, uint32_t ww,
-                                                uint32_t wh, uint8_t* fb) {
+// of the rows are the window's (ww x wh).  `fb` may be pinned host memory: the
+// kernel then writes the image across the link itself (the copy engine's first
+// transfer costs ~8 ms on this platform, a kernel's stores ~0.2 ms for 6 MB).
+// A tile row is 48 contiguous bytes on both sides: with ww % 16 == 0 every row
+// starts 16-B aligned and goes as three 16-B stores (the right edge's partial
+// tiles and other widths go byte by byte).  One workgroup per tile.
+__global__ void __launch_bounds__(64) k_untile(const uint8_t* in, const uint32_t* src, uint32_t tiles_x, uint32_t ww,
+                                               uint32_t wh, uint8_t* fb) {
     const uint32_t t = blockIdx.x;
-    const uint32_t x = (t % tiles_x) * 16u + (threadIdx.x & 15u), y = (t / tiles_x) * 16u + (threadIdx.x >> 4);
-    if (x >= ww || y >= wh) return;
-    const uint8_t* p = in + (src ? (size_t)src[t] : (size_t)t * 768u) + 3u * threadIdx.x;
-    uint8_t* q = fb + ((size_t)y * ww + x) * 3u;
-    q[0] = p[0];
-    q[1] = p[1];
-    q[2] = p[2];
+    const uint32_t x0 = (t % tiles_x) * 16u, y0 = (t / tiles_x) * 16u;
+    const uint8_t* tile = in + (src ? (size_t)src[t] : (size_t)t * 768u);
+    const uint32_t wpx = ww - x0 < 16u ? ww - x0 : 16u;   // pixels of this tile per row
+    if ((ww & 15u) == 0u) {
+        // 16 rows x 3 chunks of 16 B (wpx = 16: ww is a multiple of the tile width)
+        const uint32_t row = threadIdx.x / 3u, ch = threadIdx.x % 3u;
+        if (threadIdx.x >= 48u || y0 + row >= wh) return;
+        const uint4 v = *reinterpret_cast<const uint4*>(tile + row * 48u + ch * 16u);
+        *reinterpret_cast<uint4*>(fb + ((size_t)(y0 + row) * ww + x0) * 3u + ch * 16u) = v;
+        return;
+    }
+    for (uint32_t i = threadIdx.x; i < 256u * 3u; i += 64u) {
+        const uint32_t px = i / 3u, row = px >> 4, col = px & 15u;
+        if (col < wpx && y0 + row < wh) fb[((size_t)(y0 + row) * ww + x0 + col) * 3u + i % 3u] = tile[i];
+    }
 }
 
 }  // namespace pt
@@ -154,7 +167,7 @@ hipError_t pt_launch_trace(const pt::TraceParams& p, int variant, uint32_t lds_b
 hipError_t pt_launch_untile(const uint8_t* in, const uint32_t* src, uint32_t tiles_x, uint32_t ww, uint32_t wh,
                             uint8_t* fb, hipStream_t s) {
     const uint32_t n = tiles_x * ((wh + 15u) / 16u);
-    if (n) hipLaunchKernelGGL(pt::k_untile, dim3(n), dim3(256), 0, s, in, src, tiles_x, ww, wh, fb);
+    if (n) hipLaunchKernelGGL(pt::k_untile, dim3(n), dim3(64), 0, s, in, src, tiles_x, ww, wh, fb);
     return hipGetLastError();
 }
 hipError_t pt_launch_resolve(const pt::ResolveParams& p, uint32_t n_tiles, hipStream_t s) {

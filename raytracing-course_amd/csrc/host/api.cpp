@@ -294,6 +294,8 @@ struct pt_session {
     uint32_t* side_ctl = nullptr;     // ... and its two round-counter sets
     hipStream_t side_stream = nullptr;
     hipEvent_t side_taken = nullptr, side_end = nullptr;   // its queue is taken / it has stopped
+    std::thread side_th;          // makes the three above (joined before their first use)
+    hipError_t side_rc = hipSuccess;
     uint32_t coop_grow = 0;       // the final launch's last chains handed to whole-wave teams (0: never)
     uint32_t coop_grow_mid = 0;   // ... and an earlier stage of teams of 32 (0: none)
     uint32_t coop_team = 8;       // lanes per chain in the cooperative engine (pure-coop rate, teams of
@@ -719,9 +721,13 @@ int device_props(int dev, DevProps* out) {
     static int count = -1;
     std::lock_guard<std::mutex> lk(mu);
     if (count < 0) {
+        const auto t0 = std::chrono::steady_clock::now();
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(PT_E_NO_GPU, "no HIP device visible");
         count = n;
+        if (getenv("PT_STATS") && atoi(getenv("PT_STATS")) >= 3)
+            fprintf(stderr, "hip runtime start (hipGetDeviceCount): %.1f ms, %d device(s)\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), n);
     }
     if (dev < 0 || dev >= count) return fail(PT_E_NO_GPU, "device index out of range");
     DevProps& p = cache[dev];
@@ -922,12 +928,21 @@ extern "C" {
 const char* pt_last_error(void) { return g_err.c_str(); }
 
 int pt_device_init(int device) {
+    // (PT_STATS=3: the phases on stderr)
+    const auto t0 = std::chrono::steady_clock::now();
+    auto ms = [&t0] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+    const bool st = getenv("PT_STATS") && atoi(getenv("PT_STATS")) >= 3;
     int rc = check_device(device);
     if (rc) return rc;
+    const double t_props = ms();
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipFree(nullptr));                // creates the device context
+    const double t_ctx = ms();
     HIP_TRY(pt_preload_kernels_base());       // loads both code objects (no launch)
+    const double t_base = ms();
     HIP_TRY(pt_preload_kernels_wave());
+    const double t_wave = ms();
+    double t_copy = 0.0, t_s1 = 0.0;
     {
         // the runtime's copy path starts on its first transfer (tens of ms): do one
         // now, and make the first session's stream (a lock per device: the CLI's
@@ -947,23 +962,30 @@ int pt_device_init(int device) {
             void* d = nullptr;
             uint32_t h = 0;
             hipStream_t s = nullptr;
-            HIP_TRY(hipMalloc(&d, 64));
-            HIP_TRY(hipMemcpy(d, &h, 4, hipMemcpyHostToDevice));
-            HIP_TRY(hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost));
-            HIP_TRY(hipFree(d));
-            HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-            {
-                std::lock_guard<std::mutex> lk2(g_spare_mu);
-                g_spare_streams[device].push_back(s);
-            }
-            // ... and its early cooperative launch's stream
-            hipStream_t side = nullptr;
-            HIP_TRY(take_stream(device, &side, true));
+            // (the stream on a second thread, beside the copy path's start)
+            hipError_t se = hipSuccess;
+            std::thread sth([&s, &se, device] {
+                se = hipSetDevice(device);
+                if (se == hipSuccess) se = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+            });
+            hipError_t ce = hipMalloc(&d, 64);
+            if (ce == hipSuccess) ce = hipMemcpy(d, &h, 4, hipMemcpyHostToDevice);
+            if (ce == hipSuccess) ce = hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost);
+            if (d) (void)hipFree(d);
+            t_copy = ms();
+            sth.join();
+            t_s1 = ms();
+            HIP_TRY(ce);
+            HIP_TRY(se);
             std::lock_guard<std::mutex> lk2(g_spare_mu);
-            g_spare_side[device].push_back(side);
+            g_spare_streams[device].push_back(s);
             w->done = true;
         }
     }
+    if (st)
+        fprintf(stderr, "pt_device_init(%d) ms: runtime+props %.1f context %.1f code_base %.1f code_wave %.1f copy %.1f "
+                "stream (beside it) +%.1f\n", device, t_props, t_ctx - t_props, t_base - t_ctx, t_wave - t_base,
+                t_copy ? t_copy - t_wave : 0.0, t_s1 ? t_s1 - t_copy : 0.0);
     return PT_OK;
 }
 int pt_abi_version(void) { return PT_ABI_VERSION; }
@@ -1343,13 +1365,17 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
             }
         }
         if (take_stream(ss->dev, &ss->stream) != hipSuccess) return cleanup(fail(PT_E_HIP, "stream creation failed"));
-        // the early launch's stream and events at set-up (a stream's creation costs ms: not in the pass)
+        // the early launch's stream and events: made on a helper thread beside the set-up and
+        // the pass's first rounds (a stream's creation costs ~10 ms: neither on the set-up's
+        // path nor in the pass), joined where the first early launch needs them
         if (ss->early_k) {
-            if (take_stream(ss->dev, &ss->side_stream, true) != hipSuccess)
-                return cleanup(fail(PT_E_HIP, "stream creation failed"));
-            if (hipEventCreateWithFlags(&ss->side_taken, hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&ss->side_end, hipEventDisableTiming) != hipSuccess)
-                return cleanup(fail(PT_E_HIP, "event creation failed"));
+            const int dev = ss->dev;
+            ss->side_th = std::thread([ss, dev] {
+                ss->side_rc = hipSetDevice(dev);
+                if (ss->side_rc == hipSuccess) ss->side_rc = take_stream(dev, &ss->side_stream, true);
+                if (ss->side_rc == hipSuccess) ss->side_rc = hipEventCreateWithFlags(&ss->side_taken, hipEventDisableTiming);
+                if (ss->side_rc == hipSuccess) ss->side_rc = hipEventCreateWithFlags(&ss->side_end, hipEventDisableTiming);
+            });
         }
         void* p = nullptr;
         if (hipMalloc(&p, at) != hipSuccess) return cleanup(fail(PT_E_OOM, "device allocation failed (session buffers)"));
@@ -1629,6 +1655,10 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             const uint32_t grid = chains < ss->lowq && ss->low_grid ? ss->low_grid : ss->path_grid;
             if (k) {
                 side = true;
+                if (ss->side_th.joinable()) {
+                    ss->side_th.join();
+                    if (ss->side_rc != hipSuccess) return fail(PT_E_HIP, "side stream creation failed");
+                }
                 if (!ss->side_stream && take_stream(ss->dev, &ss->side_stream, true) != hipSuccess)
                     return fail(PT_E_HIP, "stream creation failed");
                 wp.parity = p;
@@ -1990,6 +2020,7 @@ void* pt_session_stream(pt_session* ss) {
 
 void pt_session_free(pt_session* ss) {
     if (!ss) return;
+    if (ss->side_th.joinable()) ss->side_th.join();
     (void)hipSetDevice(ss->dev);
     // both streams drained before any buffer goes (a side launch may still run after a
     // failed pass)
@@ -2077,7 +2108,8 @@ bool same_device() { return tune_int("same_device", 0) != 0; }
 // One process driving several GPUs: the packed u8 tiles of every session are
 // gathered to the first device with one grouped ncclGather over xGMI
 // (communicator cached per device set), then un-interleaved on the host.
-int gather_rccl(const std::vector<pt_session*>& sess, int dev0, uint32_t W, uint32_t H, uint8_t* rgb) {
+int gather_rccl(const std::vector<pt_session*>& sess, int dev0, uint32_t W, uint32_t H, uint8_t* rgb,
+                uint8_t* staging) {
     std::lock_guard<std::mutex> lk(g_comm_mu);
     const int n = (int)sess.size();
     std::vector<ncclComm_t>* cp = nullptr;
@@ -2127,12 +2159,13 @@ int gather_rccl(const std::vector<pt_session*>& sess, int dev0, uint32_t W, uint
     HIP_TRY(hipMalloc(&dsrc, std::max<size_t>(n_tiles, 1) * 4));
     struct Free { uint32_t* p; ~Free() { (void)hipFree(p); } } free_src{dsrc};
     HIP_TRY(hipMemcpyAsync(dsrc, src.data(), n_tiles * 4ull, hipMemcpyHostToDevice, sess[0]->stream));
-    HIP_TRY(pt_launch_untile(buf.recv, dsrc, tiles_x, W, H, sess[0]->fb, sess[0]->stream));
-    HIP_TRY(hipMemcpyAsync(rgb, sess[0]->fb, 3ull * W * H, hipMemcpyDeviceToHost, sess[0]->stream));
+    HIP_TRY(pt_launch_untile(buf.recv, dsrc, tiles_x, W, H, staging ? staging : sess[0]->fb, sess[0]->stream));
+    if (!staging) HIP_TRY(hipMemcpyAsync(rgb, sess[0]->fb, 3ull * W * H, hipMemcpyDeviceToHost, sess[0]->stream));
     for (int g = 0; g < n; ++g) {
         HIP_TRY(hipSetDevice(dev0 + g));
         HIP_TRY(hipStreamSynchronize(sess[g]->stream));
     }
+    if (staging) memcpy(rgb, staging, 3ull * W * H);
     return PT_OK;
 }
 }  // namespace
@@ -2256,6 +2289,23 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
             terr[(size_t)g] = pt_last_error();
         }
     };
+    // a pinned staging buffer for the framebuffer's copy out (a device-to-pageable copy is
+    // staged by the runtime at a fraction of the link's rate), allocated beside the render
+    uint8_t* staging = nullptr;
+    std::thread stage_th;
+    if (rgb && W && H)
+        stage_th = std::thread([&staging, bytes = 3ull * W * H] {
+            void* p = nullptr;
+            if (hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess) staging = static_cast<uint8_t*>(p);
+        });
+    struct StageFree {
+        std::thread& th;
+        uint8_t*& p;
+        ~StageFree() {
+            if (th.joinable()) th.join();
+            if (p) (void)hipHostFree(p);
+        }
+    } stage_free{stage_th, staging};
     if (ngpu == 1) {
         work(0);
     } else {
@@ -2273,7 +2323,8 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
         // PT_GATHER_AUTO: RCCL when ngpu > 1 (host fallback with a warning);
         // PT_GATHER_RCCL: RCCL at any ngpu, an error if it fails; PT_GATHER_HOST: never RCCL
         const bool try_rccl = !same && (o.gather == PT_GATHER_RCCL || (o.gather == PT_GATHER_AUTO && ngpu > 1));
-        if (try_rccl && (rc = gather_rccl(sess, o.device, W, H, rgb)) == PT_OK) {
+        if (stage_th.joinable()) stage_th.join();
+        if (try_rccl && (rc = gather_rccl(sess, o.device, W, H, rgb, staging)) == PT_OK) {
             agg.gather_rccl = 1;
         } else {
             if (o.gather == PT_GATHER_RCCL) return cleanup(rc);
@@ -2283,11 +2334,18 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
                 // one session owns every tile: un-tiled on its device, one copy out
                 pt_session* x = sess[0];
                 const uint32_t tiles_x = (W + 15u) / 16u;
+                const double g0 = ms_since(t_gather);
+                // (into the pinned staging buffer directly: the kernel's stores cross the link)
                 if (hipSetDevice(x->dev) != hipSuccess ||
-                    pt_launch_untile(x->out, nullptr, tiles_x, W, H, x->fb, x->stream) != hipSuccess ||
-                    hipMemcpyAsync(rgb, x->fb, 3ull * W * H, hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
+                    pt_launch_untile(x->out, nullptr, tiles_x, W, H, staging ? staging : x->fb, x->stream) != hipSuccess ||
+                    (!staging && hipMemcpyAsync(rgb, x->fb, 3ull * W * H, hipMemcpyDeviceToHost, x->stream) != hipSuccess) ||
                     hipStreamSynchronize(x->stream) != hipSuccess)
                     return cleanup(fail(PT_E_HIP, "framebuffer copy failed"));
+                const double g1 = ms_since(t_gather);
+                if (staging) memcpy(rgb, staging, 3ull * W * H);
+                if (getenv("PT_STATS") && atoi(getenv("PT_STATS")) >= 3)
+                    fprintf(stderr, "gather ms: staging join %.1f untile+copy %.1f (%s) host copy %.1f\n", g0, g1 - g0,
+                            staging ? "kernel into pinned" : "copy engine", ms_since(t_gather) - g1);
             }
             for (int g = 0; g < ngpu && ngpu > 1; ++g) {
                 pt_session* x = sess[(size_t)g];
