@@ -212,6 +212,8 @@ struct SceneView {
     const F4* blob;
     uint32_t o_nodes, o_aux, o_ainfo, o_anc, o_qprim, o_prim, o_bundle;
     uint32_t aux_rshift;        // wide aux entries: leaf range packed >> aux_rshift (pt_query.h)
+    float inv_emitters;         // 1.f / (float)n_emitters (pdf_mix_e), divided once on the host: the
+                                // kernels would hoist the uniform division into a VGPR for their lifetime
 };
 
 struct Ray { f3 o, d; };
@@ -514,7 +516,7 @@ PT_HD float pdf_mix_e(const SceneView& S, const EM& em, f3 x, f3 n, f3 d) {
             const Prim E = em(k);
             ps += f2u(E.p0.w) == T_BOX ? pdf_box(E, x, d) : pdf_ellipsoid(E, x, d);
         }
-        ps *= 1.f / (float)S.n_emitters;
+        ps *= S.inv_emitters;   // = 1.f / (float)S.n_emitters (IEEE division on the host)
         sum = 0.5f * sum + 0.5f * ps;
     }
     return sum;

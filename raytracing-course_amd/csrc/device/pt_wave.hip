@@ -45,6 +45,27 @@ __device__ __forceinline__ void push_ray(const WaveParams& P, const RayQ& Q, uin
 }
 
 // src/scene.cpp:193-196: one sample's jitter draws and camera ray
+// A value the optimiser must treat as new at this point: a loop-invariant expression
+// built from it (a per-lane address) is then not hoisted into a VGPR held across the
+// whole persistent loop, where it would spill
+template <class T>
+__device__ __forceinline__ T opaque_v(T v) { asm volatile("" : "+v"(v)); return v; }
+// The launch's parameter block read where it is used: scalar loads from the kernarg
+// segment at each use (its pointer is opaque there, so nothing is hoisted), for the
+// parameters of a persistent loop's rare branches, which would otherwise hold SGPRs
+// (and spill them to VGPR lanes) for the loop's whole life.  The kernel's only
+// argument is the block, at offset 0.
+template <class K>
+__device__ __forceinline__ const K& karg() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    auto p = __builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *reinterpret_cast<const K*>(p);
+#else
+    __builtin_unreachable();   // (host pass: never called)
+#endif
+}
+// a pixel's next camera sample (src/scene.cpp:189-196): x = pix % W, y = pix / W
 __device__ __forceinline__ Ray camera_sample(const CamView& cam, Rng& R, uint32_t x, uint32_t y) {
     const float fx = (float)x + rng_uniform(R);
     const float fy = (float)y + rng_uniform(R);
@@ -101,7 +122,8 @@ __device__ __forceinline__ bool shade_item(const WaveParams& P, const EM& em, ui
         nv = 0u;
         if (done < P.target) {
             // the pixel's next sample: jitter draws + camera ray
-            ray = camera_sample(P.cam, R, pix % P.tm.W, pix / P.tm.W);
+            const WaveParams& K = karg<WaveParams>();   // (read here: see end_item)
+            ray = camera_sample(K.cam, R, pix % K.tm.W, pix / K.tm.W);
             emit = true;
         }
     }
@@ -268,7 +290,9 @@ __device__ __forceinline__ bool end_item(const WaveParams& P, uint4* H, uint32_t
     hot.nv = 0u;
     bool emit = false;
     if (hot.done < P.target) {
-        ray = camera_sample(P.cam, R, pix % P.tm.W, pix / P.tm.W);
+        // (the camera block read here, not held in SGPRs across the shade wave's loop)
+        const WaveParams& K = karg<WaveParams>();
+        ray = camera_sample(K.cam, R, pix % K.tm.W, pix / K.tm.W);
         emit = true;
     }
     hot.R = R;
@@ -377,8 +401,6 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     uint32_t bsz = n_total / n_waves;
     bsz = bsz < 1u ? 1u : (bsz > P.batch ? P.batch : bsz);   // queue indices a wave takes per atomic
     const RayQ FQ = P.fq[p];
-    const uint32_t* CQ = P.cq[p];
-    uint32_t* CQout = P.cq[1u - p];
     const uint32_t xcc = xcc_id();
     uint32_t xs = 0u;                 // XCD batch counters found empty
     uint32_t bbase = 0u, bleft = 0u;  // this wave's batch of the round's work not yet handed out
@@ -395,7 +417,10 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     Query q;
     QCounts C{0u, 0u, 0u, 0u};
     // wave-level counters (scalar registers; per-lane ones would cost VGPRs)
-    uint64_t rays = 0u, fallbacks = 0u, init_exact = 0u, planes = 0u;
+    // (the plane tests are rays x n_planes: every ray taken was plane-tested by its producer;
+    // exact-DFS hand-offs per wave and launch stay far below 2^32)
+    uint64_t rays = 0u;
+    uint32_t fallbacks = 0u, init_exact = 0u;
     QProf pf;                         // (diagnostics builds only: PT_WPROF)
     for (;;) {
         const unsigned long long idle = __ballot(!active);
@@ -417,7 +442,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
             bool over;
             if (budget == 0xffffffffu) {
                 over = false;
-            } else if (P.path_ticks) {
+            } else if (karg<WaveParams>().path_ticks) {
                 // One deadline for the whole round: the trip counts of workgroups with heavy
                 // and light chains differ, so a per-wave trip budget ends them at different
                 // times and the first ones out wait for the last (a round of a rank of 8:
@@ -425,7 +450,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 if (deadline == 0u) {
                     uint32_t d = 0u;
                     if (lane_id() == 0u) {
-                        const uint32_t want = ((uint32_t)__builtin_amdgcn_s_memrealtime() + P.path_ticks) | 1u;
+                        const uint32_t want = ((uint32_t)__builtin_amdgcn_s_memrealtime() + karg<WaveParams>().path_ticks) | 1u;
                         const uint32_t old = atomicCAS(out + C_DEADLINE, 0u, want);
                         d = old ? old : want;
                     }
@@ -438,13 +463,14 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
             if (over) {
                 // the round is over for this wave: suspend its running queries
                 if (active) {
-                    const uint32_t k = wave_append(out + C_CARRY, true);
-                    uint32_t* w = CQout + (size_t)k * P.carry_words;
+                    const WaveParams& K = karg<WaveParams>();
+                    const uint32_t k = wave_append(K.ctl + PT_CTL_SET * (1u - K.parity) + C_CARRY, true);
+                    uint32_t* w = K.cq[1u - K.parity] + (size_t)k * K.carry_words;
                     *reinterpret_cast<Query*>(w) = q;
                     uint32_t* tail = w + sizeof(Query) / 4u;
                     tail[0] = slot;
                     for (uint32_t j = 0; j < q.sp; ++j) tail[1u + j] = stk.get(j);
-                    P.st.rec[2u * slot] = lds_get(L.H, (uint32_t)q.cid);   // the chain leaves the workgroup
+                    K.st.rec[2u * slot] = lds_get(L.H, (uint32_t)q.cid);   // the chain leaves the workgroup
                 }
                 const uint32_t ns = (uint32_t)__popcll(__ballot(active));
                 if (lane_id() == 0u && ns) atomicSub(&L.resident, ns);
@@ -529,16 +555,20 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
             uint32_t cid = 0u;
             if (src == 1u) cid = lds_get(L.F, (fh + lanes_below(mjoin)) % PT_CMAX);
             if (src == 2u) cid = lds_get(L.rq_cid, gi);
-            if (src == 1u && P.pin) gi = P.pin[gi];   // (the early cooperative launch took the other items)
+            if (src == 1u) {
+                const uint32_t* pin = karg<WaveParams>().pin;
+                if (pin) gi = pin[gi];   // (the early cooperative launch took the other items)
+            }
             bool took = false;   // a fresh ray (not a resumed query) started in this lane
             if (src == 1u && gi < n_carry) {
                 // resume a suspended query: state, slot, then its aux stack into LDS
-                const uint32_t* w = CQ + (size_t)gi * P.carry_words;
+                const WaveParams& K = karg<WaveParams>();
+                const uint32_t* w = K.cq[K.parity] + (size_t)gi * K.carry_words;
                 q = *reinterpret_cast<const Query*>(w);
                 const uint32_t* tail = w + sizeof(Query) / 4u;
                 slot = tail[0];
                 for (uint32_t k = 0; k < q.sp; ++k) stk.set(k, tail[1u + k]);
-                lds_put(L.H, cid, P.st.rec[2u * slot]);   // its pixel record, for its stay here
+                lds_put(L.H, cid, K.st.rec[2u * slot]);   // its pixel record, for its stay here
                 active = true;
             } else if (src != 0u) {
                 // a fresh ray of the round, or a chain's next ray from the ray ring
@@ -569,7 +599,6 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
             if (src != 0u) q.cid = cid;
             const uint32_t ntook = (uint32_t)__popcll(__ballot(took));
             rays += ntook;
-            planes += (uint64_t)ntook * P.S.n_planes;
             init_exact += (uint32_t)__popcll(__ballot(took && q.phase == Q_EXACT));
         }
         if (__ballot(active) == 0ull) {
@@ -640,10 +669,11 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 pf.query_done();
             } else if (q.phase == Q_EXACT) {
                 // rare: the exact stack DFS after this kernel; the chain leaves the workgroup
-                const uint32_t k = atomicAdd(out + C_EXACT, 1u);
-                P.ex.ro[k] = F4{q.ray.o.x, q.ray.o.y, q.ray.o.z, u2f(slot)};
-                P.ex.rd[k] = F4{q.ray.d.x, q.ray.d.y, q.ray.d.z, u2f(k)};
-                P.st.rec[2u * slot] = lds_get(L.H, (uint32_t)q.cid);   // (k_wshade shades it from HBM)
+                const WaveParams& K = karg<WaveParams>();
+                const uint32_t k = atomicAdd(K.ctl + PT_CTL_SET * (1u - K.parity) + C_EXACT, 1u);
+                K.ex.ro[k] = F4{q.ray.o.x, q.ray.o.y, q.ray.o.z, u2f(slot)};
+                K.ex.rd[k] = F4{q.ray.d.x, q.ray.d.y, q.ray.d.z, u2f(k)};
+                K.st.rec[2u * slot] = lds_get(L.H, (uint32_t)q.cid);   // (k_wshade shades it from HBM)
                 atomicAdd(&L.leaked, 1u);   // (its table entry stays taken for the round)
                 atomicSub(&L.resident, 1u);
                 active = false;
@@ -661,7 +691,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
     wave_add_u64(ctr + 5, C.aux);
     if (lane_id() == 0u) {
         if (rays) atomicAdd(ctr + 0, (unsigned long long)rays);
-        if (planes) atomicAdd(ctr + 3, (unsigned long long)planes);
+        if (rays && P.S.n_planes) atomicAdd(ctr + 3, (unsigned long long)rays * P.S.n_planes);
         if (fallbacks) atomicAdd(ctr + 6, (unsigned long long)fallbacks);
         if (init_exact) atomicAdd(ctr + 7, (unsigned long long)init_exact);
     }
@@ -777,9 +807,10 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
         }
         // finished samples for the host's progress bar: a system-scope add per ~4 k
         prog += (uint32_t)__popcll(__ballot(sdone));
-        if (P.progress && prog >= 4096u) {
-            if (lane == 0u) __hip_atomic_fetch_add(P.progress, (unsigned long long)prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            prog = 0u;
+        if (prog >= 4096u) {
+            unsigned long long* pg = karg<WaveParams>().progress;
+            if (pg && lane == 0u) __hip_atomic_fetch_add(pg, (unsigned long long)prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (pg) prog = 0u;
         }
         const bool flush = __builtin_amdgcn_readfirstlane(lds_read(L.qw_done)) == PT_NQ;
         const unsigned long long me = __ballot(emit);
@@ -792,10 +823,11 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
         if (flush) {
             // no query wave left to take it: the next round's fresh queue (the chain leaves
             // the workgroup with its pixel record)
-            const uint32_t k = wave_append(out + C_FRESH, emit);
+            const WaveParams& K = karg<WaveParams>();
+            const uint32_t k = wave_append(K.ctl + PT_CTL_SET * (1u - K.parity) + C_FRESH, emit);
             if (emit) {
-                push_ray(P, N, k, ray, slot);
-                P.st.rec[2u * slot] = lds_get(L.H, cid);
+                push_ray(K, K.fq[1u - K.parity], k, ray, slot);
+                K.st.rec[2u * slot] = lds_get(L.H, cid);
             }
             gone += (uint32_t)__popcll(me);
         } else {
@@ -843,8 +875,13 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
     }
 }
 
+// The end-of-pass (sparse) kernel runs few chains, bound by their latency, not by
+// occupancy: it is held to 2 waves per SIMD (256 VGPRs, no spills; 2 workgroups per CU
+// run at a time, the grid's others start as those finish and find the round's work taken)
 template <bool SPARSE>
-__global__ void __launch_bounds__(PT_PATH_WG) __attribute__((amdgpu_waves_per_eu(PT_PATH_WAVES_PER_EU, PT_PATH_WAVES_PER_EU))) k_wpath(WaveParams P) {
+__global__ void __launch_bounds__(PT_PATH_WG)
+__attribute__((amdgpu_waves_per_eu(SPARSE ? 2u : PT_PATH_WAVES_PER_EU, SPARSE ? 2u : PT_PATH_WAVES_PER_EU)))
+k_wpath(WaveParams P) {
     __shared__ PathLds L;
     {
         // the first planes and emitters (the shade wave's plane tests and light sampling)
@@ -1283,7 +1320,8 @@ __device__ __forceinline__ bool coop_shade(const WaveParams& P, const QcScene& Q
         px.done += 1u;
         px.nv = 0u;
         if (px.done < P.target) {
-            ray = camera_sample(P.cam, px.R, sp.w % P.tm.W, sp.w / P.tm.W);
+            const WaveParams& K = karg<WaveParams>();   // (read here: see end_item)
+            ray = camera_sample(K.cam, px.R, sp.w % K.tm.W, sp.w / K.tm.W);
             emit = true;
         }
     }
@@ -1403,7 +1441,7 @@ k_wcoop(WaveParams P) {
                     if (tl < hot.nv && (!BIG || tl < QC_FOLD)) {
                         // the current path's vertices so far (written by the path engine; any
                         // beyond QC_FOLD stay in HBM)
-                        const uint4 f = P.st.fold[(size_t)slot * P.st.depth + tl];
+                        const uint4 f = P.st.fold[(size_t)slot * P.st.depth + opaque_v(tl)];
                         L.fold[tl] = f;
                         L.fold_sh[tl] = P.S.shade[f.x & 0x3fffffffu];
                     }

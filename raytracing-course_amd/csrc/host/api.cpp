@@ -835,6 +835,7 @@ pt::SceneView host_view(const pt_scene* s, int traversal) {
     v.emitters = s->emitters.data();
     v.n_planes = (uint32_t)s->planes.size();
     v.n_emitters = (uint32_t)s->emitters.size();
+    v.inv_emitters = s->emitters.empty() ? 0.f : 1.f / (float)s->emitters.size();
     v.bg = pt::mk3(s->hs.bg[0], s->hs.bg[1], s->hs.bg[2]);
     v.box_extent = s->box_extent;
     v.anc_info = s->anc_info.data();
@@ -1459,6 +1460,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.S.emitters = ds.emitters;
     wp.S.n_planes = (uint32_t)s->planes.size();
     wp.S.n_emitters = (uint32_t)s->emitters.size();
+    wp.S.inv_emitters = s->emitters.empty() ? 0.f : 1.f / (float)s->emitters.size();
     wp.S.bg = pt::mk3(s->hs.bg[0], s->hs.bg[1], s->hs.bg[2]);
     wp.S.box_extent = s->box_extent;
     wp.S.anc_info = ds.anc_info;
@@ -1875,6 +1877,7 @@ int pt_session_trace(pt_session* ss, uint32_t spp) {
     tp.S.emitters = ds.emitters;
     tp.S.n_planes = (uint32_t)s->planes.size();
     tp.S.n_emitters = (uint32_t)s->emitters.size();
+    tp.S.inv_emitters = s->emitters.empty() ? 0.f : 1.f / (float)s->emitters.size();
     tp.S.bg = pt::mk3(s->hs.bg[0], s->hs.bg[1], s->hs.bg[2]);
     tp.S.box_extent = s->box_extent;
     tp.S.anc_info = ds.anc_info;
