@@ -237,6 +237,8 @@ enum : uint32_t { CTR_SHORT = 11u, CTR_HANDON = 12u };
 hipError_t pt_preload_kernels_base();
 hipError_t pt_preload_kernels_wave();
 hipError_t pt_launch_init(const pt::InitParams& p, uint32_t n_tiles, hipStream_t s);
+// diagnostics (PT_TUNE prespin_us): every lane busy for `us` microseconds
+hipError_t pt_launch_spin(uint32_t us, uint32_t blocks, float* sink, hipStream_t s);
 // variant: bit 0 = filtered node tests + flat replay, bit 1 = XCD-banded tile order
 hipError_t pt_launch_trace(const pt::TraceParams& p, int variant, uint32_t lds_bytes, hipStream_t s);
 // wavefront pipeline (pt_wave.hip): start a pass (first camera ray of every

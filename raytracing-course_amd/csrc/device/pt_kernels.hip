@@ -142,6 +142,20 @@ __global__ void __launch_bounds__(64) k_untile(const uint8_t* in, const uint32_t
     }
 }
 
+// Diagnostics only (PT_TUNE prespin_us, same_device=2): FMA work on every lane for
+// `ticks` of the 100-MHz clock, from each wave's own start (the grid is resident at
+// once) -- is a GPU that idled through a session's set-up slower at its render's start?
+__global__ void __launch_bounds__(256) k_spin(uint32_t ticks, float* sink) {
+    const uint32_t t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    float a = (float)threadIdx.x;
+    for (;;) {
+#pragma unroll
+        for (int k = 0; k < 64; ++k) a = fmaf(a, 1.0001f, 0.5f);
+        if ((uint32_t)__builtin_amdgcn_s_memrealtime() - t0 >= ticks) break;
+    }
+    if (a == 12345.f) sink[threadIdx.x] = a;   // (a use of the result; never taken)
+}
+
 }  // namespace pt
 
 // ---------------------------------------------------------------- launchers
@@ -172,6 +186,10 @@ hipError_t pt_launch_untile(const uint8_t* in, const uint32_t* src, uint32_t til
 }
 hipError_t pt_launch_resolve(const pt::ResolveParams& p, uint32_t n_tiles, hipStream_t s) {
     hipLaunchKernelGGL(pt::k_resolve, dim3(n_tiles), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+hipError_t pt_launch_spin(uint32_t us, uint32_t blocks, float* sink, hipStream_t s) {
+    hipLaunchKernelGGL(pt::k_spin, dim3(blocks), dim3(256), 0, s, us * 100u, sink);
     return hipGetLastError();
 }
 }

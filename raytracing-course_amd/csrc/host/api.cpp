@@ -109,6 +109,9 @@ const Rccl& rccl() {
 //                     hardware queue), 1 the greatest priority (a queue pool of its own; default),
 //                     2 a CU-masked stream over every CU (always a queue of its own); take_stream
 //   inject_fail=G     pt_render: rank G fails after its set-up (tests of the error paths)
+//   prespin_us=N      diagnostics, same_device=2: N us of FMA work on the device before each
+//                     rank's render (outside its time)
+//   staging=0         pt_render: no pinned staging buffer for the framebuffer's copy out
 //   side_late=1       test hook: the early launch's workgroups all act as late ones (take no
 //                     chain, hand every work item on to the next round)
 //   handon=0          test hook: ... and drop those items instead (lost chains: the resolve fails)
@@ -2260,6 +2263,12 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
             turn_cv.wait(lk, [&] { return created == ngpu && turn >= g; });
             f.wait = ms_since(tw);
         }
+        if (!r && same == 2 && tune_int("prespin_us", 0) > 0) {
+            // (diagnostics: the device busy before this rank's render, outside its time)
+            if (pt_launch_spin((uint32_t)tune_int("prespin_us", 0), 2048u, nullptr, x->stream) != hipSuccess)
+                r = fail(PT_E_HIP, "spin kernel launch failed");
+            if (!r) r = pt_session_sync(x);
+        }
         const auto t_r = std::chrono::steady_clock::now();
         if (!r && g == 0 && in_pass) {
             const uint64_t total = owned_pixels(x) * S;
@@ -2296,7 +2305,7 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
     // staged by the runtime at a fraction of the link's rate), allocated beside the render
     uint8_t* staging = nullptr;
     std::thread stage_th;
-    if (rgb && W && H)
+    if (rgb && W && H && tune_int("staging", 1))
         stage_th = std::thread([&staging, bytes = 3ull * W * H] {
             void* p = nullptr;
             if (hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess) staging = static_cast<uint8_t*>(p);
