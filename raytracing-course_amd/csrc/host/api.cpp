@@ -1082,7 +1082,7 @@ int pt_scene_prepare(pt_scene* s) {
             pth::build_aux_bvh(s->nodes, reg, s->aux, s->aux_depth);
             tick("aux BVH2");
         }
-        pth::build_aux_wide(s->aux, s->dnodes, PT_AUXW, s->auxsl, s->auxsl_depth, s->auxw_stack);
+        pth::build_aux_wide(s->aux, s->dnodes, PT_AUXW, s->auxsl, s->auxsl_depth, s->auxw_stack, s->regions);
         pth::annotate_aux_ranges(s->auxsl, PT_AUXW, (uint32_t)s->dnodes.size(), s->aux_rshift);
         // Query::sp (pt_query.h) counts pending aux nodes in a 7-bit field
         if (s->auxw_stack > PT_QUERY_SP_MAX)

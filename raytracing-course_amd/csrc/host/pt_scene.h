@@ -56,8 +56,10 @@ void build_aux_stackless(const std::vector<pt::AuxNode>& pairs, const std::vecto
                          std::vector<pt::AuxSL>& out, uint32_t& max_depth);
 
 // W-ary form of the auxiliary BVH (aux_bvh.cpp)
+// (regions: as for build_aux_bvh, or empty: the collapse weighs the own boxes alone)
 void build_aux_wide(const std::vector<pt::AuxNode>& pairs, const std::vector<pt::Node>& dnodes, uint32_t W,
-                    std::vector<pt::AuxSL>& out, uint32_t& max_depth, uint32_t& max_stack);
+                    std::vector<pt::AuxSL>& out, uint32_t& max_depth, uint32_t& max_stack,
+                    const std::vector<float>& regions = {});
 
 // per-entry reference-leaf ranges of the wide aux BVH (aux_bvh.cpp)
 void annotate_aux_ranges(std::vector<pt::AuxSL>& out, uint32_t W, uint32_t n_ref_nodes, uint32_t& shift);
