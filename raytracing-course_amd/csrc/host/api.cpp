@@ -104,7 +104,7 @@ const Rccl& rccl() {
 //                     its K heaviest chains (1: what W cooperative workgroups per CU hold) in a
 //                     cooperative launch on a second stream beside it; the launch hands its chains
 //                     back when the round's path workgroups finish (default: 1; 0 = off)
-//   side_team=16      that launch's teams of 16 lanes (default 8)
+//   side_team=T       that launch's teams of T lanes: 8 (default), 16, 32 or 64
 //   side_prio=0|1|2   that launch's stream: 0 normal priority (may share a main stream's
 //                     hardware queue), 1 the greatest priority (a queue pool of its own; default),
 //                     2 a CU-masked stream over every CU (always a queue of its own); take_stream
@@ -1295,7 +1295,12 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // lanes per chain of that launch: 8 (default) or 16 (half the chains, a shorter chain cycle)
         // (a scene beyond the LDS tables has only the teams-of-8 BIG instantiation)
         const bool big = ss->depth > QC_FOLD || s->planes.size() > QC_NPL || s->emitters.size() > QC_NEM;
-        ss->side_team = tune_int("side_team", 8) == 16 && !big ? 16u : 8u;
+        {
+            const int st = tune_int("side_team", 8);
+            ss->side_team = !big && (st == 16 || st == 32 || st == 64) ? (uint32_t)st : 8u;
+            if (ss->side_team == 32u && (192u < reserve + 64u || s->max_stack > 192u)) ss->side_team = 8u;
+            if (ss->side_team == 64u && (448u < reserve + 64u || s->max_stack > 448u)) ss->side_team = 8u;
+        }
         if (ss->early_k == 1u) ss->early_k = cus * ss->early_wg * QC_WAVES * (64u / ss->side_team);   // early=1: what it holds
         if (!ss->coop_max || ss->coop_team != 8u) ss->early_k = 0;
         // a round's carry output also takes the early launch's yielded chains

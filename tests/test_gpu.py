@@ -244,6 +244,23 @@ def test_aux_stack_overflow_takes_exact_dfs(pt, name, monkeypatch):
     assert np.array_equal(rgb, img)
 
 
+def test_exact_handover_beyond_the_query_lanes(pt, monkeypatch):
+    """More hand-overs to k_wexact in one round than the path engine has query lanes
+    (PT_TUNE lstack=1 on config 2's 262,144 pixels at one sample: nearly every query
+    outgrows a one-word stack; 256 CUs x 4 workgroups x 128 query lanes = 131,072):
+    the hand-over queues hold one entry per pixel, so the image and radiance equal the
+    default stack's bit for bit (which the config-2 md5 test pins to the reference)."""
+    with pt.Scene.load(U.scene_path("c2")) as s:
+        s.prepare()
+        ref, rref, st0 = s.render(samples=1, radiance=True)
+        monkeypatch.setenv("PT_TUNE", "lstack=1,coop=0")
+        rgb, r, st = s.render(samples=1, radiance=True)
+    assert st["errors"] == 0 and st["fallbacks"] > 140000
+    assert st["rays"] == st0["rays"]
+    assert r.view(np.uint32).tolist() == rref.view(np.uint32).tolist()
+    assert np.array_equal(rgb, ref)
+
+
 def test_megakernel_engine_bit_exact(pt, monkeypatch):
     """PT_TUNE engine=mega: the megakernel (one lane per pixel, whole paths) on the
     replay traversal gives the same bytes as the path engine"""
