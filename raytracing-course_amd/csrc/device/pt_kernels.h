@@ -187,7 +187,9 @@ struct WaveParams {
                                        // this many wait (or nothing else is there to shade); 32 / 48 measured
                                        // +3.7 % / +5.6 %, 64 +6.2 % over folding in every shade batch
 #endif
-#define PT_PROBE_MIN 16u               // ... or whenever this many lanes wait for one
+#define PT_PROBE_MIN 32u               // ... or whenever this many lanes wait for one (round 5: 32 against 16,
+                                       // three interleaved repeats: rank of 1 -1.2 %, of 4 -1 %, of 8 -4 %;
+                                       // 24 / 40 / 48 / 64 between or worse)
 #ifndef PT_CMAX
 #define PT_CMAX 384u                   // (512 until round 3; the LDS pixel table took the room)
 #endif
