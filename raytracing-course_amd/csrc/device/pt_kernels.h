@@ -135,6 +135,8 @@ struct WaveParams {
     uint32_t probe_min;           // ... or whenever this many lanes wait for one
     uint32_t aux_extra;           // extra aux-node steps per trip for the lanes whose next step is one
     uint32_t batch;               // k_wpath: round-queue entries a wave takes per pull (at most)
+    uint32_t end_min;             // k_wpath: ended paths the shade wave folds in a batch of their own (1..64;
+                                  // fewer when nothing else waits: PT_END_MIN)
     // k_wcoop's intake order (null: queue order): the round's work items by the pixels'
     // remaining samples, most first (k_coop_order); `order_cur` = its 256 bucket cursors
     uint32_t* order;
@@ -186,6 +188,11 @@ struct WaveParams {
 #define PT_END_MIN 64u                 // k_wpath: the shade wave folds ended paths in batches of their own, once
                                        // this many wait (or nothing else is there to shade); 32 / 48 measured
                                        // +3.7 % / +5.6 %, 64 +6.2 % over folding in every shade batch
+#endif
+#ifndef PT_END_MIN_LOW
+#define PT_END_MIN_LOW 48u             // ... in the low-chain rounds (WaveParams::end_min; round 5, three
+                                       // interleaved repeats against 64: rank of 8 -3 %, of 4 -1 %, of 1 +-0;
+                                       // 16 / 32 no better)
 #endif
 #define PT_PROBE_MIN 32u               // ... or whenever this many lanes wait for one (round 5: 32 against 16,
                                        // three interleaved repeats: rank of 1 -1.2 %, of 4 -1 %, of 8 -4 %;

@@ -377,8 +377,10 @@ struct EmitPath {
 
 
 
+#ifndef PT_PATH_REFILL_MIN
 #define PT_PATH_REFILL_MIN 8u      // idle lanes before a query wave refills (any, once the round's work is out;
                                    // 4 / 16 measured -1 % / -1.5 % in round 3)
+#endif
 #define PT_NOWORK 0xffffffffu
 #define PT_CAPPED 0xfffffffeu
 
@@ -727,7 +729,7 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
         bool emit = false, sdone = false, have = false;
         pf.begin();
         const uint32_t pend = e_tail - e_head;
-        if (pend >= PT_END_MIN || (total == 0u && pend > 0u)) {
+        if (pend >= P.end_min || (total == 0u && pend > 0u)) {
             // a batch of ended paths: folds, sums, the next samples' camera rays
             const uint32_t n = pend < 64u ? pend : 64u;
             have = lane < n;

@@ -86,10 +86,10 @@ const Rccl& rccl() {
 //                     per chain) to the end of the pass (0: never)
 //   round_batch=N     path rounds launched per chain count while the chains are far above
 //                     the hand-over (default 1)
-//   probe_every=N, probe_min=N, aux_extra=N
+//   probe_every=N, probe_min=N, aux_extra=N, end_min=N
 //                     path engine step mix: candidate probes every N-th trip or with N lanes
 //                     waiting, extra aux-node steps per trip (defaults 3, 16, 1)
-//   lowq=N, lowq_probe_every=N, lowq_probe_min=N, lowq_aux_extra=N
+//   lowq=N, lowq_probe_every=N, lowq_probe_min=N, lowq_aux_extra=N, lowq_end_min=N
 //                     the step mix of rounds that start with fewer than N chains (default
 //                     768 per CU; the mix of the other rounds)
 //   lowq_wg=N         ... and their path workgroups per CU (PT_CMAX chains each; default 2)
@@ -281,9 +281,10 @@ struct pt_session {
     uint32_t path_grid = 0, path_budget = 1024, path_ticks = 0, low_ticks = 0, path_runend = 0, path_sparse = 0, sparse_steps = 8;
     uint32_t coop_max = 0, coop_grid = 0, coop_reserve = 0;   // cooperative engine (k_wcoop) at the end of a pass
     uint32_t round_batch = 1;     // rounds launched per count while the chains are far above the hand-over
-    // k_wpath's per-trip step mix: {probe_every, probe_min, aux_extra}, and the one of
+    // k_wpath's per-trip step mix: {probe_every, probe_min, aux_extra, end_min}, and the one of
     // rounds that start with fewer than lowq chains (latency-bound: few chains per lane)
-    uint32_t mix[3] = {PT_PROBE_EVERY, PT_PROBE_MIN, PT_AUX2}, mix_low[3] = {PT_PROBE_EVERY, PT_PROBE_MIN, PT_AUX2};
+    uint32_t mix[4] = {PT_PROBE_EVERY, PT_PROBE_MIN, PT_AUX2, PT_END_MIN},
+             mix_low[4] = {PT_PROBE_EVERY, PT_PROBE_MIN, PT_AUX2, PT_END_MIN_LOW};
     uint32_t lowq = 0;
     uint32_t low_grid = 0;        // path workgroups of those rounds
     bool coop_order = true;       // the cooperative engine takes the pixels furthest from the target first
@@ -1306,12 +1307,16 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // a round's carry output also takes the early launch's yielded chains
         ss->carry_cap = (uint32_t)std::min<uint64_t>(n, (uint64_t)ss->lane_cap + ss->early_k);
         {
-            static const char* keys[3] = {"probe_every", "probe_min", "aux_extra"};
-            static const char* lkeys[3] = {"lowq_probe_every", "lowq_probe_min", "lowq_aux_extra"};
-            for (int i = 0; i < 3; ++i) {
-                ss->mix[i] = (uint32_t)std::max(i == 0 ? 1 : 0, tune_int(keys[i], (int)ss->mix[i]));
-                ss->mix_low[i] = (uint32_t)std::max(i == 0 ? 1 : 0, tune_int(lkeys[i], (int)ss->mix[i]));
+            static const char* keys[4] = {"probe_every", "probe_min", "aux_extra", "end_min"};
+            static const char* lkeys[4] = {"lowq_probe_every", "lowq_probe_min", "lowq_aux_extra", "lowq_end_min"};
+            for (int i = 0; i < 4; ++i) {
+                const int lo = i == 0 || i == 3 ? 1 : 0;
+                ss->mix[i] = (uint32_t)std::max(lo, tune_int(keys[i], (int)ss->mix[i]));
+                // (the low rounds' end_min has a default of its own; the others follow the full rounds')
+                ss->mix_low[i] = (uint32_t)std::max(lo, tune_int(lkeys[i], (int)(i == 3 ? ss->mix_low[i] : ss->mix[i])));
             }
+            ss->mix[3] = std::min<uint32_t>(ss->mix[3], 64u);
+            ss->mix_low[3] = std::min<uint32_t>(ss->mix_low[3], 64u);
             // Rounds that start with fewer than 768 chains per CU run on 2 path workgroups
             // per CU (PT_CMAX chains each) instead of 4: with that few chains the rounds are
             // bound by each chain's latency, and a query trip's instruction stream shares its
@@ -1520,6 +1525,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     // rounds): a workgroup fills closer to its chain cap in finer pulls; rank-of-1 / 2 / 4 / 8,
     // two calls: +0.5 / +0.5 / +3.5 / +3 % (8 and 16 the same at ranks of 1-4; profiles/r03_lowq)
     wp.batch = (uint32_t)std::min(64, std::max(1, tune_int("batch", 32)));
+    wp.end_min = ss->mix[3];
     wp.lstack = std::min<uint32_t>(PT_LSTACK, (uint32_t)std::max(1, tune_int("lstack", (int)PT_LSTACK)));
     if (ss->on_progress && !ss->prog_host) {
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ss->prog_host), 8, hipHostMallocMapped | hipHostMallocCoherent));
@@ -1748,6 +1754,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 wp.probe_every = m[0];
                 wp.probe_min = m[1];
                 wp.aux_extra = m[2];
+                wp.end_min = m[3];
                 if (low && ss->low_grid) {
                     grid = ss->low_grid;
                     if (!tune_has("cap")) wp.path_cap = PT_CMAX;   // (an explicit cap=N stays)
