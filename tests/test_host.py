@@ -276,6 +276,30 @@ def test_query_log_on_host(tmp_path, monkeypatch):
     assert q[:, 0].sum() > 0
 
 
+def test_aux_tree_quality_on_standin(tmp_path, monkeypatch):
+    """The wide aux tree's quality, the wavefront query's dominant cost: aux-node visits per
+    query of the host build of the query (the code the GPU runs) on six 32x32 windows of
+    the config-3 stand-in at 1 spp (tools/aux_quality.py's measure).  4.24 per query when
+    this test was written, with the region-weighted collapse of aux_bvh.cpp (which took
+    tools/aux_quality.py's default sample from 4.754 to 4.710); a builder change that costs
+    more than 3 % fails here, on the CPU."""
+    log = tmp_path / "q.bin"
+    monkeypatch.setenv("PT_TUNE", "qstats=%s" % log)
+    rows = []
+    with pt.Scene.load(U.scene_path("c3")) as s:
+        s.prepare()
+        W, H = s.info["width"], s.info["height"]
+        for j in range(2):
+            for i in range(3):
+                x0, y0 = (W - 32) * i // 2, (H - 32) * j
+                got = s.selftest_render_host(x0, y0, 32, 32, spp=1, traversal=0)
+                assert np.isfinite(got).all()
+                rows.append(np.fromfile(log, dtype=np.uint32).reshape(-1, 4))
+    q = np.concatenate(rows)
+    assert len(q) > 20000 and int((q[:, 2] >> 31).sum()) == 0
+    assert q[:, 0].mean() <= 4.24 * 1.03
+
+
 def _gamma_table():
     with pt.Scene.load(U.scene_path("practice5_1.txt")) as s:
         s.prepare()
