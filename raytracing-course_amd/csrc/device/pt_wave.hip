@@ -44,7 +44,6 @@ __device__ __forceinline__ void push_ray(const WaveParams& P, const RayQ& Q, uin
     Q.ri[qi] = q_prep(P.S, ray);
 }
 
-// src/scene.cpp:193-196: one sample's jitter draws and camera ray
 // A value the optimiser must treat as new at this point: a loop-invariant expression
 // built from it (a per-lane address) is then not hoisted into a VGPR held across the
 // whole persistent loop, where it would spill
@@ -53,8 +52,8 @@ __device__ __forceinline__ T opaque_v(T v) { asm volatile("" : "+v"(v)); return 
 // The launch's parameter block read where it is used: scalar loads from the kernarg
 // segment at each use (its pointer is opaque there, so nothing is hoisted), for the
 // parameters of a persistent loop's rare branches, which would otherwise hold SGPRs
-// (and spill them to VGPR lanes) for the loop's whole life.  The kernel's only
-// argument is the block, at offset 0.
+// (and spill them to VGPR lanes) for the loop's whole life.  Its callers' kernels
+// (k_wpath, k_wshade, k_wcoop) take the block as their only argument, at offset 0.
 template <class K>
 __device__ __forceinline__ const K& karg() {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -65,7 +64,8 @@ __device__ __forceinline__ const K& karg() {
     __builtin_unreachable();   // (host pass: never called)
 #endif
 }
-// a pixel's next camera sample (src/scene.cpp:189-196): x = pix % W, y = pix / W
+// a pixel's next camera sample, its jitter draws and camera ray (src/scene.cpp:189-196):
+// x = pix % W, y = pix / W
 __device__ __forceinline__ Ray camera_sample(const CamView& cam, Rng& R, uint32_t x, uint32_t y) {
     const float fx = (float)x + rng_uniform(R);
     const float fy = (float)y + rng_uniform(R);
