@@ -165,6 +165,9 @@ struct WaveParams {
 #define PT_SIDE_NO_HANDON 2u
 // the final launch's stop: side_stop (its C_ENDED) against n_total - side_stop_n
 #define PT_STOP_GROW 4u
+// ... test hook (PT_TUNE grow_late): that launch's odd workgroups behave as late ones
+// (stop at once and hand their untaken items on, through the intake order)
+#define PT_GROW_LATE 8u
 #define PT_ORDER_BUCKETS 256u
 
 // path engine geometry: PT_NQ query waves + 1 shade wave per workgroup; at most

@@ -1394,7 +1394,7 @@ k_wcoop(WaveParams P) {
             uint32_t fin = 0u;
             if (lane == 0u) fin = __hip_atomic_load(P.side_stop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
             fin = __builtin_amdgcn_readfirstlane(fin);
-            if (fin >= stop_n || (P.side_flags & PT_SIDE_LATE)) {
+            if (fin >= stop_n || (P.side_flags & PT_SIDE_LATE) || ((P.side_flags & PT_GROW_LATE) && (blockIdx.x & 1u))) {
                 stopped = true;
                 break;
             }
@@ -1554,9 +1554,12 @@ k_wcoop(WaveParams P) {
         // they are, their pixels' records untouched in HBM (a fresh ray is counted
         // here, as the intake would have)
         for (;;) {
-            const uint32_t gi = wave_append(out + C_HEADS, true);
+            uint32_t gi = wave_append(out + C_HEADS, true);
             const bool on = gi < n_total;
             if (__ballot(on) == 0ull) break;
+            // (through the intake order, as the teams take them: the final launch's grow stop
+            // runs with one, and a workgroup that starts late finds items no team took)
+            if (on && P.order) gi = P.order[gi];
             Ray r;
             float rp = PT_INF;
             int rid = -1;

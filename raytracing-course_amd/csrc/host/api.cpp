@@ -112,9 +112,13 @@ const Rccl& rccl() {
 //   prespin_us=N      diagnostics, same_device=2: N us of FMA work on the device before each
 //                     rank's render (outside its time)
 //   staging=0         pt_render: no pinned staging buffer for the framebuffer's copy out
+//   shortlog=1        diagnostics: on a lost-chain error, the short pixels' sample counts on stderr
+//   dupcheck=1        diagnostics: after every round, a slot that appears twice in the next round's work
 //   side_late=1       test hook: the early launch's workgroups all act as late ones (take no
 //                     chain, hand every work item on to the next round)
 //   handon=0          test hook: ... and drop those items instead (lost chains: the resolve fails)
+//   grow_late=1       test hook: the final launch's grow stop (coop_grow) with its odd workgroups
+//                     acting as late ones (they hand their untaken items on through the intake order)
 //   cap=N            chains a workgroup may hold
 //   batch=N           round-queue entries a query wave takes per pull (1..64, default 32)
 //   lstack=N          aux stack words a path-engine query may use (default and maximum PT_LSTACK;
@@ -1608,7 +1612,8 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                     uint32_t* out = ss->ctl + PT_CTL_SET * (1u - p);
                     cp_.side_stop = out + pt::C_ENDED;
                     cp_.side_stop_n = keep;            // (against the launch's own item count: before
-                    cp_.side_flags = PT_STOP_GROW;      //  the first count, `chains` is the slot count)
+                    cp_.side_flags = PT_STOP_GROW |     //  the first count, `chains` is the slot count)
+                                     (tune_int("grow_late", 0) ? PT_GROW_LATE : 0u);
                     cp_.yield_cq = wp.cq[1u - p];
                     cp_.yield_ctr = out + pt::C_CARRY;
                 }
@@ -1828,6 +1833,25 @@ int trace_wave(pt_session* ss, uint32_t spp) {
             fprintf(stderr, "\n");
             ss->roundlog_t = wall_ms();
         }
+        if (tune_int("dupcheck", 0)) {
+            // diagnostics: every slot at most once in the next round's work (fresh rays + carry)
+            const uint32_t nf = ss->ctl_host[pt::C_FRESH], nc = ss->ctl_host[pt::C_CARRY];
+            std::vector<pt::F4> ro(nf);
+            std::vector<uint32_t> cw((size_t)nc * ss->carry_words);
+            if (nf) HIP_TRY(hipMemcpy(ro.data(), wp.fq[p].ro, nf * sizeof(pt::F4), hipMemcpyDeviceToHost));
+            if (nc) HIP_TRY(hipMemcpy(cw.data(), wp.cq[p], cw.size() * 4, hipMemcpyDeviceToHost));
+            std::vector<uint8_t> seen(ss->n_slots, 0);
+            uint32_t dup = 0, bad = 0;
+            auto see = [&](uint32_t slot) {
+                if (slot >= ss->n_slots) { ++bad; return; }
+                if (seen[slot]++) ++dup;
+            };
+            for (uint32_t i = 0; i < nf; ++i) see(pt::f2u(ro[i].w));
+            for (uint32_t i = 0; i < nc; ++i) see(cw[(size_t)i * ss->carry_words + sizeof(pt::Query) / 4]);
+            if (dup || bad)
+                fprintf(stderr, "dupcheck: round %u (%s%s) fresh %u carry %u: %u duplicate slot(s), %u out of range\n",
+                        ss->rounds, chains < ss->lowq ? "low" : "full", side ? "+side" : "", nf, nc, dup, bad);
+        }
         if (ss->ctl_host[pt::C_FRESH] == 0u && ss->ctl_host[pt::C_CARRY] == 0u) break;
         if (guard > 100000u) return fail(PT_E_HIP, "wavefront rounds did not drain");
         chains = ss->ctl_host[pt::C_FRESH] + ss->ctl_host[pt::C_CARRY];
@@ -1967,6 +1991,22 @@ int pt_session_resolve(pt_session* ss, uint8_t* dev_out, float* dev_radiance) {
     if (c[pt::CTR_SHORT] != ss->short_seen) {
         const unsigned long long k = c[pt::CTR_SHORT] - ss->short_seen;
         ss->short_seen = c[pt::CTR_SHORT];
+        if (tune_int("shortlog", 0)) {
+            // diagnostics: how far the short pixels are from the target, and where they are
+            std::vector<uint4> rec(2ull * ss->n_slots);
+            if (hipMemcpy(rec.data(), ss->st.rec, rec.size() * sizeof(uint4), hipMemcpyDeviceToHost) == hipSuccess) {
+                std::map<int, uint32_t> hist;
+                uint32_t shown = 0;
+                for (uint32_t i = 0; i < ss->n_slots; ++i) {
+                    const uint32_t done = rec[2 * i].w, nv = rec[2 * i].z >> 8;
+                    if (done == rp.samples || rec[2 * i + 1].w == 0xFFFFFFFFu) continue;
+                    hist[(int)done - (int)rp.samples]++;
+                    if (shown++ < 8)
+                        fprintf(stderr, "short: slot %u pixel %u done %u nv %u\n", i, rec[2 * i + 1].w, done, nv);
+                }
+                for (auto& h : hist) fprintf(stderr, "short: done - samples = %d: %u pixels\n", h.first, h.second);
+            }
+        }
         return fail(PT_E_HIP, std::to_string(k) + " pixel(s) did not take exactly " + std::to_string(rp.samples) +
                                   " samples (a chain was lost)");
     }

@@ -442,6 +442,24 @@ def test_side_launch_hand_on_runs_and_is_counted(pt, name, monkeypatch):
     assert np.array_equal(rgb, img)
 
 
+@pytest.mark.parametrize("name", ["dragon_64x64x16", "c2_win_240_200_24x24"])
+def test_final_launch_hand_on_follows_the_intake_order(pt, name, monkeypatch):
+    """The pass's final cooperative launch takes its work items through the intake order
+    (coop_order) and, with a grow stop (coop_grow), hands the ones no team took on to the
+    next launch.  A workgroup that starts late (a device shared with other sessions) finds
+    such items; they must be handed on through the same order, or one item runs twice and
+    another never (pixels +1 / -1 samples).  PT_TUNE grow_late=1 makes the odd workgroups
+    late ones."""
+    monkeypatch.setenv("PT_TUNE", "coop=100000000,coop_order=1,coop_grow=1,grow_late=1")
+    m, img, rad = U.golden_image(name)
+    with pt.Scene.load(U.golden_scene_path(name)) as s:
+        win = tuple(m["window"]) if m["window"] else None
+        rgb, r, st = s.render(radiance=True, window=win)
+    assert st["handed_on"] > 0 and st["short_pixels"] == 0 and st["errors"] == 0
+    assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
+    assert np.array_equal(rgb, img)
+
+
 def test_lost_chains_fail_the_resolve(pt, monkeypatch):
     """A chain the engines lose leaves its pixel short of the pass target.  The resolve
     counts the owned pixels whose sample count differs from the samples traced and fails

@@ -33,7 +33,12 @@ def main():
         for r in range(a.repeat):
             for t in a.tunes:
                 os.environ["PT_TUNE"] = t
-                rgb, _, st = s.render(ngpu=a.ngpu)
+                try:
+                    rgb, _, st = s.render(ngpu=a.ngpu)
+                except pt.PTError as e:   # (e.g. the resolve's lost-chain error)
+                    bad += 1
+                    print(json.dumps({"repeat": r, "tune": t, "ok": False, "error": str(e)}), flush=True)
+                    continue
                 ppm = b"P6\n%d %d\n255\n" % (w, h) + rgb.tobytes()
                 ok = U.md5(ppm) == full["md5"] and st["rays"] == full["rays"] and st["errors"] == 0
                 bad += 0 if ok else 1
