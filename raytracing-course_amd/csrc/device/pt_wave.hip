@@ -1368,7 +1368,10 @@ k_wcoop(WaveParams P) {
     uint32_t prog = 0u;   // finished samples not yet reported (wave-uniform)
     // the stop count: side_stop_n finished path workgroups, or (the final launch's hand-over
     // to whole-wave teams) all but side_stop_n of this launch's work items ended
-    const uint32_t stop_n = !(P.side_flags & PT_STOP_GROW) ? P.side_stop_n
+    // (the late-workgroup test hooks: a stop count of 0, so the loop holds no flag test)
+    const bool late = (P.side_flags & PT_SIDE_LATE) || ((P.side_flags & PT_GROW_LATE) && (blockIdx.x & 1u));
+    const uint32_t stop_n = late ? 0u
+                            : !(P.side_flags & PT_STOP_GROW) ? P.side_stop_n
                             : n_total > P.side_stop_n ? n_total - P.side_stop_n : 0xffffffffu;
 #ifdef PT_CPROF
     // expansion, candidates, decisions, shading, next ray, chain cycles, chains, wave lifetime
@@ -1394,7 +1397,7 @@ k_wcoop(WaveParams P) {
             uint32_t fin = 0u;
             if (lane == 0u) fin = __hip_atomic_load(P.side_stop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
             fin = __builtin_amdgcn_readfirstlane(fin);
-            if (fin >= stop_n || (P.side_flags & PT_SIDE_LATE) || ((P.side_flags & PT_GROW_LATE) && (blockIdx.x & 1u))) {
+            if (fin >= stop_n) {
                 stopped = true;
                 break;
             }
@@ -1559,7 +1562,8 @@ k_wcoop(WaveParams P) {
             if (__ballot(on) == 0ull) break;
             // (through the intake order, as the teams take them: the final launch's grow stop
             // runs with one, and a workgroup that starts late finds items no team took)
-            if (on && P.order) gi = P.order[gi];
+            const uint32_t* order = karg<WaveParams>().order;
+            if (on && order) gi = order[gi];
             Ray r;
             float rp = PT_INF;
             int rid = -1;
