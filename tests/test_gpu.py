@@ -356,6 +356,22 @@ def test_render_ngpu_sessions_on_one_device(pt, cfg, ngpu, mode, monkeypatch):
     assert st["rays"] == full["rays"] and st["errors"] == 0 and st["gather_rccl"] == 0
 
 
+def test_render_ngpu_concurrent_sessions_repeated(pt, monkeypatch):
+    """Four sessions rendering config 2 at once on device 0 (same_device=1), ten times:
+    their workgroups start late and interleave differently on each render, which is how
+    the final launch's hand-on bug showed (2 failed renders in 40 before its fix;
+    DESIGN §5).  Every render must give the reference's bytes and ray count."""
+    monkeypatch.setenv("PT_TUNE", "same_device=1")
+    full = M["full"]["c2"]
+    with pt.Scene.load(U.scene_path("c2")) as s:
+        w, h = s.info["width"], s.info["height"]
+        for _ in range(10):
+            rgb, _, st = s.render(ngpu=4)
+            ppm = b"P6\n%d %d\n255\n" % (w, h) + rgb.tobytes()
+            assert U.md5(ppm) == full["md5"]
+            assert st["rays"] == full["rays"] and st["errors"] == 0 and st["short_pixels"] == 0
+
+
 @pytest.mark.parametrize("mode", ["1", "2"])
 def test_cli_ngpu_sessions_on_one_device(pt, tmp_path, mode):
     """The CLI with PT_NGPU=4 (4 sessions on device 0, PT_TUNE same_device=1 or 2): the
