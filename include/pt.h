@@ -25,14 +25,16 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 5   /* 2: pt_render_opts.gather; 3: pt_stats per-engine (coop_*) fields;
+#define PT_ABI_VERSION 6   /* 2: pt_render_opts.gather; 3: pt_stats per-engine (coop_*) fields;
                               4: pt_gather_init, and the session tile deal changed from tile
                               t -> rank t % world to tile (tx, ty) -> rank (tx + ty) % world
                               (local tiles still in ascending tile order): a driver that
                               un-interleaves packed tiles itself must use pt_unpack_tiles
                               (or ptrace.rank_tiles), not its own formula;
                               5: pt_stats.short_pixels / handed_on, and pt_session_resolve fails
-                              when an owned pixel's sample count differs from the samples traced */
+                              when an owned pixel's sample count differs from the samples traced;
+                              6: pt_stats.gather_allocs (the RCCL gather keeps its buffers per
+                              communicator), pt_session_reset */
 
 enum {
     PT_OK = 0,
@@ -153,6 +155,9 @@ typedef struct pt_stats {
        cooperative launch's late workgroups handed on to the next round untaken */
     uint64_t short_pixels;
     uint64_t handed_on;
+    /* ABI 6: device allocations pt_render's RCCL gather made (its send / receive buffers are
+       kept per communicator: 0 on every render after the first of a device set and size) */
+    uint64_t gather_allocs;
 } pt_stats;
 
 /* Scene::Render minus the stream write: renders W*H*3 u8 (row-major, top row
@@ -196,6 +201,11 @@ int pt_session_trace(pt_session* ss, uint32_t spp);
  * dev_radiance (optional, device) receives 256*3 f32 per tile. */
 int pt_session_resolve(pt_session* ss, uint8_t* dev_out, float* dev_radiance);
 int pt_session_sync(pt_session* ss);
+/* restart every owned pixel at sample 0 (its stream re-seeded, its sum zeroed), the
+ * session's buffers and counters kept: the next trace(S) renders exactly what a new
+ * session would -- Scene::Render's job again without the set-up (bench.py repeats the
+ * metric's 256-spp frame this way).  Runs any trace() not yet run first. */
+int pt_session_reset(pt_session* ss);
 /* copy the internal packed buffer to host memory (after resolve+sync) */
 int pt_session_read_packed(pt_session* ss, uint8_t* host_out, size_t bytes);
 /* scatter packed tiles of `rank` (world ranks) into a width*height*3 image

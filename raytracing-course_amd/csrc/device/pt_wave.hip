@@ -1006,7 +1006,9 @@ __device__ __forceinline__ bool qc_prim_hit(const SceneView& S, uint32_t i, cons
 // k_wcoop's work counters: per wave in LDS, one LDS add per wave and counting site (a
 // lane-private counter costs a VGPR for the kernel's life; the engine sits at the
 // 3-waves-per-SIMD limit)
-enum : uint32_t { LC_RAYS = 0u, LC_NODES, LC_PTESTS, LC_PLANES, LC_AUX, LC_FALLB, LC_HANDED, LC_N = 8u };
+// (no plane-test counter: every counted ray tests every plane, so the plane tests are the
+// rays x n_planes, formed in 64 bits at the end -- a 32-bit LDS count of them could wrap)
+enum : uint32_t { LC_RAYS = 0u, LC_NODES, LC_PTESTS, LC_SPARE, LC_AUX, LC_FALLB, LC_HANDED, LC_N = 8u };
 __device__ __forceinline__ void lc_add(uint32_t* lc, uint32_t k, bool c, uint32_t w = 1u) {
     const unsigned long long m = __ballot(c);
     if (m && lane_id() == (uint32_t)__ffsll((long long)m) - 1u) atomicAdd(lc + k, (uint32_t)__popcll(m) * w);
@@ -1434,7 +1436,6 @@ k_wcoop(WaveParams P) {
                         pid = FQ.pid[fi];
                         pre = FQ.ri[fi];
                         lc_add(lc, LC_RAYS, tl == 0u);
-                        lc_add(lc, LC_PLANES, tl == 0u, P.S.n_planes);
                     }
                     // the pixel's state for the chain's life: RNG / vertices / samples and the
                     // sum in the first lane's registers, the current path's fold records in LDS
@@ -1479,7 +1480,6 @@ k_wcoop(WaveParams P) {
         }
         prog += (uint32_t)__popcll(__ballot(sdone));
         lc_add(lc, LC_RAYS, emit);
-        lc_add(lc, LC_PLANES, emit, P.S.n_planes);
         emit = __shfl(emit ? 1 : 0, (int)tbase, 64) != 0;
         QC_TICK(3);
         {
@@ -1533,7 +1533,9 @@ k_wcoop(WaveParams P) {
         // not counted again: its ray was counted when first taken), its pixel state and the
         // current path's fold records to HBM (the path engine continues the path from there)
         const uint32_t k = wave_append(P.yield_ctr, have && tl == 0u);
-        if (have && tl == 0u) {
+        // (k < carry_cap always: the host sizes the stops to the carry queue; a yield past it
+        // would be a lost chain, which the resolve reports, never a write past the queue)
+        if (have && tl == 0u && k < P.carry_cap) {
             Query q;
             q_init_pre(ray, Pt, pid, pre, q);
             uint32_t* w = P.yield_cq + (size_t)k * P.carry_words;
@@ -1586,10 +1588,9 @@ k_wcoop(WaveParams P) {
                 rpre = FQ.ri[fi];
             }
             lc_add(lc, LC_RAYS, on && gi >= n_carry);
-            lc_add(lc, LC_PLANES, on && gi >= n_carry, P.S.n_planes);
             lc_add(lc, LC_HANDED, on);
             const uint32_t k2 = wave_append(P.yield_ctr, on);
-            if (on) {
+            if (on && k2 < P.carry_cap) {
                 Query q;
                 q_init_pre(r, rp, rid, rpre, q);
                 uint32_t* w = P.yield_cq + (size_t)k2 * P.carry_words;
@@ -1609,6 +1610,7 @@ k_wcoop(WaveParams P) {
         const uint32_t to[LC_N] = {0u, 1u, 2u, 3u, 5u, 6u, CTR_HANDON, 0u};
         for (uint32_t k = 0; k < LC_HANDED + 1u; ++k)
             if (v[k]) atomicAdd(ctr + to[k], (unsigned long long)v[k]);
+        if (v[LC_RAYS] && P.S.n_planes) atomicAdd(ctr + 3, (unsigned long long)v[LC_RAYS] * P.S.n_planes);
         if (v[LC_RAYS]) atomicAdd(ctr + 8, (unsigned long long)v[LC_RAYS]);
         if (v[LC_NODES]) atomicAdd(ctr + 9, (unsigned long long)v[LC_NODES]);
         if (v[LC_PTESTS]) atomicAdd(ctr + 10, (unsigned long long)v[LC_PTESTS]);

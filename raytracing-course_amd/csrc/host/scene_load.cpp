@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -314,9 +315,17 @@ void parse_scene(const char* text, size_t len, HScene& S) {
     if (n == 1) {
         parse_stretch(text, len, parts[0]);
     } else {
+        // (a stretch whose thread cannot be started is parsed here, after the others start)
         std::vector<std::thread> th;
-        for (size_t i = 0; i < n; ++i)
-            th.emplace_back([&, i] { parse_stretch(text + cut[i], cut[i + 1] - cut[i], parts[i]); });
+        std::vector<size_t> here;
+        for (size_t i = 0; i < n; ++i) {
+            try {
+                th.emplace_back([&, i] { parse_stretch(text + cut[i], cut[i + 1] - cut[i], parts[i]); });
+            } catch (const std::system_error&) {
+                here.push_back(i);
+            }
+        }
+        for (size_t i : here) parse_stretch(text + cut[i], cut[i + 1] - cut[i], parts[i]);
         for (auto& t : th) t.join();
     }
     size_t np = 0;

@@ -26,7 +26,7 @@ TRAVERSAL_REPLAY = 0
 TRAVERSAL_EXACT = 1
 TRAVERSAL_REPLAY_DIV = 2
 GATHER_AUTO, GATHER_RCCL, GATHER_HOST = 0, 1, 2
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # One HIP runtime per process: PyTorch bundles its own libamdhip64 (soname
 # libamdhip64.so.7, but its users link the unversioned name), so loading
@@ -67,7 +67,7 @@ class Stats(C.Structure):
                 ("rounds", C.c_uint64), ("gather_rccl", C.c_uint64),
                 ("coop_rays", C.c_uint64), ("coop_node_visits", C.c_uint64), ("coop_prim_tests", C.c_uint64),
                 ("coop_aux_visits", C.c_uint64), ("coop_ms", C.c_double), ("coop_launches", C.c_uint64),
-                ("short_pixels", C.c_uint64), ("handed_on", C.c_uint64)]
+                ("short_pixels", C.c_uint64), ("handed_on", C.c_uint64), ("gather_allocs", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -97,6 +97,7 @@ _sig = {
     "pt_session_trace": (C.c_int, [_P, C.c_uint32]),
     "pt_session_resolve": (C.c_int, [_P, _P, _P]),
     "pt_session_sync": (C.c_int, [_P]),
+    "pt_session_reset": (C.c_int, [_P]),
     "pt_session_read_packed": (C.c_int, [_P, _P, C.c_size_t]),
     "pt_unpack_tiles": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P]),
     "pt_unpack_tiles_f32": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _P, _P]),
@@ -128,6 +129,12 @@ def _check(rc):
     if rc != PT_OK:
         raise PTError(rc, _lib.pt_last_error().decode(errors="replace"))
     return rc
+
+
+def last_error():
+    """pt_last_error(): the message of the calling thread's last failure (also one a call
+    recovered from, such as the RCCL gather's fail-over to the host)."""
+    return _lib.pt_last_error().decode(errors="replace")
 
 
 def _ptr(a):
@@ -253,6 +260,11 @@ class Session:
 
     def sync(self):
         _check(_lib.pt_session_sync(self._h))
+
+    def reset(self):
+        """Restart every owned pixel at sample 0 (buffers and counters kept): the next
+        trace(S) renders what a new session would."""
+        _check(_lib.pt_session_reset(self._h))
 
     def read_packed(self):
         out = np.zeros(self.packed_bytes, np.uint8)

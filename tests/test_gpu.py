@@ -331,9 +331,44 @@ def test_render_gather_paths(pt, ngpu_gather):
     with pt.Scene.load(U.golden_scene_path("dragon_64x64x16")) as s:
         rgb, r, st = s.render(radiance=True, gather=mode)
         rgb2, _, st2 = s.render(gather=mode)   # the cached communicator is reused
+        rgb3, _, st3 = s.render(gather=mode)   # ... and its buffers: nothing allocated
     assert st["gather_rccl"] == (1 if ngpu_gather == "rccl" else 0)
-    assert st2["gather_rccl"] == st["gather_rccl"]
-    assert np.array_equal(rgb, img) and np.array_equal(rgb2, img)
+    assert st2["gather_rccl"] == st3["gather_rccl"] == st["gather_rccl"]
+    assert st2["gather_allocs"] == st3["gather_allocs"] == 0
+    if ngpu_gather != "rccl":
+        assert st["gather_allocs"] == 0
+    assert np.array_equal(rgb, img) and np.array_equal(rgb2, img) and np.array_equal(rgb3, img)
+    assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
+
+
+def test_rccl_gather_buffers_grow_once(pt):
+    """The RCCL gather's send / receive buffers are kept per communicator: a render of a
+    larger frame than any before grows them once (gather_allocs > 0), and the next
+    renders of either size allocate nothing and keep the bytes."""
+    with pt.Scene.load(U.scene_path("c1")) as s:
+        big, _, st = s.render(gather=pt.GATHER_RCCL)
+        small, _, st2 = s.render(gather=pt.GATHER_RCCL, window=(16, 32, 64, 48))
+        big2, _, st3 = s.render(gather=pt.GATHER_RCCL)
+    assert st["gather_rccl"] == st2["gather_rccl"] == st3["gather_rccl"] == 1
+    assert st2["gather_allocs"] == 0 and st3["gather_allocs"] == 0
+    assert np.array_equal(big, big2) and np.array_equal(small, big[32:80, 16:80])
+    ppm = b"P6\n%d %d\n255\n" % (big.shape[1], big.shape[0]) + big.tobytes()
+    assert U.md5(ppm) == M["full"]["c1"]["md5"]
+
+
+def test_rccl_gather_fails_over_to_the_host(pt, monkeypatch):
+    """PT_GATHER_AUTO: when the RCCL gather fails (PT_TUNE inject_rccl=1 fails it before
+    any RCCL call), pt_render gathers through the host: the same bytes, gather_rccl = 0,
+    and the reason in pt_last_error.  PT_GATHER_RCCL makes the same failure an error."""
+    monkeypatch.setenv("PT_TUNE", "inject_rccl=1")
+    m, img, rad = U.golden_image("dragon_64x64x16")
+    with pt.Scene.load(U.golden_scene_path("dragon_64x64x16")) as s:
+        rgb, r, st = s.render(radiance=True, gather=pt.GATHER_AUTO)
+        assert "injected RCCL gather failure" in pt.last_error()
+        with pytest.raises(pt.PTError, match="injected RCCL gather failure"):
+            s.render(gather=pt.GATHER_RCCL)
+    assert st["gather_rccl"] == 0 and st["gather_allocs"] == 0
+    assert np.array_equal(rgb, img)
     assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
 
 

@@ -35,7 +35,7 @@ def test_abi_exports_every_declared_symbol():
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
     assert set(names) == set(pt.EXPORTED)
-    assert pt.abi_version() == pt.ABI_VERSION == 5
+    assert pt.abi_version() == pt.ABI_VERSION == 6
 
 
 @pytest.mark.parametrize("name", sorted(M["bvh"]))
