@@ -3,12 +3,14 @@
 
 Workload (N=1): config 3 of BASELINE.json -- the md5-pinned ~90k-triangle
 dragon stand-in (scenes/make_scene.py c3; the reference's dragon_100k file is
-missing) at 1920x1080, RAY_DEPTH 6.  One "step" = `--spp-per-step` (default 16)
-samples for every pixel of the frame: the reference's spp loop advanced by
-that many (each pixel's minstd_rand stream and f32 sum stay resident in HBM,
-so K steps are exactly the first K*spp of the 256 spp).  `value` = Mray/s =
-closest-hit queries (Scene::RayIntersection calls, counted on the GPU) over
-the timed region.
+missing) at 1920x1080, RAY_DEPTH 6.  One "step" = the metric's job: the whole
+frame at `--spp-per-step` (default 256, the config's SAMPLES) samples per pixel,
+as ONE pass from sample 0 (pt_session_reset re-seeds every pixel's minstd_rand
+stream and zeroes its f32 sum), then the device tonemap and the gather of the
+8-bit framebuffer -- so every step pays the pass's end tail exactly as the
+metric's render does, and the last step's framebuffer is the 256-spp image
+(checked against the CLI's PPM).  `value` = Mray/s = closest-hit queries
+(Scene::RayIntersection calls, counted on the GPU) over the timed region.
 
 Multi-GPU: one process per GPU.  `python bench.py --gpus N` (no WORLD_SIZE in
 the environment) starts the N ranks itself under torch.distributed.run before
@@ -18,11 +20,11 @@ ranks in diagonal stripes (no data-path collective).  `--scaling strong` (the
 default, the metric's own job: "1080p/256spp, 1/2/4/8 GPU"): a step is
 spp-per-step samples of EVERY pixel of the frame at any N, each rank rendering
 its 1/N of the pixels, so the job is fixed and N GPUs should finish it N times
-faster (`--steps 16` = the whole 256-spp frame).  `--scaling weak`: every rank
-advances its pixels by spp-per-step x N samples per step (per-GPU work fixed as
-N grows; one long pass per rank, which hides the end-of-pass tail).  The timed
-region ends with the framebuffer resolve (tonemap on device) and an RCCL gather
-of the packed 8-bit tiles to rank 0.
+faster.  `--scaling weak`: every rank renders its pixels at spp-per-step x N
+samples per step (per-GPU work fixed as N grows; a longer pass per rank, which
+hides more of the end-of-pass tail).  Every step ends with the framebuffer
+resolve (tonemap on device) and an RCCL gather of the packed 8-bit tiles to
+rank 0.
 
 Also reported: the roofline of the dominant kernel (k_wpath, the persistent
 path engine: closest-hit queries + shading) from in-kernel counters and
@@ -116,9 +118,10 @@ def probe_ranks(args, rank, world):
     got = [None] * world
     dist.all_gather_object(got, {"rank": rank, "pid": os.getpid(), "local_rank": int(os.environ.get("LOCAL_RANK", 0))})
     if rank == 0:
+        # (no scene here: the default spp is config 3's SAMPLES, 256; every step is one pass)
+        spp = rank_spp(args.spp_per_step or 256, world, args.scaling)
         print(json.dumps({"probe": True, "n_gpus": world, "gpus_arg": args.gpus, "ranks": got,
-                          "scaling": args.scaling, "rank_spp_per_step": rank_spp(args.spp_per_step, world, args.scaling),
-                          "pass_spp": rank_spp(args.spp_per_step, world, args.scaling) * args.steps}))
+                          "scaling": args.scaling, "rank_spp_per_step": spp, "pass_spp": spp}))
     dist.destroy_process_group()
     del torch
 
@@ -193,11 +196,12 @@ def host_cpus():
 # bounded samples of every BASELINE config (render only, load + BVH timed apart):
 #   name -> (scene config, spp override, x0, y0, w, rows, row stride)
 # Rows are spread over the frame (stride) so the sample's per-ray cost is the
-# frame's, not one band's.  c1 is the full image at full spp.
+# frame's, not one band's.  c1 is the full image at full spp; c3, the workload of
+# `value`, the full frame at 1 spp (the smallest spp of >= 60 s).
 CPU_SAMPLES = {
     "c1": ("c1", 0, 0, 0, 256, 256, 1),
     "c2": ("c2", 0, 0, 4, 512, 8, 64),
-    "c3": ("c3", 1, 0, 9, 1920, 12, 90),
+    "c3": ("c3", 1, 0, 0, 1920, 1080, 1),   # the full frame at SAMPLES 1 (~2 min on 16 threads)
     "c4_metal": ("c4_metal", 1, 0, 9, 1920, 6, 180),
     "c4_glass": ("c4_glass", 1, 0, 9, 1920, 6, 180),
     "c5": ("c5", 1, 0, 18, 3840, 4, 540),
@@ -425,8 +429,9 @@ def main():
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3")
-    ap.add_argument("--spp-per-step", type=int, default=16,
-                    help="samples per pixel per step (strong: of every pixel of the frame; weak: x N per rank)")
+    ap.add_argument("--spp-per-step", type=int, default=0,
+                    help="samples per pixel per step: one pass from sample 0 (default: the config's SAMPLES, 256 "
+                         "for c3; strong: of every pixel of the frame; weak: x N per rank)")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="strong (default): the frame's job split over N GPUs; weak: per-GPU work fixed")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -493,25 +498,29 @@ def main():
     t_ready = time.perf_counter()
     # strong: every pixel of the frame advances spp-per-step per step at any N (a rank owns 1/N of
     # them); weak: a rank's pixels advance N times as far, so its work per step is the one-GPU work
-    spp = rank_spp(args.spp_per_step, world, args.scaling)
+    spp = rank_spp(args.spp_per_step or info["samples"], world, args.scaling)
     packed = torch.empty(max(ss.packed_bytes, 1), dtype=torch.uint8, device=device)
-    for _ in range(args.warmup):
+
+    def step():
+        # the job: every owned pixel from sample 0 through `spp` samples as one pass, the
+        # device tonemap, and the 8-bit framebuffer's gather to rank 0
+        ss.reset()
         ss.trace(spp)
-    # the warmup also runs the resolve and the gather once (their first use loads code
-    # objects and sets up the collective, which is not a per-run cost)
-    ss.resolve(dev_out=packed.data_ptr() if ss.packed_bytes else None)
-    ss.sync()
-    gather_tiles(dist, packed[: ss.packed_bytes].to(coll_device), rank, world, W, H, coll_device)
+        ss.resolve(dev_out=packed.data_ptr() if ss.packed_bytes else None)
+        ss.sync()
+        return gather_tiles(dist, packed[: ss.packed_bytes].to(coll_device), rank, world, W, H, coll_device)
+
+    # (the warmup's first resolve and gather load code objects and set up the collective)
+    for _ in range(max(args.warmup, 0)):
+        step()
     ss.sync()
     st0 = ss.stats()
 
     barrier()
     t0 = time.perf_counter()
+    img = None
     for _ in range(args.steps):
-        ss.trace(spp)
-    ss.resolve(dev_out=packed.data_ptr() if ss.packed_bytes else None)
-    ss.sync()
-    img = gather_tiles(dist, packed[: ss.packed_bytes].to(coll_device), rank, world, W, H, coll_device)
+        img = step()
     barrier()
     t1 = time.perf_counter()
     st1 = ss.stats()
@@ -544,7 +553,7 @@ def main():
         T = float(tmax[0])
         total_rays = float(tsum[1])
         res = {
-            "metric": "Mray/s (closest-hit queries/s), dragon stand-in 1080p, RAY_DEPTH 6",
+            "metric": "Mray/s (closest-hit queries/s), dragon stand-in 1080p/%d spp, RAY_DEPTH 6" % spp,
             "value": total_rays / T / 1e6,
             "unit": "Mray/s",
             "n_gpus": world,
@@ -556,10 +565,10 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: md5-pinned 89,928-triangle dragon stand-in (SURVEY §8d), per-pixel reference seeds",
-            "config": {"workload": "config 3: %s %dx%d, %d spp of every pixel per step (%s scaling; the metric's "
-                                   "job is 256 spp = 16 steps of 16), RAY_DEPTH %d; %s traversal of the reference "
-                                   "tree (bit-exact)" % (args.config, W, H, spp, args.scaling, info["ray_depth"],
-                                                         args.traversal),
+            "config": {"workload": "config 3: %s %dx%d, one step = the job: every pixel from sample 0 through "
+                                   "%d spp as one pass + device tonemap + gather (%s scaling), RAY_DEPTH %d; %s "
+                                   "traversal of the reference tree (bit-exact)"
+                                   % (args.config, W, H, spp, args.scaling, info["ray_depth"], args.traversal),
                        "pixels": W * H, "samples_per_step": W * H * spp,
                        "spp_per_step_per_pixel": spp, "scaling": args.scaling,
                        "parallelism": "pixel tiles x%d" % world},
@@ -568,7 +577,7 @@ def main():
             "kernel_ms_per_step": kms / args.steps,
             "rays": total_rays,
             "msamples_per_s": W * H * spp * args.steps / T / 1e6,
-            "pass_spp": spp * args.steps,
+            "pass_spp": spp,
             "node_visits_per_ray": float(tsum[2]) / max(total_rays, 1),
             "aux_visits_per_ray": float(tsum[6]) / max(total_rays, 1),
             "fallback_rate": float(tsum[7]) / max(total_rays, 1),
@@ -585,7 +594,7 @@ def main():
         }
         if per_rank:
             res["per_rank"] = per_rank
-        res["projected_c3_render_s"] = (256.0 / (spp * args.steps)) * T
+        res["job_s"] = T / max(args.steps, 1)   # one job (step): the frame's pass, tonemap and gather
     ss.close()
     scene.close()
     # the host-side legs run after the timed region, on rank 0 only; the other
@@ -607,6 +616,10 @@ def main():
                 # kernel time (HIP events) and over pt_render's wall -- beside `value`, whose 16-spp
                 # steps coalesce into a pass of steps x 16
                 res["render_256spp_mray_s"] = res["wall_to_ppm"]["render_mray_s"]
+                if res["framebuffer_md5"] and spp == info["samples"]:
+                    # the last step's framebuffer is the config's image: the CLI's PPM payload
+                    ppm = b"P6\n%d %d\n255\n" % (W, H) + img.tobytes()
+                    res["framebuffer_equals_cli_ppm"] = hashlib.md5(ppm).hexdigest() == res["wall_to_ppm"]["ppm_md5"]
                 res["render_256spp_wall_mray_s"] = res["wall_to_ppm"]["render_wall_mray_s"]
                 res["render_256spp_clocks"] = ("render_256spp_mray_s: rays / the pass's kernel time (HIP "
                                                "events); render_256spp_wall_mray_s: rays / pt_render's wall "

@@ -122,16 +122,16 @@ def test_bench_gpus_n_starts_n_ranks(n):
     assert sorted(r["local_rank"] for r in out["ranks"]) == list(range(n))
 
 
-@pytest.mark.parametrize("scaling,spp", [("strong", 16), ("weak", 32), (None, 16)])
+@pytest.mark.parametrize("scaling,spp", [("strong", 256), ("weak", 512), (None, 256)])
 def test_bench_scaling_modes(scaling, spp):
-    """`--scaling strong` (default): a step advances every pixel of the frame by
-    spp-per-step at any N -- the metric's fixed job, 16 steps = 256 spp; `--scaling
-    weak`: a rank's pixels advance N x spp-per-step per step (per-GPU work fixed)."""
-    args = ["--gpus", "2", "--probe-ranks", "--steps", "16"] + (["--scaling", scaling] if scaling else [])
+    """`--scaling strong` (default): a step is the metric's fixed job -- every pixel of
+    the frame at 256 spp (config 3's SAMPLES), one pass from sample 0, at any N;
+    `--scaling weak`: a rank's pixels take N x 256 spp per step (per-GPU work fixed)."""
+    args = ["--gpus", "2", "--probe-ranks", "--steps", "3"] + (["--scaling", scaling] if scaling else [])
     rc, out, err = _bench(args)
     assert rc == 0, err[-2000:]
     assert out["scaling"] == (scaling or "strong")
-    assert out["rank_spp_per_step"] == spp and out["pass_spp"] == 16 * spp
+    assert out["rank_spp_per_step"] == spp and out["pass_spp"] == spp
     assert sorted(r["rank"] for r in out["ranks"]) == [0, 1]
 
 

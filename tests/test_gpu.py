@@ -341,6 +341,35 @@ def test_render_gather_paths(pt, ngpu_gather):
     assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
 
 
+def test_session_reset_renders_the_job_again(pt):
+    """pt_session_reset restarts every owned pixel at sample 0: after any pass, reset +
+    trace(S) gives the bytes, radiance and rays of a new session's trace(S) (bench.py
+    repeats the metric's frame this way)."""
+    m, img, rad = U.golden_image("dragon_64x64x16")
+    with pt.Scene.load(U.golden_scene_path("dragon_64x64x16")) as s:
+        s.prepare()
+        spp = s.info["samples"]
+        outs = []
+        ss = pt.Session(s, device=0)
+        for pre in (0, 5, spp):
+            if pre:
+                ss.trace(pre)
+                ss.sync()
+                ss.reset()
+            st0 = ss.stats()
+            ss.trace(spp)
+            ss.resolve()
+            ss.sync()
+            st1 = ss.stats()
+            outs.append((ss.read_packed(), st1["rays"] - st0["rays"]))
+        ss.close()
+        ref, _, st = s.render()
+    for packed, rays in outs:
+        got = np.zeros_like(ref)
+        pt.unpack_tiles(packed, ref.shape[1], ref.shape[0], 0, 1, got)
+        assert np.array_equal(got, img) and rays == st["rays"]
+
+
 def test_rccl_gather_buffers_grow_once(pt):
     """The RCCL gather's send / receive buffers are kept per communicator: a render of a
     larger frame than any before grows them once (gather_allocs > 0), and the next
