@@ -19,13 +19,14 @@ namespace pt {
 enum : uint32_t { QH_IDX = 0u, QH_T, QH_LID, QH_NX, QH_NY, QH_NZ, QH_IN, QH_INFO, QH_N };
 template <uint32_t T>
 struct QcTeamLds {
-    static constexpr uint32_t SCAP = T == 64u ? 448u : T == 32u ? 192u : QC_SCAP_MIN;   // aux stack (also the
-                                                                                      // leader's exact DFS stack)
+    // aux stack words per chain (also the leader's exact DFS stack): a whole-wave team's own;
+    // smaller teams share their wave's pool (QcPoolLds), SCAP words per chain
+    static constexpr uint32_t SCAP = T == 64u ? 448u : T == 32u ? 192u : QC_SCAP_MIN;
     static constexpr uint32_t CCAP = 5u * T;                    // candidates (< T + 4 T at any time)
     static constexpr uint32_t HCAP = T >= 32u ? 32u : T == 16u ? 16u : 12u;   // hitting leaves per query (more: the
                                                                               // exact DFS); LDS fits 3 WGs per CU
-    uint32_t stk[SCAP];
-    uint32_t cand[CCAP];
+    uint32_t stk[T == 64u ? SCAP : 1u];
+    uint32_t cand[T == 64u ? CCAP : 1u];
     uint32_t hl[QH_N][HCAP];       // hitting leaves: index, first-min t, its prim, hit normal and side,
                                    // ancestor-list info
     uint32_t perm[HCAP];           // their preorder: perm[k] = the entry of the k-th smallest index
@@ -34,6 +35,24 @@ struct QcTeamLds {
     uint4 fold[QC_FOLD];           // ... and {idm, s1, s2, -}
     uint4 sum;                     // the pixel's sum.rgb and global index (rec[2 slot + 1]) while the team
                                    // owns it (touched at path ends only: registers would spill)
+};
+// per wave, teams of T < 64 (qc_pool): the chains' pending aux nodes and candidate
+// leaves, (chain << 29 | node / leaf ordinal) items, and each chain's ray
+template <uint32_t T>
+struct QcPoolLds {
+    static constexpr uint32_t CPW = 64u / T;                    // chains per wave
+    static constexpr uint32_t SW = QcTeamLds<T>::SCAP * CPW;    // pending nodes (chain c's exact DFS stack after
+                                                                // the query: words [c SCAP, (c + 1) SCAP))
+    static constexpr uint32_t CW = 128u;                        // candidates (< 64 + 64 at any time)
+    uint32_t stk[SW];
+    uint32_t cand[CW];
+    F4 ray[CPW][4];                // {o.xyz, pre.w}, {d.xyz, -}, {1/d}, {o / d}
+    uint32_t nh[CPW];              // hitting leaves found (may pass HCAP: then the exact DFS)
+    uint32_t ovf[CPW];             // the chain takes the exact DFS (its items are skipped)
+};
+template <>
+struct QcPoolLds<64u> {
+    uint32_t unused;
 };
 // per workgroup: the records every chain cycle reads, copied once per launch
 struct QcScene {
@@ -115,6 +134,124 @@ __device__ __forceinline__ void lc_add(uint32_t* lc, uint32_t k, bool c, uint32_
 #define QC_CP_PASS
 #endif
 
+// Phases 3-5 of the query, per team (team-uniform arguments; dec = this team decides):
+// the hitting leaves L.hl[0, nh) in reference preorder, each decided on its root path
+// with the bound the recursion carries there; the result as qc_team's.
+template <uint32_t T>
+__device__ __forceinline__ int qc_decide(const SceneView& S, QcTeamLds<T>& L, bool on, bool dec, uint32_t nh,
+                                         const Ray& ray, float P, int pid, uint32_t* lc, Hit& hit,
+                                         bool& bvh QC_CP_ARG) {
+    QC_T0();
+    const uint32_t lane = lane_id(), tl = lane % T, tbase = lane - tl;
+    const unsigned long long tmask = T == 64u ? ~0ull : (((1ull << T) - 1ull) << tbase);
+    // 3. the hitting leaves in reference preorder (distinct indices: rank = count below)
+    for (uint32_t i0 = 0;; i0 += T) {
+        const bool srt = dec && i0 < nh;
+        if (__ballot(srt) == 0ull) break;
+        const bool act = srt && i0 + tl < nh;
+        const uint32_t c = act ? L.hl[QH_IDX][i0 + tl] : 0u;
+        uint32_t rank = 0u;
+        for (uint32_t j = 0; __ballot(srt && j < nh) != 0ull; ++j)
+            if (srt && j < nh) rank += L.hl[QH_IDX][j] < c ? 1u : 0u;
+        if (act) L.perm[rank] = i0 + tl;
+    }
+    // 4. decide them in order: lane j of the team holds nodes j, j + T, ... of the
+    //    leaf's root path with their exact slab results (the reference's division form)
+    constexpr uint32_t NB = 64u / T;            // path blocks (a root path has at most 63 nodes)
+    constexpr uint32_t NG = NB < 4u ? NB : 4u;  // blocks loaded together
+    uint32_t nrec = 0u;
+    float bt = PT_INF;
+    int res = pid, resk = -1;
+    for (uint32_t kk = 0;; ++kk) {
+        const bool dk = dec && kk < nh;
+        if (__ballot(dk) == 0ull) break;
+        const uint32_t ke = dk ? L.perm[kk] : 0u;   // the kk-th hitting leaf in preorder
+        const uint32_t info = dk ? L.hl[QH_INFO][ke] : 0u;
+        const uint32_t off = info & 0x03ffffffu, len = dk ? info >> 26 : 0u;
+        float carry = P;          // the bound at the previous block's last node
+        uint32_t vlast = 0u;      // that node
+        bool fail = false;
+        for (uint32_t g = 0; g < NB; g += NG) {
+            if (__ballot(g * T < len) == 0ull) break;
+            uint32_t v[NG], hf[NG];
+            float tq[NG];
+#pragma unroll
+            for (uint32_t b = 0; b < NG; ++b) {
+                const uint32_t j = (g + b) * T + tl;
+                v[b] = j < len ? S.anc[off + j] : 0u;
+            }
+#pragma unroll
+            for (uint32_t b = 0; b < NG; ++b) {
+                const bool pon = (g + b) * T + tl < len;
+                const Node nd = S.nodes[v[b]];
+                float t = 0.f;
+                uint32_t in = 0u;
+                const bool hs = pon && node_slab(nd, ray, t, in);
+                tq[b] = t;
+                hf[b] = (hs ? 1u : 0u) | (in << 1);
+                lc_add(lc, LC_NODES, pon);
+            }
+#pragma unroll
+            for (uint32_t b = 0; b < NG; ++b) {
+                if (__ballot((g + b) * T < len) == 0ull) break;
+                const uint32_t j = (g + b) * T + tl;
+                const bool pon = j < len;
+                const uint32_t up = __shfl(v[b], (int)(lane == 0u ? 0u : lane - 1u), 64);
+                const uint32_t prev = tl == 0u ? vlast : up;
+                // the carried bound: at a right child the minimum over the entered hits of its
+                // left sibling's subtree (prev, v), if any; else the parent's (scan down the path)
+                const bool rc = pon && j > 0u && v[b] != prev + 1u;
+                float m = 0.f;
+                bool any = false;
+                for (uint32_t r = 0; __ballot(r < nrec) != 0ull; ++r) {
+                    if (r < nrec) {
+                        const uint32_t ri = L.r_idx[r];
+                        const float rt = u2f(L.r_t[r]);
+                        if (rc && ri > prev && ri < v[b]) {
+                            if (!any || rt < m) m = rt;
+                            any = true;
+                        }
+                    }
+                }
+                const unsigned long long dm = __ballot(any) & tmask;
+                const unsigned long long below = dm & ((2ull << lane) - 1ull);
+                const int src = below ? 63 - __clzll((long long)below) : (int)lane;
+                const float mb = __shfl(m, src, 64);
+                const float bound = below ? mb : carry;
+                // src/bvh.cpp:188-198: slab miss, or pruned by the bound (not interior)
+                const bool ok = !pon || ((hf[b] & 1u) && !(bound < tq[b] && !(hf[b] & 2u)));
+                fail = fail || (__ballot(!ok) & tmask) != 0ull;
+                carry = __shfl(bound, (int)(tbase + T - 1u), 64);
+                vlast = __shfl(v[b], (int)(tbase + T - 1u), 64);
+            }
+        }
+        if (dk && !fail) {
+            // 5. entered: record; first strict minimum; replaces the plane iff closer
+            const float lt = u2f(L.hl[QH_T][ke]);
+            if (tl == 0u) {
+                L.r_idx[nrec] = L.hl[QH_IDX][ke];
+                L.r_t[nrec] = f2u(lt);
+            }
+            ++nrec;
+            if (lt < bt) {
+                bt = lt;
+                if (lt < P) {
+                    res = (int)L.hl[QH_LID][ke];
+                    resk = (int)ke;
+                }
+            }
+        }
+    }
+    QC_TICK(2);
+    if (resk >= 0) {
+        bvh = true;
+        hit.t = u2f(L.hl[QH_T][resk]);
+        hit.n = mk3(u2f(L.hl[QH_NX][resk]), u2f(L.hl[QH_NY][resk]), u2f(L.hl[QH_NZ][resk]));
+        hit.interior = L.hl[QH_IN][resk];
+    }
+    return on ? res : -1;
+}
+
 // The query of one ray per team (every argument team-uniform; `on` = this team has
 // a query).  `reserve` = 3 (aux depth + 2): above SCAP - reserve pending nodes the
 // expansion takes fewer nodes per round, so a depth-first descent still fits.
@@ -128,8 +265,8 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
     constexpr uint32_t SCAP = QcTeamLds<T>::SCAP, HCAP = QcTeamLds<T>::HCAP;
     const uint32_t lane = lane_id(), tl = lane % T, tbase = lane - tl;
     const unsigned long long tmask = T == 64u ? ~0ull : (((1ull << T) - 1ull) << tbase);
-    const uint32_t slim = SCAP - reserve;
     bvh = false;
+    const uint32_t slim = SCAP - reserve;
     exact = on && pre.w != pre.w;
     const bool run = on && !exact;
     const bool par = signbit(pre.w);
@@ -250,113 +387,155 @@ __device__ int qc_team(const SceneView& S, const QcScene& Q, QcTeamLds<T>& L, bo
     }
     QC_TICK(0);
     if (ovf) exact = true;
-    const bool dec = run && !ovf;
-    // 3. the hitting leaves in reference preorder (distinct indices: rank = count below)
-    for (uint32_t i0 = 0;; i0 += T) {
-        const bool srt = dec && i0 < nh;
-        if (__ballot(srt) == 0ull) break;
-        const bool act = srt && i0 + tl < nh;
-        const uint32_t c = act ? L.hl[QH_IDX][i0 + tl] : 0u;
-        uint32_t rank = 0u;
-        for (uint32_t j = 0; __ballot(srt && j < nh) != 0ull; ++j)
-            if (srt && j < nh) rank += L.hl[QH_IDX][j] < c ? 1u : 0u;
-        if (act) L.perm[rank] = i0 + tl;
+    return qc_decide<T>(S, L, on, run && !ovf, nh, ray, P, pid, lc, hit, bvh QC_CP_PASS);
+}
+
+// The query for teams of T < 64 lanes, phases 1-2 pooled over the wave: the 64/T
+// chains' aux expansions share one stack of (chain, node) items and one list of
+// (chain, leaf) candidates, so every round expands up to 16 pending nodes (a lane
+// per entry) and tests up to 64 candidates, of whichever chains have them.  A team
+// of 8 lanes alone expands 2 nodes per round, and the wave's teams run in step, so
+// its rounds followed its slowest chain's work; pooled they follow the chains' sum
+// (and the depth).  Which leaves are collected does not depend on the order, and the
+// hitting leaves go to their team's list (L.hl, any order: qc_decide sorts them),
+// so the result is qc_team's.  The lanes that take an item read its chain's ray from
+// the pool (W.ray).  `reserve` as for qc_team, over the pool.
+template <uint32_t T>
+__device__ int qc_pool(const SceneView& S, const QcScene& Q, QcPoolLds<T>& W, QcTeamLds<T>* Lw, bool on,
+                       const Ray& ray, float P, int pid, F4 pre, uint32_t reserve, uint32_t* lc, bool& exact, Hit& hit,
+                       bool& bvh QC_CP_ARG) {
+    QC_T0();
+    constexpr uint32_t SW = QcPoolLds<T>::SW, HCAP = QcTeamLds<T>::HCAP;
+    constexpr uint32_t KN = 64u / PT_AUXW;      // nodes per expansion round
+    const uint32_t lane = lane_id(), tl = lane % T, team = lane / T;
+    bvh = false;
+    exact = on && pre.w != pre.w;
+    const bool run = on && !exact;
+    if (tl == 0u) {
+        // the chain's ray and query set-up, for the lanes that take its items
+        W.ray[team][0] = F4{ray.o.x, ray.o.y, ray.o.z, pre.w};
+        W.ray[team][1] = F4{ray.d.x, ray.d.y, ray.d.z, 0.f};
+        W.ray[team][2] = F4{pre.x, pre.y, pre.z, 0.f};
+        W.ray[team][3] = F4{ray.o.x * pre.x, ray.o.y * pre.y, ray.o.z * pre.z, 0.f};
+        W.nh[team] = 0u;
+        W.ovf[team] = 0u;
     }
-    // 4. decide them in order: lane j of the team holds nodes j, j + T, ... of the
-    //    leaf's root path with their exact slab results (the reference's division form)
-    constexpr uint32_t NB = 64u / T;            // path blocks (a root path has at most 63 nodes)
-    constexpr uint32_t NG = NB < 4u ? NB : 4u;  // blocks loaded together
-    uint32_t nrec = 0u;
-    float bt = PT_INF;
-    int res = pid, resk = -1;
-    for (uint32_t kk = 0;; ++kk) {
-        const bool dk = dec && kk < nh;
-        if (__ballot(dk) == 0ull) break;
-        const uint32_t ke = dk ? L.perm[kk] : 0u;   // the kk-th hitting leaf in preorder
-        const uint32_t info = dk ? L.hl[QH_INFO][ke] : 0u;
-        const uint32_t off = info & 0x03ffffffu, len = dk ? info >> 26 : 0u;
-        float carry = P;          // the bound at the previous block's last node
-        uint32_t vlast = 0u;      // that node
-        bool fail = false;
-        for (uint32_t g = 0; g < NB; g += NG) {
-            if (__ballot(g * T < len) == 0ull) break;
-            uint32_t v[NG], hf[NG];
-            float tq[NG];
-#pragma unroll
-            for (uint32_t b = 0; b < NG; ++b) {
-                const uint32_t j = (g + b) * T + tl;
-                v[b] = j < len ? S.anc[off + j] : 0u;
+    // every running chain's root node
+    const unsigned long long mr = __ballot(run && tl == 0u);
+    if (run && tl == 0u) W.stk[lanes_below(mr)] = team << 29;
+    uint32_t ns = (uint32_t)__popcll(mr), nc = 0u;   // wave-uniform
+    bool wovf = false;                               // the pool overflowed: every chain takes the exact DFS
+    const uint32_t slim = SW - reserve;
+    for (;;) {
+        // 2. candidate leaves, 64 at a time (the rest once the expansion is over): the
+        //    bundle's bound-free slab test and first-primitive test in one round of
+        //    loads, then the leaf's further primitives
+        while (nc >= 64u || (ns == 0u && nc > 0u)) {
+            QC_TICK(0);
+            const uint32_t take = nc < 64u ? nc : 64u;
+            nc -= take;
+            const uint32_t item = lane < take ? W.cand[nc + lane] : 0u;
+            const uint32_t ch = item >> 29;
+            const bool act = lane < take && W.ovf[ch] == 0u;
+            const F4 q0 = W.ray[ch][0], q1 = W.ray[ch][1], q2 = W.ray[ch][2];
+            Ray ir;
+            ir.o = mk3(q0.x, q0.y, q0.z);
+            ir.d = mk3(q1.x, q1.y, q1.z);
+            const f3 iinv = mk3(q2.x, q2.y, q2.z);
+            const uint32_t ord = act ? item & 0x1fffffffu : 0u;
+            const uint32_t bo = S.o_bundle + PT_BUNDLE_BYTES * ord;
+            const F4 b0 = blob_piece(S, bo), b1 = blob_piece(S, bo + 16u), b2 = blob_piece(S, bo + 32u),
+                     b3 = blob_piece(S, bo + 48u), b4 = blob_piece(S, bo + 64u), b5 = blob_piece(S, bo + 80u);
+            const uint32_t c = f2u(b3.x);          // the reference leaf
+            const uint32_t ainfo = act ? S.anc_info[c] : 0u;
+            Node nd;
+            nd.a = b4;                             // the leaf's node record: {c.xyz, s.x}, {s.y, s.z, first, count}
+            nd.b = F4{b5.x, b5.y, b3.y, b3.z};
+            lc_add(lc, LC_NODES, act);
+            const bool hb = act && qc_slab_hit(nd, ir, iinv, signbit(q0.w));
+            const uint32_t ref = f2u(b3.y), cnt = hb ? f2u(b3.z) : 0u;
+            Hit best;
+            best.t = PT_INF;
+            best.n = mk3(0.f, 0.f, 0.f);
+            best.interior = 0u;
+            int lid = -1;
+            lc_add(lc, LC_PTESTS, cnt != 0u);
+            if (cnt) {
+                Hit hh;
+                if (qc_prim_hit_rec(S, ref, b0, b1, b2, F4{b3.w, 0.f, 0.f, 0.f}, ir, hh)) { best = hh; lid = (int)ref; }
             }
-#pragma unroll
-            for (uint32_t b = 0; b < NG; ++b) {
-                const bool pon = (g + b) * T + tl < len;
-                const Node nd = S.nodes[v[b]];
-                float t = 0.f;
-                uint32_t in = 0u;
-                const bool hs = pon && node_slab(nd, ray, t, in);
-                tq[b] = t;
-                hf[b] = (hs ? 1u : 0u) | (in << 1);
-                lc_add(lc, LC_NODES, pon);
-            }
-#pragma unroll
-            for (uint32_t b = 0; b < NG; ++b) {
-                if (__ballot((g + b) * T < len) == 0ull) break;
-                const uint32_t j = (g + b) * T + tl;
-                const bool pon = j < len;
-                const uint32_t up = __shfl(v[b], (int)(lane == 0u ? 0u : lane - 1u), 64);
-                const uint32_t prev = tl == 0u ? vlast : up;
-                // the carried bound: at a right child the minimum over the entered hits of its
-                // left sibling's subtree (prev, v), if any; else the parent's (scan down the path)
-                const bool rc = pon && j > 0u && v[b] != prev + 1u;
-                float m = 0.f;
-                bool any = false;
-                for (uint32_t r = 0; __ballot(r < nrec) != 0ull; ++r) {
-                    if (r < nrec) {
-                        const uint32_t ri = L.r_idx[r];
-                        const float rt = u2f(L.r_t[r]);
-                        if (rc && ri > prev && ri < v[b]) {
-                            if (!any || rt < m) m = rt;
-                            any = true;
-                        }
-                    }
-                }
-                const unsigned long long dm = __ballot(any) & tmask;
-                const unsigned long long below = dm & ((2ull << lane) - 1ull);
-                const int src = below ? 63 - __clzll((long long)below) : (int)lane;
-                const float mb = __shfl(m, src, 64);
-                const float bound = below ? mb : carry;
-                // src/bvh.cpp:188-198: slab miss, or pruned by the bound (not interior)
-                const bool ok = !pon || ((hf[b] & 1u) && !(bound < tq[b] && !(hf[b] & 2u)));
-                fail = fail || (__ballot(!ok) & tmask) != 0ull;
-                carry = __shfl(bound, (int)(tbase + T - 1u), 64);
-                vlast = __shfl(v[b], (int)(tbase + T - 1u), 64);
-            }
-        }
-        if (dk && !fail) {
-            // 5. entered: record; first strict minimum; replaces the plane iff closer
-            const float lt = u2f(L.hl[QH_T][ke]);
-            if (tl == 0u) {
-                L.r_idx[nrec] = L.hl[QH_IDX][ke];
-                L.r_t[nrec] = f2u(lt);
-            }
-            ++nrec;
-            if (lt < bt) {
-                bt = lt;
-                if (lt < P) {
-                    res = (int)L.hl[QH_LID][ke];
-                    resk = (int)ke;
+            for (uint32_t i = 1; __ballot(i < cnt) != 0ull; ++i) {
+                lc_add(lc, LC_PTESTS, i < cnt);
+                if (i < cnt) {
+                    Hit hh;
+                    if (qc_prim_hit(S, ref + i, ir, hh) && hh.t < best.t) { best = hh; lid = (int)(ref + i); }
                 }
             }
+            if (lid >= 0) {
+                // (distinct leaves: the list's order is free)
+                const uint32_t j = atomicAdd(&W.nh[ch], 1u);
+                if (j < HCAP) {
+                    QcTeamLds<T>& H = Lw[ch];
+                    H.hl[QH_IDX][j] = c;
+                    H.hl[QH_T][j] = f2u(best.t);
+                    H.hl[QH_LID][j] = (uint32_t)lid;
+                    H.hl[QH_NX][j] = f2u(best.n.x);
+                    H.hl[QH_NY][j] = f2u(best.n.y);
+                    H.hl[QH_NZ][j] = f2u(best.n.z);
+                    H.hl[QH_IN][j] = best.interior;
+                    H.hl[QH_INFO][j] = ainfo;
+                } else {
+                    W.ovf[ch] = 1u;                // more hitting leaves than the list: the exact DFS
+                }
+            }
+            QC_TICK(1);
         }
+        if (ns == 0u) break;
+        // 1. expansion: the KN most recent pending nodes (with few free words the pool
+        //    is expanded depth-first, so a descent fits the reserve), a lane per entry
+        uint32_t k = slim > ns ? (slim - ns) / 3u : 0u;
+        k = k < 1u ? 1u : k;
+        k = k > KN ? KN : k;
+        k = k > ns ? ns : k;
+        if (ns + 3u * k > SW) {                    // cannot happen with the host's reserve (checked)
+            wovf = true;
+            break;
+        }
+        ns -= k;
+        const uint32_t ni = lane / PT_AUXW, e = lane % PT_AUXW;
+        const uint32_t item = ni < k ? W.stk[ns + ni] : 0u;
+        const uint32_t ch = item >> 29, node = item & 0x1fffffffu;
+        const bool act = ni < k && W.ovf[ch] == 0u;
+        lc_add(lc, LC_AUX, act && e == 0u);
+        F4 ea, eb;
+        if (node < QC_TOPN) {
+            ea = Q.top[node * PT_AUXW + e].a;
+            eb = Q.top[node * PT_AUXW + e].b;
+        } else {
+            const uint32_t bo = S.o_aux + (node * PT_AUXW + e) * (uint32_t)sizeof(AuxSL);
+            ea = blob_piece(S, bo);
+            eb = blob_piece(S, bo + 16u);
+        }
+        const F4 q0 = W.ray[ch][0], q1 = W.ray[ch][1], q2 = W.ray[ch][2], q3 = W.ray[ch][3];
+        Ray ir;
+        ir.o = mk3(q0.x, q0.y, q0.z);
+        ir.d = mk3(q1.x, q1.y, q1.z);
+        const uint32_t code = f2u(eb.w);
+        bool h = act && code != 0xffffffffu;
+        if (h) h = aux_entry_hit(ea, eb, ir, mk3(q2.x, q2.y, q2.z), mk3(q3.x, q3.y, q3.z), q0.w);
+        const bool leaf = h && (code & 0x80000000u) != 0u;
+        const bool inner = h && (code & 0x80000000u) == 0u;
+        const unsigned long long mi = __ballot(inner), ml = __ballot(leaf);
+        if (inner) W.stk[ns + lanes_below(mi)] = ch << 29 | code;
+        if (leaf) W.cand[nc + lanes_below(ml)] = ch << 29 | f2u(eb.z);   // (a leaf entry's range: its bundle)
+        ns += (uint32_t)__popcll(mi);
+        nc += (uint32_t)__popcll(ml);
     }
-    QC_TICK(2);
-    if (resk >= 0) {
-        bvh = true;
-        hit.t = u2f(L.hl[QH_T][resk]);
-        hit.n = mk3(u2f(L.hl[QH_NX][resk]), u2f(L.hl[QH_NY][resk]), u2f(L.hl[QH_NZ][resk]));
-        hit.interior = L.hl[QH_IN][resk];
-    }
-    return on ? res : -1;
+    QC_TICK(0);
+    const uint32_t nh = W.nh[team];
+    const bool ovf = run && (wovf || W.ovf[team] != 0u || nh > HCAP);
+    if (ovf) exact = true;
+    return qc_decide<T>(S, Lw[team], on, run && !ovf, nh, ray, P, pid, lc, hit, bvh QC_CP_PASS);
 }
 
 // the chain's pixel state while a team owns it (its first lane's registers; the sum
@@ -430,6 +609,7 @@ template <uint32_t T, bool BIG>
 __global__ void __launch_bounds__(64u * QC_WAVES) __attribute__((amdgpu_waves_per_eu(QC_WAVES_PER_EU, QC_WAVES_PER_EU)))
 k_wcoop(WaveParams P) {
     __shared__ QcTeamLds<T> Ls[QC_WAVES * (64u / T)];
+    __shared__ QcPoolLds<T> Pool[T < 64u ? QC_WAVES : 1u];   // (teams of T < 64: the wave's query pool)
     __shared__ QcScene Q;
     const uint32_t lane = lane_id(), tl = lane % T, tbase = lane - tl;
     QcTeamLds<T>& L = Ls[(threadIdx.x >> 6) * (64u / T) + lane / T];
@@ -545,13 +725,21 @@ k_wcoop(WaveParams P) {
         if (__ballot(have) == 0ull) break;
         bool ex, bvh;
         Hit h;
-        int id = qc_team<T>(P.S, Q, L, have, ray, Pt, pid, pre, P.coop_reserve, lc, ex, h, bvh QC_CP_PASS);
+        int id;
+        if constexpr (T < 64u)
+            id = qc_pool<T>(P.S, Q, Pool[threadIdx.x >> 6], &Ls[(threadIdx.x >> 6) * (64u / T)], have, ray, Pt, pid, pre,
+                            P.coop_reserve, lc, ex, h, bvh QC_CP_PASS);
+        else
+            id = qc_team<T>(P.S, Q, L, have, ray, Pt, pid, pre, P.coop_reserve, lc, ex, h, bvh QC_CP_PASS);
         bool emit = false, sdone = false;
         QC_T0();
         if (tl == 0u && have) {
             if (ex) {
                 // the exact stack DFS (non-finite rays, too many hitting leaves)
-                LdsMemN<1u> stk{L.stk};
+                // (its stack: the team's own, or its chain's slice of the wave's pool)
+                uint32_t* xs = L.stk;
+                if constexpr (T < 64u) xs = Pool[threadIdx.x >> 6].stk + (lane / T) * QcTeamLds<T>::SCAP;
+                LdsMemN<1u> stk{xs};
                 QCounts Cx{0u, 0u, 0u, 0u};
                 id = q_exact(P.S, ray, stk, h, Cx);
                 atomicAdd(lc + LC_NODES, Cx.nodes);
