@@ -158,7 +158,24 @@ typedef struct pt_stats {
     /* ABI 6: device allocations pt_render's RCCL gather made (its send / receive buffers are
        kept per communicator: 0 on every render after the first of a device set and size) */
     uint64_t gather_allocs;
+    /* ABI 6: work items handed on at each place where work changes hands between the
+       engines' launches, waves or queues (PT_HO_*; DESIGN.md §4 "Hand-off sites") */
+    uint64_t handoff[12];
 } pt_stats;
+/* pt_stats.handoff sites (each has a PT_TUNE hook that forces it and one, drop=<name>, that
+ * drops its items -- the resolve must then fail: INTEGRATION.md) */
+enum {
+    PT_HO_SUSPEND = 0,      /* path engine, round end: running queries -> the next carry queue */
+    PT_HO_FLUSH = 1,        /* path engine, shade wave after the query waves left: next rays -> next fresh queue */
+    PT_HO_RINGOUT = 2,      /* path engine, shade wave's exit: ray-ring leftovers -> next fresh queue */
+    PT_HO_EXACT = 3,        /* path engine: a query -> the exact-DFS kernels (k_wexact, k_wshade) */
+    PT_HO_SIDE_TAKE = 4,    /* early cooperative launch: the heaviest chains taken from the round's work */
+    PT_HO_SIDE_YIELD = 5,   /* early launch's stop: its running chains -> the next carry queue */
+    PT_HO_SIDE_HANDON = 6,  /* early launch's late workgroups: untaken items -> the next carry queue */
+    PT_HO_GROW_YIELD = 7,   /* final launch's grow stop: its running chains -> the bigger teams' launch */
+    PT_HO_GROW_HANDON = 8,  /* final launch's late workgroups: untaken items -> the bigger teams' launch */
+    PT_HO_N = 9
+};
 
 /* Scene::Render minus the stream write: renders W*H*3 u8 (row-major, top row
  * first, exactly the reference's P6 payload) into rgb, and optionally the

@@ -91,7 +91,7 @@ enum : uint32_t { C_FRESH = 0u, C_CARRY = 1u, C_DONE = 3u, C_EXACT = 4u, C_FRONT
 #define PT_CTL_SET 288u          // words per counter set (C_HEADS + 8 x 32)
 // statistics counters: one copy per XCD (PT_CTR_COPIES x PT_CTR_STRIDE u64), summed by the host
 #define PT_CTR_COPIES 8u
-#define PT_CTR_STRIDE 16u
+#define PT_CTR_STRIDE 32u
 
 struct WaveParams {
     SceneView S;
@@ -157,6 +157,10 @@ struct WaveParams {
     uint32_t* yield_cq;
     uint32_t* yield_ctr;
     uint32_t side_flags;          // PT_SIDE_* test hooks of that launch (0 in every render)
+    // test hook (PT_TUNE drop=<site>): 1 + the hand-off site (PT_HO_*, include/pt.h) whose
+    // items are dropped instead of handed on -- their chains are lost, which the resolve
+    // must report (0 in every render)
+    uint32_t drop;
 };
 // k_wcoop beside a path round, test hooks (PT_TUNE side_late / handon): every workgroup
 // behaves as one that started after the round's end (takes nothing, hands every item on);
@@ -168,6 +172,12 @@ struct WaveParams {
 // ... test hook (PT_TUNE grow_late): that launch's odd workgroups behave as late ones
 // (stop at once and hand their untaken items on, through the intake order)
 #define PT_GROW_LATE 8u
+// ... test hook (PT_TUNE side_stop_now): the early launch stops after its first chain cycle
+// (every team then yields its chain to the next round's carry queue)
+#define PT_SIDE_STOP_NOW 16u
+// path rounds, test hook (PT_TUNE shade_hold): the shade wave shades nothing until every
+// query wave has left (in rounds with a budget), so all it shades goes through its flush
+#define PT_SHADE_HOLD 32u
 #define PT_ORDER_BUCKETS 256u
 
 // path engine geometry: PT_NQ query waves + 1 shade wave per workgroup; at most
@@ -241,8 +251,12 @@ struct ResolveParams {
                                   // samples done differ from `samples` (a lost chain; must be 0)
 };
 // statistics counter slots (per copy, PT_CTR_STRIDE u64) besides rays .. fallbacks_ray (0-7)
-// and the cooperative engine's share (8-10, 13)
-enum : uint32_t { CTR_SHORT = 11u, CTR_HANDON = 12u };
+// and the cooperative engine's share (8-10, 13); CTR_HO + PT_HO_*: the items handed on at
+// each hand-off site (include/pt.h PT_HO_*; DESIGN.md §4 "Hand-off sites")
+enum : uint32_t { CTR_SHORT = 11u, CTR_HANDON = 12u, CTR_HO = 16u };
+// the hand-off sites (include/pt.h PT_HO_*, which the host checks these against)
+enum : uint32_t { HO_SUSPEND = 0u, HO_FLUSH, HO_RINGOUT, HO_EXACT, HO_SIDE_TAKE, HO_SIDE_YIELD, HO_SIDE_HANDON,
+                  HO_GROW_YIELD, HO_GROW_HANDON, HO_N };
 
 }  // namespace pt
 

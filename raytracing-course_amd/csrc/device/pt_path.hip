@@ -247,8 +247,11 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 over = wpost >= budget;
             }
             if (over) {
-                // the round is over for this wave: suspend its running queries
-                if (active) {
+                // the round is over for this wave: suspend its running queries (hand-off site
+                // HO_SUSPEND; PT_TUNE drop=suspend loses them instead)
+                const WaveParams& K0 = karg<WaveParams>();
+                const bool drop = K0.drop == 1u + HO_SUSPEND;
+                if (active && !drop) {
                     const WaveParams& K = karg<WaveParams>();
                     const uint32_t k = wave_append(K.ctl + PT_CTL_SET * (1u - K.parity) + C_CARRY, true);
                     uint32_t* w = K.cq[1u - K.parity] + (size_t)k * K.carry_words;
@@ -259,7 +262,10 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                     K.st.rec[2u * slot] = lds_get(L.H, (uint32_t)q.cid);   // the chain leaves the workgroup
                 }
                 const uint32_t ns = (uint32_t)__popcll(__ballot(active));
-                if (lane_id() == 0u && ns) atomicSub(&L.resident, ns);
+                if (lane_id() == 0u && ns) {
+                    atomicSub(&L.resident, ns);
+                    atomicAdd(ctr_copy(K0.counters) + CTR_HO + HO_SUSPEND, (unsigned long long)ns);
+                }
                 pf.exit_budget();
                 break;
             }
@@ -455,11 +461,14 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
                 pf.query_done();
             } else if (q.phase == Q_EXACT) {
                 // rare: the exact stack DFS after this kernel; the chain leaves the workgroup
+                // (hand-off site HO_EXACT, counted with the fallbacks; PT_TUNE drop=exact)
                 const WaveParams& K = karg<WaveParams>();
-                const uint32_t k = atomicAdd(K.ctl + PT_CTL_SET * (1u - K.parity) + C_EXACT, 1u);
-                K.ex.ro[k] = F4{q.ray.o.x, q.ray.o.y, q.ray.o.z, u2f(slot)};
-                K.ex.rd[k] = F4{q.ray.d.x, q.ray.d.y, q.ray.d.z, u2f(k)};
-                K.st.rec[2u * slot] = lds_get(L.H, (uint32_t)q.cid);   // (k_wshade shades it from HBM)
+                if (K.drop != 1u + HO_EXACT) {
+                    const uint32_t k = atomicAdd(K.ctl + PT_CTL_SET * (1u - K.parity) + C_EXACT, 1u);
+                    K.ex.ro[k] = F4{q.ray.o.x, q.ray.o.y, q.ray.o.z, u2f(slot)};
+                    K.ex.rd[k] = F4{q.ray.d.x, q.ray.d.y, q.ray.d.z, u2f(k)};
+                    K.st.rec[2u * slot] = lds_get(L.H, (uint32_t)q.cid);   // (k_wshade shades it from HBM)
+                }
                 atomicAdd(&L.leaked, 1u);   // (its table entry stays taken for the round)
                 atomicSub(&L.resident, 1u);
                 active = false;
@@ -479,6 +488,7 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
         if (rays) atomicAdd(ctr + 0, (unsigned long long)rays);
         if (rays && P.S.n_planes) atomicAdd(ctr + 3, (unsigned long long)rays * P.S.n_planes);
         if (fallbacks) atomicAdd(ctr + 6, (unsigned long long)fallbacks);
+        if (fallbacks) atomicAdd(ctr + CTR_HO + HO_EXACT, (unsigned long long)fallbacks);
         if (init_exact) atomicAdd(ctr + 7, (unsigned long long)init_exact);
     }
     pf.store(P.wg_prof, rays);
@@ -500,6 +510,15 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
     // ended paths waiting for their fold (this wave's own queue: {slot | miss << 31, table entry})
     uint2* endq = P.endq + (size_t)blockIdx.x * PT_CMAX;
     uint32_t e_head = 0u, e_tail = 0u;
+    uint32_t nflush = 0u;             // chains flushed to the next round after the query waves left
+    if (karg<WaveParams>().side_flags & PT_SHADE_HOLD) {
+        // (test hook: the query waves of a round with a budget leave by themselves)
+        const WaveParams& K = karg<WaveParams>();
+        const uint32_t* in = K.ctl + PT_CTL_SET * K.parity;
+        const uint32_t n_total = K.pin ? K.pin_n : in[C_FRESH] + in[C_CARRY];
+        if (n_total > K.path_runend)
+            while (__builtin_amdgcn_readfirstlane(lds_read(L.qw_done)) != PT_NQ) __builtin_amdgcn_s_sleep(2);
+    }
     for (;;) {
         // published entries of the done rings (ring indices are compile-time: no scratch)
         uint32_t av[PT_NQ], total = 0u;
@@ -608,13 +627,15 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
         f_tail += gone;
         if (flush) {
             // no query wave left to take it: the next round's fresh queue (the chain leaves
-            // the workgroup with its pixel record)
+            // the workgroup with its pixel record; hand-off site HO_FLUSH, PT_TUNE drop=flush)
             const WaveParams& K = karg<WaveParams>();
-            const uint32_t k = wave_append(K.ctl + PT_CTL_SET * (1u - K.parity) + C_FRESH, emit);
-            if (emit) {
+            const bool keep = emit && K.drop != 1u + HO_FLUSH;
+            const uint32_t k = wave_append(K.ctl + PT_CTL_SET * (1u - K.parity) + C_FRESH, keep);
+            if (keep) {
                 push_ray(K, K.fq[1u - K.parity], k, ray, slot);
                 K.st.rec[2u * slot] = lds_get(L.H, cid);
             }
+            nflush += (uint32_t)__popcll(me);
             gone += (uint32_t)__popcll(me);
         } else {
             if (emit) {
@@ -642,11 +663,17 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
     if (P.progress && prog && lane == 0u)
         __hip_atomic_fetch_add(P.progress, (unsigned long long)prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // the ray ring's leftovers (no query wave takes from it any more) -> next round, with
-    // their pixel records
+    // their pixel records (hand-off site HO_RINGOUT, PT_TUNE drop=ringout)
     const uint32_t h = lds_read(L.rq_head);
-    for (uint32_t b = h; b < tail; b += 64u) {
+    if (lane == 0u && (nflush || tail != h)) {
+        unsigned long long* ctr = ctr_copy(P.counters);
+        if (nflush) atomicAdd(ctr + CTR_HO + HO_FLUSH, (unsigned long long)nflush);
+        if (tail != h) atomicAdd(ctr + CTR_HO + HO_RINGOUT, (unsigned long long)(tail - h));
+    }
+    const uint32_t ring_end = karg<WaveParams>().drop == 1u + HO_RINGOUT ? h : tail;
+    for (uint32_t b = h; b < ring_end; b += 64u) {
         const uint32_t i = b + lane;
-        const bool has = i < tail;
+        const bool has = i < ring_end;
         // (the append first: ring values held across its atomic would live in scratch)
         const uint32_t k = wave_append(out + C_FRESH, has);
         if (has) {

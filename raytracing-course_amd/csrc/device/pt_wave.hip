@@ -137,15 +137,19 @@ __global__ void __launch_bounds__(256) k_side_take(WaveParams P, uint32_t k, Ray
     const uint32_t j = blockIdx.x * 256u + threadIdx.x;
     const bool on = j < k;
     const uint32_t gi = on ? P.order[j] : 0u;
-    const bool carry = on && gi < n_carry;
+    // (hand-off site HO_SIDE_TAKE; PT_TUNE drop=side_take loses the items instead: the path
+    // round skips them all the same)
+    const bool keep = on && P.drop != 1u + HO_SIDE_TAKE;
+    wave_add_u64(ctr_copy(P.counters) + CTR_HO + HO_SIDE_TAKE, on ? 1ull : 0ull);
+    const bool carry = keep && gi < n_carry;
     const uint32_t kc = wave_append(side_ctl + C_CARRY, carry);
-    const uint32_t kf = wave_append(side_ctl + C_FRESH, on && !carry);
+    const uint32_t kf = wave_append(side_ctl + C_FRESH, keep && !carry);
     if (carry) {
         const uint32_t* w = P.cq[P.parity] + (size_t)gi * P.carry_words;
         uint32_t* d = side_carry + (size_t)kc * P.carry_words;
         *reinterpret_cast<Ray*>(d) = reinterpret_cast<const Query*>(w)->ray;
         d[sizeof(Query) / 4u] = w[sizeof(Query) / 4u];
-    } else if (on) {
+    } else if (keep) {
         const RayQ& F = P.fq[P.parity];
         const uint32_t fi = gi - n_carry;
         side.ro[kf] = F.ro[fi];

@@ -115,7 +115,7 @@ __device__ __forceinline__ bool qc_prim_hit(const SceneView& S, uint32_t i, cons
 // 3-waves-per-SIMD limit)
 // (no plane-test counter: every counted ray tests every plane, so the plane tests are the
 // rays x n_planes, formed in 64 bits at the end -- a 32-bit LDS count of them could wrap)
-enum : uint32_t { LC_RAYS = 0u, LC_NODES, LC_PTESTS, LC_SPARE, LC_AUX, LC_FALLB, LC_HANDED, LC_N = 8u };
+enum : uint32_t { LC_RAYS = 0u, LC_NODES, LC_PTESTS, LC_YIELD, LC_AUX, LC_FALLB, LC_HANDED, LC_N = 8u };
 __device__ __forceinline__ void lc_add(uint32_t* lc, uint32_t k, bool c, uint32_t w = 1u) {
     const unsigned long long m = __ballot(c);
     if (m && lane_id() == (uint32_t)__ffsll((long long)m) - 1u) atomicAdd(lc + k, (uint32_t)__popcll(m) * w);
@@ -640,7 +640,9 @@ k_wcoop(WaveParams P) {
     // to whole-wave teams) all but side_stop_n of this launch's work items ended
     // (the late-workgroup test hooks: a stop count of 0, so the loop holds no flag test)
     const bool late = (P.side_flags & PT_SIDE_LATE) || ((P.side_flags & PT_GROW_LATE) && (blockIdx.x & 1u));
-    const uint32_t stop_n = late ? 0u
+    // (test hook side_stop_now: no stop test before the first chain cycle, a stop count of 0 after it)
+    uint32_t skip_stop = (P.side_flags & PT_SIDE_STOP_NOW) ? 1u : 0u;
+    const uint32_t stop_n = late || skip_stop ? 0u
                             : !(P.side_flags & PT_STOP_GROW) ? P.side_stop_n
                             : n_total > P.side_stop_n ? n_total - P.side_stop_n : 0xffffffffu;
 #ifdef PT_CPROF
@@ -661,7 +663,9 @@ k_wcoop(WaveParams P) {
     px.R.saved_ok = 0u;
     px.nv = px.done = 0u;
     for (;;) {
-        if (P.side_stop) {
+        if (P.side_stop && skip_stop) {
+            skip_stop = 0u;
+        } else if (P.side_stop) {
             // beside a path round: once its workgroups have all finished, the chains leave at
             // this chain cycle's end (after the loop: the yield's registers stay out of it)
             uint32_t fin = 0u;
@@ -808,10 +812,14 @@ k_wcoop(WaveParams P) {
         // suspended query at its start, to the round's next carry queue (a resumed query is
         // not counted again: its ray was counted when first taken), its pixel state and the
         // current path's fold records to HBM (the path engine continues the path from there)
-        const uint32_t k = wave_append(P.yield_ctr, have && tl == 0u);
+        // (hand-off site HO_SIDE_YIELD, or HO_GROW_YIELD for the final launch's grow stop;
+        // PT_TUNE drop=side_yield / grow_yield loses them instead)
+        const bool drop = P.drop == 1u + ((P.side_flags & PT_STOP_GROW) ? HO_GROW_YIELD : HO_SIDE_YIELD);
+        lc_add(lc, LC_YIELD, have && tl == 0u);
+        const uint32_t k = wave_append(P.yield_ctr, have && tl == 0u && !drop);
         // (k < carry_cap always: the host sizes the stops to the carry queue; a yield past it
         // would be a lost chain, which the resolve reports, never a write past the queue)
-        if (have && tl == 0u && k < P.carry_cap) {
+        if (have && tl == 0u && !drop && k < P.carry_cap) {
             Query q;
             q_init_pre(ray, Pt, pid, pre, q);
             uint32_t* w = P.yield_cq + (size_t)k * P.carry_words;
@@ -865,8 +873,11 @@ k_wcoop(WaveParams P) {
             }
             lc_add(lc, LC_RAYS, on && gi >= n_carry);
             lc_add(lc, LC_HANDED, on);
-            const uint32_t k2 = wave_append(P.yield_ctr, on);
-            if (on && k2 < P.carry_cap) {
+            // (hand-off site HO_SIDE_HANDON, or HO_GROW_HANDON; PT_TUNE drop=side_handon /
+            // grow_handon: the items taken here are lost instead)
+            const bool keep = on && P.drop != 1u + ((P.side_flags & PT_STOP_GROW) ? HO_GROW_HANDON : HO_SIDE_HANDON);
+            const uint32_t k2 = wave_append(P.yield_ctr, keep);
+            if (keep && k2 < P.carry_cap) {
                 Query q;
                 q_init_pre(r, rp, rid, rpre, q);
                 uint32_t* w = P.yield_cq + (size_t)k2 * P.carry_words;
@@ -883,9 +894,11 @@ k_wcoop(WaveParams P) {
     if (lane == 0u) {
         unsigned long long* ctr = ctr_copy(P.counters);
         const uint32_t v[LC_N] = {lc[0], lc[1], lc[2], lc[3], lc[4], lc[5], lc[6], lc[7]};
-        const uint32_t to[LC_N] = {0u, 1u, 2u, 3u, 5u, 6u, CTR_HANDON, 0u};
+        const bool grow = (P.side_flags & PT_STOP_GROW) != 0u;
+        const uint32_t to[LC_N] = {0u, 1u, 2u, CTR_HO + (grow ? HO_GROW_YIELD : HO_SIDE_YIELD), 5u, 6u, CTR_HANDON, 0u};
         for (uint32_t k = 0; k < LC_HANDED + 1u; ++k)
             if (v[k]) atomicAdd(ctr + to[k], (unsigned long long)v[k]);
+        if (v[LC_HANDED]) atomicAdd(ctr + CTR_HO + (grow ? HO_GROW_HANDON : HO_SIDE_HANDON), (unsigned long long)v[LC_HANDED]);
         if (v[LC_RAYS] && P.S.n_planes) atomicAdd(ctr + 3, (unsigned long long)v[LC_RAYS] * P.S.n_planes);
         if (v[LC_RAYS]) atomicAdd(ctr + 8, (unsigned long long)v[LC_RAYS]);
         if (v[LC_NODES]) atomicAdd(ctr + 9, (unsigned long long)v[LC_NODES]);

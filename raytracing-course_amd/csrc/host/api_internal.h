@@ -136,9 +136,19 @@ uint64_t owned_pixels(const pt_session* ss);
 hipError_t read_counters(pt_session* ss, unsigned long long c[PT_CTR_STRIDE]);
 int flush_trace(pt_session* ss);
 int trace_wave(pt_session* ss, uint32_t spp);
+// the hand-off site named `name` (PT_HO_*: "suspend", "flush", "ringout", "exact", "side_take",
+// "side_yield", "side_handon", "grow_yield", "grow_handon"), or -1
+int handoff_site(const char* name);
 // a scene beyond the cooperative engine's LDS tables (RAY_DEPTH > QC_FOLD, more than
 // QC_NPL planes or QC_NEM emitters) runs its BIG instantiation
 bool coop_big(const pt_session* ss);
+
+static_assert(pt::HO_SUSPEND == PT_HO_SUSPEND && pt::HO_FLUSH == PT_HO_FLUSH && pt::HO_RINGOUT == PT_HO_RINGOUT &&
+                  pt::HO_EXACT == PT_HO_EXACT && pt::HO_SIDE_TAKE == PT_HO_SIDE_TAKE &&
+                  pt::HO_SIDE_YIELD == PT_HO_SIDE_YIELD && pt::HO_SIDE_HANDON == PT_HO_SIDE_HANDON &&
+                  pt::HO_GROW_YIELD == PT_HO_GROW_YIELD && pt::HO_GROW_HANDON == PT_HO_GROW_HANDON &&
+                  pt::HO_N == PT_HO_N && PT_HO_N <= 12 && pt::CTR_HO + PT_HO_N <= PT_CTR_STRIDE,
+              "hand-off sites: device and ABI numbering differ");
 
 }  // namespace pti
 

@@ -97,7 +97,12 @@ const Rccl& rccl() {
 //                     late ones (they hand their untaken items on through the intake order)
 //   side_stop_now=1   the early launch stops at its first chain cycle's end (every team yields
 //                     its chain to the next round's carry queue)
-//   yield_drop=1      ... and its yields drop the chain instead (lost chains: the resolve fails)
+//   shade_hold=1      path rounds with a budget: the shade wave shades nothing until every query
+//                     wave has left, so everything it shades is flushed to the next round
+//   drop=<site>       the items of one hand-off site (PT_HO_*: suspend, flush, ringout, exact,
+//                     side_take, side_yield, side_handon, grow_yield, grow_handon) are dropped
+//                     instead of handed on (lost chains: the resolve fails); pt_stats.handoff
+//                     counts every site's items
 //   cap=N             chains a workgroup may hold
 //   batch=N           round-queue entries a query wave takes per pull (1..64, default 32)
 //   lstack=N          aux stack words a path-engine query may use (default and maximum PT_LSTACK;
@@ -147,6 +152,14 @@ int tune_int(const char* key, int def) {
 int stats_level() {
     const char* e = getenv("PT_STATS");
     return e ? atoi(e) : 0;
+}
+
+int handoff_site(const char* name) {
+    static const char* names[PT_HO_N] = {"suspend", "flush", "ringout", "exact", "side_take",
+                                         "side_yield", "side_handon", "grow_yield", "grow_handon"};
+    for (int k = 0; k < PT_HO_N; ++k)
+        if (strcmp(name, names[k]) == 0) return k;
+    return -1;
 }
 
 unsigned prep_threads() { return std::max(1u, std::min(16u, std::thread::hardware_concurrency())); }

@@ -388,6 +388,7 @@ int pt_render(pt_scene* s, const pt_render_opts* opts, uint8_t* rgb, float* radi
         agg.aux_visits += st.aux_visits; agg.fallbacks += st.fallbacks;
         agg.fallbacks_ray += st.fallbacks_ray;
         agg.short_pixels += st.short_pixels; agg.handed_on += st.handed_on;
+        for (int k = 0; k < PT_HO_N; ++k) agg.handoff[k] += st.handoff[k];
         agg.isect_ms = std::max(agg.isect_ms, st.isect_ms);
         agg.isect_launches += st.isect_launches;
         agg.coop_rays += st.coop_rays; agg.coop_node_visits += st.coop_node_visits;

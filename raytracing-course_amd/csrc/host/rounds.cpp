@@ -78,6 +78,15 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     wp.batch = (uint32_t)std::min(64, std::max(1, tune_int("batch", 32)));
     wp.end_min = ss->mix[3];
     wp.lstack = std::min<uint32_t>(PT_LSTACK, (uint32_t)std::max(1, tune_int("lstack", (int)PT_LSTACK)));
+    // test hooks: PT_TUNE shade_hold=1 (path rounds: the shade wave waits for the query waves to
+    // leave), drop=<site> (the items of one hand-off site are lost: the resolve must fail)
+    wp.side_flags = tune_int("shade_hold", 0) ? PT_SHADE_HOLD : 0u;
+    wp.drop = 0u;
+    if (const std::string d = tune_str("drop"); !d.empty()) {
+        const int site = handoff_site(d.c_str());
+        if (site < 0) return fail(PT_E_INVALID, "PT_TUNE drop=" + d + ": no such hand-off site");
+        wp.drop = 1u + (uint32_t)site;
+    }
     if (ss->on_progress && !ss->prog_host) {
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ss->prog_host), 8, hipHostMallocMapped | hipHostMallocCoherent));
         *ss->prog_host = 0ull;
@@ -265,6 +274,7 @@ int trace_wave(pt_session* ss, uint32_t spp) {
                 sp.yield_cq = wp.cq[1u - p];
                 sp.yield_ctr = out + pt::C_CARRY;
                 sp.side_flags = (tune_int("side_late", 0) ? PT_SIDE_LATE : 0u) |
+                                (tune_int("side_stop_now", 0) ? PT_SIDE_STOP_NOW : 0u) |
                                 (tune_int("handon", 1) ? 0u : PT_SIDE_NO_HANDON);
                 hipEvent_t i0, i1;
                 HIP_TRY(hipEventCreate(&i0));

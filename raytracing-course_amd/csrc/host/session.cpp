@@ -595,6 +595,7 @@ int pt_session_stats(pt_session* ss, pt_stats* st) {
     st->coop_launches = ss->coop_launches;
     st->short_pixels = c[pt::CTR_SHORT];
     st->handed_on = c[pt::CTR_HANDON];
+    for (uint32_t k = 0; k < PT_HO_N; ++k) st->handoff[k] = c[pt::CTR_HO + k];
     return PT_OK;
 }
 

@@ -26,6 +26,9 @@ TRAVERSAL_REPLAY = 0
 TRAVERSAL_EXACT = 1
 TRAVERSAL_REPLAY_DIV = 2
 GATHER_AUTO, GATHER_RCCL, GATHER_HOST = 0, 1, 2
+# pt_stats.handoff sites, in PT_HO_* order (include/pt.h; PT_TUNE drop=<name>)
+HANDOFF_SITES = ("suspend", "flush", "ringout", "exact", "side_take", "side_yield", "side_handon", "grow_yield",
+                 "grow_handon")
 ABI_VERSION = 6
 
 # One HIP runtime per process: PyTorch bundles its own libamdhip64 (soname
@@ -67,10 +70,13 @@ class Stats(C.Structure):
                 ("rounds", C.c_uint64), ("gather_rccl", C.c_uint64),
                 ("coop_rays", C.c_uint64), ("coop_node_visits", C.c_uint64), ("coop_prim_tests", C.c_uint64),
                 ("coop_aux_visits", C.c_uint64), ("coop_ms", C.c_double), ("coop_launches", C.c_uint64),
-                ("short_pixels", C.c_uint64), ("handed_on", C.c_uint64), ("gather_allocs", C.c_uint64)]
+                ("short_pixels", C.c_uint64), ("handed_on", C.c_uint64), ("gather_allocs", C.c_uint64),
+                ("handoff", C.c_uint64 * 12)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["handoff"] = {name: int(self.handoff[i]) for i, name in enumerate(HANDOFF_SITES)}
+        return d
 
 
 class SessionOpts(C.Structure):

@@ -552,6 +552,54 @@ def test_lost_chains_fail_the_resolve(pt, monkeypatch):
             s.render()
 
 
+# Every place where work changes hands between the engines' launches, waves and queues
+# (DESIGN.md §4 "Hand-off sites"), with the PT_TUNE setting that makes it certainly run.
+# pt_stats.handoff counts each site's items where they change hands.
+HANDOFF_FORCE = {
+    "suspend": "coop=0,runend=0,budget=2",                      # path round end: running queries -> carry queue
+    "flush": "coop=0,runend=0,budget=2,shade_hold=1",          # shade wave after the query waves left -> fresh queue
+    "ringout": "coop=0,runend=0,budget=2",                     # ray-ring leftovers at the shade wave's exit
+    "exact": "coop=0,lstack=1",                         # path query -> k_wexact / k_wshade
+    "side_take": "coop=300,budget=2,early=1,early_at=100000000",                    # early launch's intake
+    "side_yield": "coop=300,budget=2,early=1,early_at=100000000,side_stop_now=1",   # its stop: yields
+    "side_handon": "coop=300,budget=2,early=1,early_at=100000000,early_wg=8,side_late=1",   # late workgroups
+    "grow_yield": "coop=100000000,coop_grow=100",        # final launch's grow stop: yields
+    "grow_handon": "coop=100000000,coop_order=1,coop_grow=1,grow_late=1",   # its late workgroups
+}
+
+
+@pytest.mark.parametrize("site", sorted(HANDOFF_FORCE))
+def test_handoff_site_runs_and_keeps_every_sample(pt, site, monkeypatch):
+    """Each hand-off site, forced: its items are counted (pt_stats.handoff > 0), no pixel
+    is short of its samples, and the bytes and radiance bits are the reference's."""
+    monkeypatch.setenv("PT_TUNE", HANDOFF_FORCE[site])
+    m, img, rad = U.golden_image("dragon_64x64x16")
+    with pt.Scene.load(U.golden_scene_path("dragon_64x64x16")) as s:
+        rgb, r, st = s.render(radiance=True)
+    assert st["handoff"][site] > 0, st["handoff"]
+    assert st["short_pixels"] == 0 and st["errors"] == 0
+    assert r.view(np.uint32).tolist() == rad.view(np.uint32).tolist()
+    assert np.array_equal(rgb, img)
+
+
+@pytest.mark.parametrize("site", sorted(HANDOFF_FORCE))
+def test_handoff_site_dropped_fails_the_resolve(pt, site, monkeypatch):
+    """The same site forced with its hand-on disabled (PT_TUNE drop=<site>: its items are
+    dropped, not handed on): the chains are lost, and pt_render must return the resolve's
+    lost-chain error (src/scene.cpp:192-199: every pixel takes exactly SAMPLES samples)."""
+    monkeypatch.setenv("PT_TUNE", HANDOFF_FORCE[site] + ",drop=" + site)
+    with pt.Scene.load(U.golden_scene_path("dragon_64x64x16")) as s:
+        with pytest.raises(pt.PTError, match="did not take exactly"):
+            s.render()
+
+
+def test_handoff_drop_names_are_checked(pt, monkeypatch):
+    monkeypatch.setenv("PT_TUNE", "drop=nowhere")
+    with pt.Scene.load(U.golden_scene_path("dragon_64x64x16")) as s:
+        with pytest.raises(pt.PTError, match="no such hand-off site"):
+            s.render()
+
+
 @pytest.mark.parametrize("mode", ["1", "2"])
 @pytest.mark.parametrize("bad", [0, 1, 2])
 def test_render_ngpu_failed_rank_returns(pt, mode, bad, monkeypatch):
