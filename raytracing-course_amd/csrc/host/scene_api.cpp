@@ -475,8 +475,8 @@ int pt_scene_prepare(pt_scene* s) {
     if (!s) return fail(PT_E_INVALID, "null scene");
     if (s->prepared) return PT_OK;
     try {
-        // PT_TUNE prepstats=1: per-stage times on stderr
-        const bool stats = tune_int("prepstats", 0) != 0;
+        // PT_TUNE prepstats=1 (or PT_STATS=3): per-stage times on stderr
+        const bool stats = tune_int("prepstats", 0) != 0 || stats_level() >= 3;
         auto tick = [stats, t = std::chrono::steady_clock::now()](const char* what) mutable {
             if (!stats) return;
             const auto n = std::chrono::steady_clock::now();
