@@ -30,7 +30,7 @@
 //     preorder; it replaces the plane hit iff strictly closer (scene.cpp:70-74).
 //
 // qc_run() is the same algorithm on one thread (host tests, PT_TUNE
-// qengine=coop in the self-tests); qc_wave() in pt_wave.hip is the wave form.
+// qengine=coop in the self-tests); qc_team() / qc_pool() in pt_wcoop.hip are the wave forms.
 #pragma once
 #include "pt_query.h"
 

@@ -65,7 +65,7 @@ struct TraceParams {
     unsigned long long* wg_prof;  // optional per-workgroup {start, end, HW_ID, XCC_ID} (diagnostics)
 };
 
-// ---- wavefront renderer (pt_wave.hip) ----------------------------------
+// ---- wavefront renderer (pt_wave.h: pt_wave.hip, pt_path.hip, pt_wcoop.hip) ----
 struct RayQ {                     // rays waiting for a closest-hit query
     F4* ro;                       // {o.xyz, u32 slot}
     F4* rd;                       // {d.xyz, P = closest plane t (computed by the producer)}
@@ -214,7 +214,7 @@ struct WaveParams {
 #define PT_CMAX 384u                   // (512 until round 3; the LDS pixel table took the room)
 #endif
 // The rings, the query lanes' aux stacks and the resident chains' pixel records
-// live in LDS (4 workgroups per CU; pt_wave.hip static_asserts the fit):
+// live in LDS (4 workgroups per CU; pt_path.hip static_asserts the fit):
 //   pixel table PT_CMAX entries (16 B: RNG, vertex count, samples done -- rec[2 slot]
 //              while the chain stays in the workgroup) and their free ring
 //   ray ring   PT_CMAX entries (54 B: ray, slot, plane t and prim, q_prep record, table entry)
@@ -226,7 +226,7 @@ struct WaveParams {
 #define PT_LSTACK 16u                  // (+1 word per lane: the stack's trash word)
 
 // cooperative engine (k_wcoop, the end of a pass): one wave per chain, QC_WAVES
-// independent waves per workgroup, per-wave LDS for the query (pt_wave.hip QcLds)
+// independent waves per workgroup, per-team and per-wave LDS for the query (pt_wcoop.hip QcTeamLds, QcPoolLds)
 #ifndef QC_WAVES
 #define QC_WAVES 4u
 #endif
@@ -267,7 +267,7 @@ hipError_t pt_launch_init(const pt::InitParams& p, uint32_t n_tiles, hipStream_t
 hipError_t pt_launch_spin(uint32_t us, uint32_t blocks, float* sink, hipStream_t s);
 // variant: bit 0 = filtered node tests + flat replay, bit 1 = XCD-banded tile order
 hipError_t pt_launch_trace(const pt::TraceParams& p, int variant, uint32_t lds_bytes, hipStream_t s);
-// wavefront pipeline (pt_wave.hip): start a pass (first camera ray of every
+// wavefront pipeline (pt_wave.hip, pt_path.hip, pt_wcoop.hip): start a pass (first camera ray of every
 // owned pixel), then path-engine rounds
 hipError_t pt_launch_wave_start(pt::WaveParams p, hipStream_t s);
 // path engine round: {k_wpath, k_wexact, k_wshade (exact results)}

@@ -46,7 +46,7 @@ namespace pt {
 //   w7: code (internal child node, 0x80000000 | reference leaf, 0xffffffff empty)
 // A reference leaf matters only if its own box is crossed (else it is never
 // entered) AND one of its primitives is hit, which can only happen inside its
-// hit region (host/api.cpp leaf_hit_region: a plain triangle is only ever hit
+// hit region (host/scene_api.cpp leaf_hit_region: a plain triangle is only ever hit
 // on its copy moved onto the plane through the origin, widened there for the
 // edge tests' rounding).  A subtree holds such a leaf only if the ray crosses
 // both the union of its own boxes and the union of its hit regions, so an entry

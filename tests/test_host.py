@@ -425,3 +425,15 @@ def test_coarse_binary16_aux_boxes_warn_and_stay_exact(tmp_path, capfd, k, d):
         got = {t: s.selftest_render_host(232, 200, 16, 16, spp=2, traversal=v) for t, v in TRAVERSALS.items()}
     assert got["replay"].view(np.uint32).tolist() == got["exact"].view(np.uint32).tolist()
     assert got["replay_div"].view(np.uint32).tolist() == got["exact"].view(np.uint32).tolist()
+
+
+def test_handoff_sites_mirror_the_abi():
+    """pt_stats.handoff's sites (include/pt.h PT_HO_*) in ptrace's order (HANDOFF_SITES, the
+    PT_TUNE drop=<name> names), and pt_stats.handoff wide enough for them."""
+    import re
+    hdr = open(os.path.join(U.REPO, "include", "pt.h")).read()
+    ids = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"PT_HO_([A-Z_]+) = (\d+)", hdr)}
+    n = ids.pop("n")
+    assert sorted(ids.values()) == list(range(n))
+    assert tuple(sorted(ids, key=ids.get)) == pt.HANDOFF_SITES
+    assert re.search(r"uint64_t handoff\[(\d+)\]", hdr).group(1) == str(dict(pt.Stats._fields_)["handoff"]._length_)
