@@ -367,8 +367,16 @@ def roofline(st0, st1, traffic_json, key):
            "rays_share": (d["rays"] - d["coop_rays"]) / max(d["rays"], 1),
            "alg_bytes_per_ray": alg_bytes * launches / max(d["rays"] - d["coop_rays"], 1)}
     if d["coop_launches"]:
+        # its algorithmic bytes (the same record sizes x its own visit counters) over its summed
+        # launch time (HIP events; the early launch runs beside path rounds, so this is the rate
+        # the cooperative teams drew while they ran, not an exclusive one)
+        cbytes = (d["coop_node_visits"] * st1["node_bytes"] + d["coop_prim_tests"] * st1["prim_bytes"] +
+                  d["coop_aux_visits"] * st1["aux_bytes"])
+        cach = cbytes / (d["coop_ms"] / 1e3) / 1e9 if d["coop_ms"] > 0 else 0.0
         rec["coop"] = {"kernel": "k_wcoop (end of pass)", "launches": d["coop_launches"], "ms": d["coop_ms"],
-                       "rays": d["coop_rays"], "mray_s": d["coop_rays"] / max(d["coop_ms"], 1e-9) / 1e3}
+                       "rays": d["coop_rays"], "mray_s": d["coop_rays"] / max(d["coop_ms"], 1e-9) / 1e3,
+                       "alg_bytes": cbytes, "alg_bytes_per_ray": cbytes / max(d["coop_rays"], 1),
+                       "achieved": cach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": cach / HBM_PEAK_GBS}
     prof = None
     try:
         prof = json.load(open(traffic_json)).get(key)

@@ -510,7 +510,6 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
     // ended paths waiting for their fold (this wave's own queue: {slot | miss << 31, table entry})
     uint2* endq = P.endq + (size_t)blockIdx.x * PT_CMAX;
     uint32_t e_head = 0u, e_tail = 0u;
-    uint32_t nflush = 0u;             // chains flushed to the next round after the query waves left
     if (karg<WaveParams>().side_flags & PT_SHADE_HOLD) {
         // (test hook: the query waves of a round with a budget leave by themselves)
         const WaveParams& K = karg<WaveParams>();
@@ -635,7 +634,8 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
                 push_ray(K, K.fq[1u - K.parity], k, ray, slot);
                 K.st.rec[2u * slot] = lds_get(L.H, cid);
             }
-            nflush += (uint32_t)__popcll(me);
+            // (counted here: a count carried through the loop would hold a register for its life)
+            if (lane == 0u && me) atomicAdd(ctr_copy(K.counters) + CTR_HO + HO_FLUSH, (unsigned long long)__popcll(me));
             gone += (uint32_t)__popcll(me);
         } else {
             if (emit) {
@@ -665,11 +665,7 @@ __device__ __forceinline__ void path_shade_wave(const WaveParams& P, PathLds& L)
     // the ray ring's leftovers (no query wave takes from it any more) -> next round, with
     // their pixel records (hand-off site HO_RINGOUT, PT_TUNE drop=ringout)
     const uint32_t h = lds_read(L.rq_head);
-    if (lane == 0u && (nflush || tail != h)) {
-        unsigned long long* ctr = ctr_copy(P.counters);
-        if (nflush) atomicAdd(ctr + CTR_HO + HO_FLUSH, (unsigned long long)nflush);
-        if (tail != h) atomicAdd(ctr + CTR_HO + HO_RINGOUT, (unsigned long long)(tail - h));
-    }
+    if (lane == 0u && tail != h) atomicAdd(ctr_copy(P.counters) + CTR_HO + HO_RINGOUT, (unsigned long long)(tail - h));
     const uint32_t ring_end = karg<WaveParams>().drop == 1u + HO_RINGOUT ? h : tail;
     for (uint32_t b = h; b < ring_end; b += 64u) {
         const uint32_t i = b + lane;

@@ -21,10 +21,11 @@ template <uint32_t T>
 struct QcTeamLds {
     // aux stack words per chain (also the leader's exact DFS stack): a whole-wave team's own;
     // smaller teams share their wave's pool (QcPoolLds), SCAP words per chain
-    static constexpr uint32_t SCAP = T == 64u ? 448u : T == 32u ? 192u : QC_SCAP_MIN;
+    // (teams of 4: 64, so that their wave's pool -- 16 chains -- stays at 1,024 words)
+    static constexpr uint32_t SCAP = T == 64u ? 448u : T == 32u ? 192u : T == 4u ? 64u : QC_SCAP_MIN;
     static constexpr uint32_t CCAP = 5u * T;                    // candidates (< T + 4 T at any time)
-    static constexpr uint32_t HCAP = T >= 32u ? 32u : T == 16u ? 16u : 12u;   // hitting leaves per query (more: the
-                                                                              // exact DFS); LDS fits 3 WGs per CU
+    static constexpr uint32_t HCAP = T >= 32u ? 32u : T == 16u ? 16u : T == 8u ? 12u : 8u;   // hitting leaves per
+                                    // query (more: the exact DFS); LDS fits 3 WGs per CU (teams of 4: 2)
     uint32_t stk[T == 64u ? SCAP : 1u];
     uint32_t cand[T == 64u ? CCAP : 1u];
     uint32_t hl[QH_N][HCAP];       // hitting leaves: index, first-min t, its prim, hit normal and side,
@@ -37,10 +38,12 @@ struct QcTeamLds {
                                    // owns it (touched at path ends only: registers would spill)
 };
 // per wave, teams of T < 64 (qc_pool): the chains' pending aux nodes and candidate
-// leaves, (chain << 29 | node / leaf ordinal) items, and each chain's ray
+// leaves, (chain << SH | node / leaf ordinal) items, and each chain's ray
 template <uint32_t T>
 struct QcPoolLds {
     static constexpr uint32_t CPW = 64u / T;                    // chains per wave
+    static constexpr uint32_t SH = CPW > 8u ? 28u : 29u;        // item = chain << SH | node (host: nodes < 2^SH)
+    static constexpr uint32_t MASK = (1u << SH) - 1u;
     static constexpr uint32_t SW = QcTeamLds<T>::SCAP * CPW;    // pending nodes (chain c's exact DFS stack after
                                                                 // the query: words [c SCAP, (c + 1) SCAP))
     static constexpr uint32_t CW = 128u;                        // candidates (< 64 + 64 at any time)
@@ -422,7 +425,7 @@ __device__ int qc_pool(const SceneView& S, const QcScene& Q, QcPoolLds<T>& W, Qc
     }
     // every running chain's root node
     const unsigned long long mr = __ballot(run && tl == 0u);
-    if (run && tl == 0u) W.stk[lanes_below(mr)] = team << 29;
+    if (run && tl == 0u) W.stk[lanes_below(mr)] = team << QcPoolLds<T>::SH;
     uint32_t ns = (uint32_t)__popcll(mr), nc = 0u;   // wave-uniform
     bool wovf = false;                               // the pool overflowed: every chain takes the exact DFS
     const uint32_t slim = SW - reserve;
@@ -435,14 +438,14 @@ __device__ int qc_pool(const SceneView& S, const QcScene& Q, QcPoolLds<T>& W, Qc
             const uint32_t take = nc < 64u ? nc : 64u;
             nc -= take;
             const uint32_t item = lane < take ? W.cand[nc + lane] : 0u;
-            const uint32_t ch = item >> 29;
+            const uint32_t ch = item >> QcPoolLds<T>::SH;
             const bool act = lane < take && W.ovf[ch] == 0u;
             const F4 q0 = W.ray[ch][0], q1 = W.ray[ch][1], q2 = W.ray[ch][2];
             Ray ir;
             ir.o = mk3(q0.x, q0.y, q0.z);
             ir.d = mk3(q1.x, q1.y, q1.z);
             const f3 iinv = mk3(q2.x, q2.y, q2.z);
-            const uint32_t ord = act ? item & 0x1fffffffu : 0u;
+            const uint32_t ord = act ? item & QcPoolLds<T>::MASK : 0u;
             const uint32_t bo = S.o_bundle + PT_BUNDLE_BYTES * ord;
             const F4 b0 = blob_piece(S, bo), b1 = blob_piece(S, bo + 16u), b2 = blob_piece(S, bo + 32u),
                      b3 = blob_piece(S, bo + 48u), b4 = blob_piece(S, bo + 64u), b5 = blob_piece(S, bo + 80u);
@@ -504,7 +507,7 @@ __device__ int qc_pool(const SceneView& S, const QcScene& Q, QcPoolLds<T>& W, Qc
         ns -= k;
         const uint32_t ni = lane / PT_AUXW, e = lane % PT_AUXW;
         const uint32_t item = ni < k ? W.stk[ns + ni] : 0u;
-        const uint32_t ch = item >> 29, node = item & 0x1fffffffu;
+        const uint32_t ch = item >> QcPoolLds<T>::SH, node = item & QcPoolLds<T>::MASK;
         const bool act = ni < k && W.ovf[ch] == 0u;
         lc_add(lc, LC_AUX, act && e == 0u);
         F4 ea, eb;
@@ -526,8 +529,8 @@ __device__ int qc_pool(const SceneView& S, const QcScene& Q, QcPoolLds<T>& W, Qc
         const bool leaf = h && (code & 0x80000000u) != 0u;
         const bool inner = h && (code & 0x80000000u) == 0u;
         const unsigned long long mi = __ballot(inner), ml = __ballot(leaf);
-        if (inner) W.stk[ns + lanes_below(mi)] = ch << 29 | code;
-        if (leaf) W.cand[nc + lanes_below(ml)] = ch << 29 | f2u(eb.z);   // (a leaf entry's range: its bundle)
+        if (inner) W.stk[ns + lanes_below(mi)] = ch << QcPoolLds<T>::SH | code;
+        if (leaf) W.cand[nc + lanes_below(ml)] = ch << QcPoolLds<T>::SH | f2u(eb.z);   // (a leaf entry's range: its bundle)
         ns += (uint32_t)__popcll(mi);
         nc += (uint32_t)__popcll(ml);
     }
@@ -640,9 +643,9 @@ k_wcoop(WaveParams P) {
     // to whole-wave teams) all but side_stop_n of this launch's work items ended
     // (the late-workgroup test hooks: a stop count of 0, so the loop holds no flag test)
     const bool late = (P.side_flags & PT_SIDE_LATE) || ((P.side_flags & PT_GROW_LATE) && (blockIdx.x & 1u));
-    // (test hook side_stop_now: no stop test before the first chain cycle, a stop count of 0 after it)
-    uint32_t skip_stop = (P.side_flags & PT_SIDE_STOP_NOW) ? 1u : 0u;
-    const uint32_t stop_n = late || skip_stop ? 0u
+    // (test hook side_stop_now: no stop test at the top; the loop leaves after its first chain cycle)
+    const uint32_t stop_n = (P.side_flags & PT_SIDE_STOP_NOW) ? 0xffffffffu
+                            : late ? 0u
                             : !(P.side_flags & PT_STOP_GROW) ? P.side_stop_n
                             : n_total > P.side_stop_n ? n_total - P.side_stop_n : 0xffffffffu;
 #ifdef PT_CPROF
@@ -663,9 +666,7 @@ k_wcoop(WaveParams P) {
     px.R.saved_ok = 0u;
     px.nv = px.done = 0u;
     for (;;) {
-        if (P.side_stop && skip_stop) {
-            skip_stop = 0u;
-        } else if (P.side_stop) {
+        if (P.side_stop) {
             // beside a path round: once its workgroups have all finished, the chains leave at
             // this chain cycle's end (after the loop: the yield's registers stay out of it)
             uint32_t fin = 0u;
@@ -716,12 +717,12 @@ k_wcoop(WaveParams P) {
                     px.nv = hot.nv;
                     px.done = hot.done;
                     if (tl == 0u) L.sum = P.st.rec[2u * slot + 1u];
-                    if (tl < hot.nv && (!BIG || tl < QC_FOLD)) {
-                        // the current path's vertices so far (written by the path engine; any
-                        // beyond QC_FOLD stay in HBM)
-                        const uint4 f = P.st.fold[(size_t)slot * P.st.depth + opaque_v(tl)];
-                        L.fold[tl] = f;
-                        L.fold_sh[tl] = P.S.shade[f.x & 0x3fffffffu];
+                    // the current path's vertices so far (written by the path engine; any
+                    // beyond QC_FOLD stay in HBM; teams of 4: a lane takes two)
+                    for (uint32_t v = tl; v < hot.nv && (!BIG || v < QC_FOLD); v += T) {
+                        const uint4 f = P.st.fold[(size_t)slot * P.st.depth + opaque_v(v)];
+                        L.fold[v] = f;
+                        L.fold_sh[v] = P.S.shade[f.x & 0x3fffffffu];
                     }
                 }
             }
@@ -801,6 +802,10 @@ k_wcoop(WaveParams P) {
 #endif
         }
         QC_TICK(4);
+        if (karg<WaveParams>().side_flags & PT_SIDE_STOP_NOW) {
+            stopped = true;
+            break;
+        }
         if (P.progress && prog >= 256u) {
             if (lane == 0u)
                 __hip_atomic_fetch_add(P.progress, (unsigned long long)prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -833,7 +838,7 @@ k_wcoop(WaveParams P) {
             P.st.rec[2u * slot + 1u] = L.sum;
         }
         const uint32_t nv = __shfl(px.nv, (int)tbase, 64);
-        if (have && tl < nv && (!BIG || tl < QC_FOLD)) P.st.fold[(size_t)slot * P.st.depth + tl] = L.fold[tl];
+        for (uint32_t v = tl; have && v < nv && (!BIG || v < QC_FOLD); v += T) P.st.fold[(size_t)slot * P.st.depth + v] = L.fold[v];
         have = false;
     }
     if (stopped && !(P.side_flags & PT_SIDE_NO_HANDON)) {
@@ -937,6 +942,7 @@ hipError_t pt_launch_coop(pt::WaveParams p, uint32_t grid, uint32_t team, bool b
         if (team == 64u) hipLaunchKernelGGL((pt::k_wcoop<64u, true>), dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
         else hipLaunchKernelGGL((pt::k_wcoop<8u, true>), dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
     } else if (team == 8u) hipLaunchKernelGGL((pt::k_wcoop<8u, false>), dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
+    else if (team == 4u) hipLaunchKernelGGL((pt::k_wcoop<4u, false>), dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
     else if (team == 16u) hipLaunchKernelGGL((pt::k_wcoop<16u, false>), dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
     else if (team == 32u) hipLaunchKernelGGL((pt::k_wcoop<32u, false>), dim3(grid), dim3(64u * QC_WAVES), 0, s, p);
     else hipLaunchKernelGGL((pt::k_wcoop<64u, false>), dim3(grid), dim3(64u * QC_WAVES), 0, s, p);

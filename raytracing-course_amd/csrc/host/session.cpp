@@ -204,10 +204,21 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         ss->coop_grid = cus * 8u;
         // (a depth-first descent below the expansion limit adds at most 3 entries per level)
         const uint32_t reserve = 3u * (s->auxsl_depth + 2u);
+        // a team size's stacks hold this tree: the expansion (its own stack, or for teams of 4
+        // the wave's pool of 1,024 words) a depth-first descent below the reserve, and the
+        // leader's exact DFS (its stack, or its 64-word slice of the pool) the whole tree
+        // (and for teams below 64 the pool's items, chain << 29 | node -- teams of 4: << 28 -- hold
+        // every aux entry index)
+        auto team_ok = [&](uint32_t t) {
+            if (t < 64u && s->auxsl.size() >= (1ull << (t == 4u ? 28 : 29))) return false;
+            if (t == 4u) return 1024u >= reserve + 64u && s->max_stack <= 64u;
+            const uint32_t scap = t == 64u ? 448u : t == 32u ? 192u : QC_SCAP_MIN;
+            return scap >= reserve + 64u && s->max_stack <= scap;
+        };
         ss->coop_team = (uint32_t)tune_int("coop_team", (int)ss->coop_team);
-        if (ss->coop_team != 8u && ss->coop_team != 16u && ss->coop_team != 32u) ss->coop_team = 64u;
-        const uint32_t scap = ss->coop_team == 64u ? 448u : ss->coop_team == 32u ? 192u : QC_SCAP_MIN;
-        if (scap < reserve + 64u || s->max_stack > scap) ss->coop_team = 64u;   // deep trees: whole-wave teams
+        if (ss->coop_team != 4u && ss->coop_team != 8u && ss->coop_team != 16u && ss->coop_team != 32u)
+            ss->coop_team = 64u;
+        if (!team_ok(ss->coop_team)) ss->coop_team = 64u;   // deep trees: whole-wave teams
         // (paths deeper than QC_FOLD keep their further fold records in HBM, planes and
         // emitters beyond QC_NPL / QC_NEM come from HBM: no scene limit besides the stacks)
         if (448u < reserve + 64u || s->max_stack > 448u)
@@ -239,9 +250,8 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         const bool big = coop_big(ss);
         {
             const int st = tune_int("side_team", 8);
-            ss->side_team = !big && (st == 16 || st == 32 || st == 64) ? (uint32_t)st : 8u;
-            if (ss->side_team == 32u && (192u < reserve + 64u || s->max_stack > 192u)) ss->side_team = 8u;
-            if (ss->side_team == 64u && (448u < reserve + 64u || s->max_stack > 448u)) ss->side_team = 8u;
+            ss->side_team = !big && (st == 4 || st == 16 || st == 32 || st == 64) ? (uint32_t)st : 8u;
+            if (!team_ok(ss->side_team)) ss->side_team = 8u;
         }
         if (ss->early_k == 1u) ss->early_k = cus * ss->early_wg * QC_WAVES * (64u / ss->side_team);   // early=1: what it holds
         if (!ss->coop_max || ss->coop_team != 8u) ss->early_k = 0;

@@ -153,11 +153,11 @@ def test_device_init(pt):
     assert pt._lib.pt_device_init(4096) == pt.PT_E_NO_GPU
 
 
-@pytest.mark.parametrize("engine", ["coop64", "coop32", "coop16", "coop8", "coop8grow", "path"])
+@pytest.mark.parametrize("engine", ["coop64", "coop32", "coop16", "coop8", "coop4", "coop8grow", "path"])
 @pytest.mark.parametrize("name", sorted(M["images"]))
 def test_golden_images_each_engine(pt, name, engine, monkeypatch):
     """The replay traversal with one engine for the whole pass: the cooperative
-    engine (a team of 64, 32 or 16 lanes per chain: breadth-first aux expansion,
+    engine (a team of 64, 32, 16, 8 or 4 lanes per chain: breadth-first aux expansion,
     all candidate leaves at once, root paths a block of nodes per round;
     pt_coop.h) or the path engine alone (coop=0).  All must reproduce the
     reference's bytes and ray count.  coop8grow: teams of 8 that hand their last 64
@@ -181,7 +181,7 @@ def test_golden_images_each_engine(pt, name, engine, monkeypatch):
         assert st["rounds"] in ((1, 2) if grow else (1,))
 
 
-@pytest.mark.parametrize("team", ["64", "16", "8", "8grow"])
+@pytest.mark.parametrize("team", ["64", "16", "8", "4", "8grow"])
 @pytest.mark.parametrize("cfg", ["c1", "c2"])
 def test_coop_engine_full_config_md5(pt, cfg, team, monkeypatch):
     """Configs 1 and 2 entirely on the cooperative engine: reference md5 and ray count
@@ -483,7 +483,8 @@ TUNE_KEYS = ["wg_per_cu=2", "wg_per_cu=1", "runend=1000000", "sparse_steps=2", "
              # every early workgroup a late one (side_late), the side stream at each priority
              "coop=300,early=1,early_at=100000000,side_late=1",
              "coop=300,early=1,early_at=100000000,side_prio=0", "coop=300,early=1,early_at=100000000,side_prio=2",
-             "coop=300,early=1,early_at=100000000,side_team=16",
+             "coop=300,early=1,early_at=100000000,side_team=16", "coop=300,early=1,early_at=100000000,side_team=4",
+             "coop=300,coop_team=4",
              # diagnostics hooks (their counters are compiled in only with -DPT_CPROF / -DPT_WPROF;
              # the host side runs in every build)
              "coop=300,cprof=1", "wgprof=/tmp/pt_wgprof_test.bin"]

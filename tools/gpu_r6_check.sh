@@ -12,7 +12,7 @@ if [ "${BENCH:-1}" = "1" ]; then
   timeout -k 10 900 python bench.py --steps ${STEPS:-20} --warmup ${WARMUP:-5} ${BENCH_ARGS:-} > $O/bench.json 2> $O/bench.err || { echo BENCH_FAIL; tail -20 $O/bench.err; exit 1; }
   python3 -c "
 import json; d=json.load(open('$O/bench.json')); w=d.get('wall_to_ppm') or {}; r=d['roofline']; c=d.get('cpu_baseline') or {}
-print('BENCH', round(d['value']), round(d['ms_per_step'],2), round(r['frac'],3), r.get('coop'), 'r256', d.get('render_256spp_mray_s'), d.get('render_256spp_wall_mray_s'), 'ppm_s', w.get('seconds'), 'teardown', w.get('teardown_s'), 'fb=cli', d.get('framebuffer_equals_cli_ppm'), 'cpu', c.get('value'), (c.get('configs') or {}).get('c3', {}).get('render_s'))"
+print('BENCH', round(d['value']), round(d['ms_per_step'],2), round(r['frac'],3), {k: (round(v,3) if isinstance(v,float) else v) for k,v in (r.get('coop') or {}).items()}, 'r256', d.get('render_256spp_mray_s'), d.get('render_256spp_wall_mray_s'), 'ppm_s', w.get('seconds'), 'teardown', w.get('teardown_s'), 'fb=cli', d.get('framebuffer_equals_cli_ppm'), 'cpu', c.get('value'), (c.get('configs') or {}).get('c3', {}).get('render_s'))"
 fi
 if [ "${DIST:-0}" = "1" ]; then
   for sc in strong weak; do
