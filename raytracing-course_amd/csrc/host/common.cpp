@@ -66,7 +66,7 @@ const Rccl& rccl() {
 //                     the step mix of rounds that start with fewer than N chains (default
 //                     768 per CU; the mix of the other rounds, except lowq_end_min: 48)
 //   lowq_wg=N         ... and their path workgroups per CU (PT_CMAX chains each; default 2)
-//   coop_team=T       lanes per chain in the cooperative engine (8, 16, 32, 64)
+//   coop_team=T       lanes per chain in the cooperative engine (8 default, 4, 16, 32, 64)
 //   coop_grow=N       the final cooperative launch (teams of 8) hands its last N chains to a launch
 //                     of whole-wave teams (default: 16 per CU; 0 = never; at most the carry queue)
 //   coop_grow_mid=N   ... and, before that, its last N chains to teams of 32 (default 0: no such stage)
@@ -77,7 +77,7 @@ const Rccl& rccl() {
 //                     its K heaviest chains (1: what W cooperative workgroups per CU hold) in a
 //                     cooperative launch on a second stream beside it; the launch hands its chains
 //                     back when the round's path workgroups finish (default: 1; 0 = off)
-//   side_team=T       that launch's teams of T lanes: 8 (default), 16, 32 or 64
+//   side_team=T       that launch's teams of T lanes: 4 (default), 8, 16, 32 or 64
 //   side_prio=0|1|2   that launch's stream: 0 normal priority (may share a main stream's
 //                     hardware queue), 1 the greatest priority (a queue pool of its own; default),
 //                     2 a CU-masked stream over every CU (always a queue of its own); take_stream

@@ -245,16 +245,19 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         ss->early_wg = (uint32_t)std::max(1, tune_int("early_wg", 1));
         ss->early_at = (uint32_t)std::max(0, tune_int("early_at", (int)(cus * 768u)));
         ss->early_k = (uint32_t)std::max(0, tune_int("early", 1));
-        // lanes per chain of that launch: 8 (default) or 16 (half the chains, a shorter chain cycle)
+        // lanes per chain of that launch: 4 (default: 16 chains per wave, its pooled query keeps
+        // a wave's lanes busy with half as many lanes per chain; rank 0 of 8 73.5-75.2 ms against
+        // 76.4-83.1 with teams of 8, of 4 130.4-132.0 against 131.1-133.7, of 1 472-476 against
+        // 476-480: profiles/r06_coop/team4), 8, 16, 32 or 64
         // (a scene beyond the LDS tables has only the teams-of-8 BIG instantiation)
         const bool big = coop_big(ss);
         {
-            const int st = tune_int("side_team", 8);
+            const int st = tune_int("side_team", 4);
             ss->side_team = !big && (st == 4 || st == 16 || st == 32 || st == 64) ? (uint32_t)st : 8u;
-            if (!team_ok(ss->side_team)) ss->side_team = 8u;
+            if (!team_ok(ss->side_team)) ss->side_team = team_ok(8u) ? 8u : 64u;
         }
         if (ss->early_k == 1u) ss->early_k = cus * ss->early_wg * QC_WAVES * (64u / ss->side_team);   // early=1: what it holds
-        if (!ss->coop_max || ss->coop_team != 8u) ss->early_k = 0;
+        if (!ss->coop_max || (ss->coop_team != 8u && ss->coop_team != 4u) || ss->side_team == 64u) ss->early_k = 0;
         // a round's carry output also takes the early launch's yielded chains
         ss->carry_cap = (uint32_t)std::min<uint64_t>(n, (uint64_t)ss->lane_cap + ss->early_k);
         {

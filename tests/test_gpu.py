@@ -483,7 +483,7 @@ TUNE_KEYS = ["wg_per_cu=2", "wg_per_cu=1", "runend=1000000", "sparse_steps=2", "
              # every early workgroup a late one (side_late), the side stream at each priority
              "coop=300,early=1,early_at=100000000,side_late=1",
              "coop=300,early=1,early_at=100000000,side_prio=0", "coop=300,early=1,early_at=100000000,side_prio=2",
-             "coop=300,early=1,early_at=100000000,side_team=16", "coop=300,early=1,early_at=100000000,side_team=4",
+             "coop=300,early=1,early_at=100000000,side_team=16", "coop=300,early=1,early_at=100000000,side_team=8",
              "coop=300,coop_team=4",
              # diagnostics hooks (their counters are compiled in only with -DPT_CPROF / -DPT_WPROF;
              # the host side runs in every build)
