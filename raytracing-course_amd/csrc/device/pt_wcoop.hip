@@ -806,6 +806,18 @@ k_wcoop(WaveParams P) {
             stopped = true;
             break;
         }
+        // (the wave's 32-bit visit counters go to the 64-bit statistics before they could wrap:
+        // a chain cycle adds far less than 2^31)
+        if (lane == 0u && (lc[LC_NODES] | lc[LC_PTESTS] | lc[LC_AUX]) >= 0x80000000u) {
+            unsigned long long* ctr = ctr_copy(karg<WaveParams>().counters);
+            atomicAdd(ctr + 9, (unsigned long long)lc[LC_NODES]);
+            atomicAdd(ctr + 1, (unsigned long long)lc[LC_NODES]);
+            atomicAdd(ctr + 10, (unsigned long long)lc[LC_PTESTS]);
+            atomicAdd(ctr + 2, (unsigned long long)lc[LC_PTESTS]);
+            atomicAdd(ctr + 13, (unsigned long long)lc[LC_AUX]);
+            atomicAdd(ctr + 5, (unsigned long long)lc[LC_AUX]);
+            lc[LC_NODES] = lc[LC_PTESTS] = lc[LC_AUX] = 0u;
+        }
         if (P.progress && prog >= 256u) {
             if (lane == 0u)
                 __hip_atomic_fetch_add(P.progress, (unsigned long long)prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
