@@ -429,12 +429,14 @@ __device__ __forceinline__ void path_query_wave(const WaveParams& P, PathLds& L,
             if (turn) ptrip = 0u;
             if (want_probe && !probe_go) kind = 7u;
             pf.kinds(kind == 0u, pick != 0u, kind == 0u || kind == pick);
+            pf.kind_mix(kind == 0u ? ((q.node & PT_LEAFQ) ? 1u : 0u) : kind == pick ? kind + 1u : 7u);
             if (kind == 0u || kind == pick) q_step(P.S, q, C, stk);
             // aux_extra more aux-node steps in the same trip for the lanes whose next step is one
 #pragma unroll 1
             for (uint32_t x = 0; x < P.aux_extra; ++x) {
                 const bool a2 = active && q.phase == Q_AUX && !(q.node & PT_LEAFQ);
                 if (__ballot(a2) == 0ull) break;
+                pf.extra_aux((uint32_t)__popcll(__ballot(a2)));
                 if (a2) q_aux_step(P.S, q, C, stk);
             }
         }

@@ -16,6 +16,9 @@ struct QProf {
     uint64_t t0, s0 = 0, s1 = 0;
     uint64_t qlat = 0, qn = 0, qsteps = 0, qstart = 0;   // per lane
     uint32_t qs = 0;
+    // per step kind (0 aux node, 1 probe, 2 leaf check, 3 walk entries, 4 walk nodes): times its
+    // code was issued for the wave, and the lanes that used it
+    uint64_t kiss[5] = {0, 0, 0, 0, 0}, klanes[5] = {0, 0, 0, 0, 0};
     __device__ QProf() : t0(__builtin_amdgcn_s_memtime()) {}
     // (LL = PathLds; read through volatile generic pointers, diagnostics only)
     template <class LL>
@@ -44,6 +47,21 @@ struct QProf {
         if (__ballot(aux_lane) != 0ull) auxtrips++;
         if (pick) picktrips++;
         stepped += (uint64_t)__popcll(__ballot(stepped_lane));
+    }
+    // cat: this lane's step kind in the trip's step (> 4: none)
+    __device__ void kind_mix(uint32_t cat) {
+        for (uint32_t k = 0; k < 5u; ++k) {
+            const unsigned long long m = __ballot(cat == k);
+            if (m) {
+                kiss[k]++;
+                klanes[k] += (uint64_t)__popcll(m);
+            }
+        }
+    }
+    // an extra aux-node step of the same trip, for n lanes
+    __device__ void extra_aux(uint32_t n) {
+        kiss[0]++;
+        klanes[0] += n;
     }
     __device__ void step_end() {
         s1 = __builtin_amdgcn_s_memtime();
@@ -78,6 +96,11 @@ struct QProf {
             atomicAdd(w + 24, picktrips);
             atomicAdd(w + 25, stepped);
             atomicAdd(w + 26, donecyc);
+            const uint32_t ki[5] = {37u, 38u, 39u, 44u, 45u};
+            for (uint32_t k = 0; k < 5u; ++k) {
+                atomicAdd(w + ki[k], kiss[k]);
+                atomicAdd(w + 59u + k, klanes[k]);
+            }
         }
         wave_add_u64(w + 17, qlat);
         wave_add_u64(w + 18, qn);
@@ -129,6 +152,8 @@ struct QProf {
     __device__ void sleep() {}
     __device__ void refill_end(bool) {}
     __device__ void kinds(bool, bool, uint32_t) {}
+    __device__ void kind_mix(uint32_t) {}
+    __device__ void extra_aux(uint32_t) {}
     __device__ void step_end() {}
     __device__ void query_done() {}
     __device__ void done_end() {}

@@ -42,3 +42,10 @@ if tot[54:59].sum():
     print("QW exec by step kind (cycles per trip with that kind, share of trips): " + "; ".join(
         "%s %.0f (%.2f)" % (n, tot[48 + i] / max(tot[54 + i], 1), tot[54 + i] / max(tot[2] - tot[4], 1)) for i, n in enumerate(names))
         + "; before the first kind %.0f per stepping trip" % (tot[53] / max(tot[2] - tot[4], 1)))
+if tot[[37, 38, 39, 44, 45]].sum():
+    names = ["aux node", "probe", "leaf check", "walk entries", "walk nodes"]
+    iss = tot[[37, 38, 39, 44, 45]]
+    print("QW step kinds (-DPT_WPROF): issues per stepping trip / mean lanes per issue: " + "; ".join(
+        "%s %.3f / %.1f" % (n, iss[i] / max(tot[2] - tot[4], 1), tot[59 + i] / max(iss[i], 1)) for i, n in enumerate(names))
+        + "; all kinds: %.2f issues per trip, %.1f lanes per issue" % (iss.sum() / max(tot[2] - tot[4], 1),
+                                                                     tot[59:64].sum() / max(iss.sum(), 1)))
