@@ -569,11 +569,18 @@ HANDOFF_FORCE = {
 }
 
 
-@pytest.mark.parametrize("site", sorted(HANDOFF_FORCE))
-def test_handoff_site_runs_and_keeps_every_sample(pt, site, monkeypatch):
+# every site with the defaults, the early launch's sites also with teams of 8 (the default is 4)
+# and the final launch's with teams of 4 (the default is 8)
+HANDOFF_CASES = [(k, "") for k in sorted(HANDOFF_FORCE)] + \
+    [(k, ",side_team=8") for k in sorted(HANDOFF_FORCE) if k.startswith("side_")] + \
+    [(k, ",coop_team=4") for k in sorted(HANDOFF_FORCE) if k.startswith("grow_")]
+
+
+@pytest.mark.parametrize("site,team", HANDOFF_CASES)
+def test_handoff_site_runs_and_keeps_every_sample(pt, site, team, monkeypatch):
     """Each hand-off site, forced: its items are counted (pt_stats.handoff > 0), no pixel
     is short of its samples, and the bytes and radiance bits are the reference's."""
-    monkeypatch.setenv("PT_TUNE", HANDOFF_FORCE[site])
+    monkeypatch.setenv("PT_TUNE", HANDOFF_FORCE[site] + team)
     m, img, rad = U.golden_image("dragon_64x64x16")
     with pt.Scene.load(U.golden_scene_path("dragon_64x64x16")) as s:
         rgb, r, st = s.render(radiance=True)
@@ -583,12 +590,12 @@ def test_handoff_site_runs_and_keeps_every_sample(pt, site, monkeypatch):
     assert np.array_equal(rgb, img)
 
 
-@pytest.mark.parametrize("site", sorted(HANDOFF_FORCE))
-def test_handoff_site_dropped_fails_the_resolve(pt, site, monkeypatch):
+@pytest.mark.parametrize("site,team", HANDOFF_CASES)
+def test_handoff_site_dropped_fails_the_resolve(pt, site, team, monkeypatch):
     """The same site forced with its hand-on disabled (PT_TUNE drop=<site>: its items are
     dropped, not handed on): the chains are lost, and pt_render must return the resolve's
     lost-chain error (src/scene.cpp:192-199: every pixel takes exactly SAMPLES samples)."""
-    monkeypatch.setenv("PT_TUNE", HANDOFF_FORCE[site] + ",drop=" + site)
+    monkeypatch.setenv("PT_TUNE", HANDOFF_FORCE[site] + team + ",drop=" + site)
     with pt.Scene.load(U.golden_scene_path("dragon_64x64x16")) as s:
         with pytest.raises(pt.PTError, match="did not take exactly"):
             s.render()
