@@ -608,8 +608,9 @@ __device__ __forceinline__ bool coop_shade(const WaveParams& P, const QcScene& Q
 // BIG: a scene beyond the LDS tables (RAY_DEPTH > QC_FOLD, more than QC_NPL planes
 // or QC_NEM emitters): the rest of them from HBM (a separate instantiation, so the
 // common case carries none of that code)
+// (teams of 4: 70 KB of LDS per workgroup, 2 per CU, so 2 waves per SIMD)
 template <uint32_t T, bool BIG>
-__global__ void __launch_bounds__(64u * QC_WAVES) __attribute__((amdgpu_waves_per_eu(QC_WAVES_PER_EU, QC_WAVES_PER_EU)))
+__global__ void __launch_bounds__(64u * QC_WAVES) __attribute__((amdgpu_waves_per_eu(T == 4u ? 2u : QC_WAVES_PER_EU, T == 4u ? 2u : QC_WAVES_PER_EU)))
 k_wcoop(WaveParams P) {
     __shared__ QcTeamLds<T> Ls[QC_WAVES * (64u / T)];
     __shared__ QcPoolLds<T> Pool[T < 64u ? QC_WAVES : 1u];   // (teams of T < 64: the wave's query pool)
