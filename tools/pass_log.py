@@ -6,7 +6,8 @@ render sees it) for ONE coalesced pass of --spp samples (the metric's job: every
 pixel 256 spp), after one warm-up pass, under PT_TUNE roundlog=<level> (plus --tune):
 each round's chains in and out, its kind (full / low, +side for an early
 cooperative launch), wall ms and rays, and at level 3 the unfinished pixels'
-remaining samples.  Prints the log lines of the timed pass and one JSON summary.
+remaining samples.  Prints the log lines of the timed pass and one JSON summary
+(--first: also the process's first pass, whose code and buffers are cold).
   python tools/pass_log.py [--config c3] [--world 8] [--rank 0] [--spp 256] [--level 2]
 """
 import argparse
@@ -35,8 +36,8 @@ def child(a):
             dt = time.perf_counter() - t0
             st = ss.stats()
             print("PASS_END %d" % it, file=sys.stderr, flush=True)
-            if it == 1:
-                print(json.dumps({"world": a.world, "rank": a.rank, "spp": a.spp, "pass_ms": dt * 1e3,
+            if it == 1 or a.first:
+                print(json.dumps({"pass": it, "world": a.world, "rank": a.rank, "spp": a.spp, "pass_ms": dt * 1e3,
                                   "rays": st["rays"], "mray_s": st["rays"] / dt / 1e6, "rounds": st["rounds"],
                                   "coop_ms": st["coop_ms"], "coop_launches": st["coop_launches"],
                                   "coop_rays": st["coop_rays"], "isect_ms": st["isect_ms"],
@@ -52,6 +53,7 @@ def main():
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--level", type=int, default=2)
     ap.add_argument("--tune", default="")
+    ap.add_argument("--first", action="store_true", help="also the first (cold) pass of the process")
     ap.add_argument("--child", action="store_true")
     a = ap.parse_args()
     if a.child:
@@ -64,6 +66,9 @@ def main():
         sys.stderr.write(r.stderr[-2000:])
         sys.exit(r.returncode)
     lines = r.stderr.splitlines()
+    if a.first:
+        for ln in lines[lines.index("PASS_START 0") + 1:lines.index("PASS_END 0")]:
+            print("pass0 " + ln)
     i0 = lines.index("PASS_START 1")
     i1 = lines.index("PASS_END 1")
     for ln in lines[i0 + 1:i1]:
