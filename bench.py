@@ -417,7 +417,7 @@ def roofline(st0, st1, traffic_json, key):
 
 def kernel_resources():
     """the compiler's resource report of the path engine's two instantiations and the
-    cooperative engine's default one (teams of 8; tools/kernel_resources.py)"""
+    cooperative engine's two small-team ones (teams of 4, the default, and 8; tools/kernel_resources.py)"""
     try:
         import kernel_resources as KR
         ks = KR.kernel("k_wpath")
@@ -425,6 +425,8 @@ def kernel_resources():
         for k, v in KR.kernel("k_wcoop").items():
             if "ILj8ELb0" in k:
                 out["coop_team8"] = v
+            if "ILj4ELb0" in k:
+                out["coop_team4"] = v
         return out
     except Exception:
         return None

@@ -226,8 +226,10 @@ struct pt_session {
     hipError_t side_rc = hipSuccess;
     uint32_t coop_grow = 0;       // the final launch's last chains handed to whole-wave teams (0: never)
     uint32_t coop_grow_mid = 0;   // ... and an earlier stage of teams of 32 (0: none)
-    uint32_t coop_team = 8;       // lanes per chain in the cooperative engine (pure-coop rate, teams of
-                                  // 64 / 32 / 16 / 8: 283 / 392 / 572 / 815 Mray/s)
+    uint32_t coop_team = 4;       // lanes per chain in the cooperative engine (pure-coop rate, teams of
+                                  // 64 / 32 / 16 / 8: 283 / 392 / 572 / 815 Mray/s; the final launch in
+                                  // teams of 4 against 8, rank 0 of 1 / 8: 475.9 / 74.7 ms against
+                                  // 476.3 / 79.2, means of 5 interleaved runs, profiles/r06_coop/team4)
     // every device buffer below lives in one allocation (pt_session_create)
     unsigned char* arena = nullptr;
     size_t arena_bytes = 0;

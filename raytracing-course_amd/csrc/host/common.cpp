@@ -66,8 +66,8 @@ const Rccl& rccl() {
 //                     the step mix of rounds that start with fewer than N chains (default
 //                     768 per CU; the mix of the other rounds, except lowq_end_min: 48)
 //   lowq_wg=N         ... and their path workgroups per CU (PT_CMAX chains each; default 2)
-//   coop_team=T       lanes per chain in the cooperative engine (8 default, 4, 16, 32, 64)
-//   coop_grow=N       the final cooperative launch (teams of 8) hands its last N chains to a launch
+//   coop_team=T       lanes per chain in the cooperative engine (4 default, 8, 16, 32, 64)
+//   coop_grow=N       the final cooperative launch (teams of 4) hands its last N chains to a launch
 //                     of whole-wave teams (default: 16 per CU; 0 = never; at most the carry queue)
 //   coop_grow_mid=N   ... and, before that, its last N chains to teams of 32 (default 0: no such stage)
 //   coop_order=0      the pass's final cooperative launch takes its chains in queue order (default:

@@ -1,7 +1,7 @@
 // rounds.cpp -- the wavefront pass of a session (trace_wave): k_wcamera seeds it,
 // path rounds (k_wpath -> k_wexact -> k_wshade) run until the chains are few, the
 // early cooperative launch runs beside the low-chain rounds on the side stream, and
-// the final cooperative launch (teams of 8, then whole-wave teams) runs the rest to
+// the final cooperative launch (teams of 4, then whole-wave teams) runs the rest to
 // the end of the pass.  DESIGN.md §4 describes each step.
 #include <stdio.h>
 #include <string.h>
@@ -120,14 +120,14 @@ int trace_wave(pt_session* ss, uint32_t spp) {
     for (uint32_t guard = 0;; ++guard) {
         if (chains <= ss->coop_max) {
             // The cooperative engine runs every remaining chain to the end of the pass.  A
-            // launch of teams of 8 (the default) stops once all but ss->coop_grow of its chains
+            // launch of teams of 4 (the default) stops once all but ss->coop_grow of its chains
             // have ended and hands those -- the pass's slowest, whose chain cycle sets the
             // launch's end -- to a launch of whole-wave teams (the shortest cycle).
             // (a scene beyond the engine's LDS tables runs the BIG instantiation: teams of 8 or 64)
             const bool big = coop_big(ss);
             uint32_t team = big && ss->coop_team != 64u ? 8u : ss->coop_team;
             for (;;) {
-                // the next stage: teams of 8 -> (coop_grow_mid) teams of 32 -> (coop_grow) whole waves
+                // the next stage: teams of 4 or 8 -> (coop_grow_mid, from 8) teams of 32 -> (coop_grow) whole waves
                 uint32_t keep = 0u, next_team = 64u;
                 if (team == 8u && !big && ss->coop_grow_mid > ss->coop_grow && chains > ss->coop_grow_mid) {
                     keep = ss->coop_grow_mid;

@@ -239,7 +239,7 @@ int pt_session_create(pt_scene* s, const pt_session_opts* o, pt_session** out) {
         // tree too deep for the teams-of-32 stack skips it)
         ss->coop_grow_mid = (uint32_t)std::max(0, tune_int("coop_grow_mid", 0));
         if (192u < reserve + 64u || s->max_stack > 192u) ss->coop_grow_mid = 0u;
-        // Early cooperative launch (teams of 8, QC_WAVES waves per workgroup: 32 chains each):
+        // Early cooperative launch (teams of side_team lanes, QC_WAVES waves per workgroup):
         // the low-chain rounds leave each CU room for one more workgroup, which the heaviest
         // chains use from then on instead of waiting for the final hand-over
         ss->early_wg = (uint32_t)std::max(1, tune_int("early_wg", 1));

@@ -484,7 +484,7 @@ TUNE_KEYS = ["wg_per_cu=2", "wg_per_cu=1", "runend=1000000", "sparse_steps=2", "
              "coop=300,early=1,early_at=100000000,side_late=1",
              "coop=300,early=1,early_at=100000000,side_prio=0", "coop=300,early=1,early_at=100000000,side_prio=2",
              "coop=300,early=1,early_at=100000000,side_team=16", "coop=300,early=1,early_at=100000000,side_team=8",
-             "coop=300,coop_team=4",
+             "coop=300,coop_team=8",
              # diagnostics hooks (their counters are compiled in only with -DPT_CPROF / -DPT_WPROF;
              # the host side runs in every build)
              "coop=300,cprof=1", "wgprof=/tmp/pt_wgprof_test.bin"]
@@ -570,10 +570,10 @@ HANDOFF_FORCE = {
 
 
 # every site with the defaults, the early launch's sites also with teams of 8 (the default is 4)
-# and the final launch's with teams of 4 (the default is 8)
+# and the final launch's also with teams of 8 (the default is 4)
 HANDOFF_CASES = [(k, "") for k in sorted(HANDOFF_FORCE)] + \
     [(k, ",side_team=8") for k in sorted(HANDOFF_FORCE) if k.startswith("side_")] + \
-    [(k, ",coop_team=4") for k in sorted(HANDOFF_FORCE) if k.startswith("grow_")]
+    [(k, ",coop_team=8") for k in sorted(HANDOFF_FORCE) if k.startswith("grow_")]
 
 
 @pytest.mark.parametrize("site,team", HANDOFF_CASES)
